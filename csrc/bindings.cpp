@@ -1,0 +1,74 @@
+// Python bindings for the penroz CDNA4 kernels (module ``penroz_kernels``).
+#include <torch/extension.h>
+
+// layernorm.hip
+void layernorm_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor b, double eps, torch::Tensor y, torch::Tensor mean,
+                   torch::Tensor rstd);
+void add_layernorm_fwd(torch::Tensor resid_in, torch::Tensor delta, torch::Tensor resid_out, torch::Tensor w,
+                       torch::Tensor b, double eps, torch::Tensor y, torch::Tensor mean, torch::Tensor rstd);
+void layernorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor mean, torch::Tensor rstd, torch::Tensor w,
+                   torch::Tensor dresid, bool accumulate, c10::optional<torch::Tensor> dresid_bf, torch::Tensor dw,
+                   torch::Tensor db, c10::optional<torch::Tensor> dbias_prev);
+// rmsnorm.hip
+std::vector<torch::Tensor> rmsnorm_fwd(torch::Tensor x, torch::Tensor w, double eps);
+std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor w, torch::Tensor rstd);
+// elementwise.hip
+void gelu_fwd(torch::Tensor x, int64_t approx, torch::Tensor y);
+void gelu_bwd(torch::Tensor dy, torch::Tensor x, int64_t approx, c10::optional<torch::Tensor> dbias, torch::Tensor out);
+void colsum(torch::Tensor x, torch::Tensor out);
+torch::Tensor gated_act_fwd(torch::Tensor g, torch::Tensor u, int64_t kind);
+std::vector<torch::Tensor> gated_act_bwd(torch::Tensor dy, torch::Tensor g, torch::Tensor u, int64_t kind);
+void embedding_fwd(torch::Tensor idx, torch::Tensor wte, torch::Tensor wpe, int64_t off, torch::Tensor out);
+void embedding_bwd(torch::Tensor dout, torch::Tensor idx, torch::Tensor dwte, torch::Tensor dwpe, int64_t off);
+torch::Tensor rope_qkv(torch::Tensor qkv, torch::Tensor cosv, torch::Tensor sinv, int64_t H, int64_t Hkv, int64_t D,
+                       bool inverse);
+void kv_quantize(torch::Tensor x, torch::Tensor q, torch::Tensor scale, int64_t pos);
+std::vector<torch::Tensor> tensor_stats(torch::Tensor x, int64_t bins);
+// cross_entropy.hip
+torch::Tensor cross_entropy_fwd_bwd(torch::Tensor logits, torch::Tensor targets, double scale, int64_t ignore_index);
+// adamw.hip
+void adamw_step(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, c10::optional<torch::Tensor> shadow,
+                double lr, double b1, double b2, double eps, double wd, int64_t step, double grad_scale, bool maximize);
+void adam_step(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, c10::optional<torch::Tensor> shadow,
+               double lr, double b1, double b2, double eps, double wd, int64_t step, double grad_scale, bool maximize);
+void multi_tensor_adam(std::vector<torch::Tensor> ps, std::vector<torch::Tensor> gs, std::vector<torch::Tensor> ms,
+                       std::vector<torch::Tensor> vs, double lr, double b1, double b2, double eps, double wd,
+                       int64_t step, double grad_scale, bool maximize, bool decoupled);
+// sampling.hip
+torch::Tensor sample_tokens(torch::Tensor logits, c10::optional<torch::Tensor> uniform, double temperature,
+                            int64_t top_k);
+// decode_attn.hip
+torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c10::optional<torch::Tensor> k_scale,
+                          c10::optional<torch::Tensor> v_scale, int64_t S, int64_t q_offset, double scale);
+// flash_attn.hip
+void flash_attn_fwd(torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int64_t H, int64_t Hkv, int64_t D,
+                    double scale, double p_drop, int64_t seed);
+void flash_attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, torch::Tensor dqkv,
+                    int64_t H, int64_t Hkv, int64_t D, double scale, double p_drop, int64_t seed);
+
+PYBIND11_MODULE(penroz_kernels, m) {
+  m.doc() = "penroz hand-written HIP kernels for MI355X (gfx950)";
+  m.def("layernorm_fwd", &layernorm_fwd);
+  m.def("add_layernorm_fwd", &add_layernorm_fwd);
+  m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("rmsnorm_fwd", &rmsnorm_fwd);
+  m.def("rmsnorm_bwd", &rmsnorm_bwd);
+  m.def("gelu_fwd", &gelu_fwd);
+  m.def("gelu_bwd", &gelu_bwd);
+  m.def("colsum", &colsum);
+  m.def("gated_act_fwd", &gated_act_fwd);
+  m.def("gated_act_bwd", &gated_act_bwd);
+  m.def("embedding_fwd", &embedding_fwd);
+  m.def("embedding_bwd", &embedding_bwd);
+  m.def("rope_qkv", &rope_qkv);
+  m.def("kv_quantize", &kv_quantize);
+  m.def("tensor_stats", &tensor_stats);
+  m.def("cross_entropy_fwd_bwd", &cross_entropy_fwd_bwd);
+  m.def("adamw_step", &adamw_step);
+  m.def("adam_step", &adam_step);
+  m.def("multi_tensor_adam", &multi_tensor_adam);
+  m.def("sample_tokens", &sample_tokens);
+  m.def("decode_attn", &decode_attn);
+  m.def("flash_attn_fwd", &flash_attn_fwd);
+  m.def("flash_attn_bwd", &flash_attn_bwd);
+}

@@ -1,0 +1,131 @@
+// Shared device helpers for the penroz CDNA4 (gfx950) kernels.
+//
+// Conventions: wave64 everywhere (lane = threadIdx.x & 63), 16-byte vector memory access for
+// every bf16/fp32 stream (Guideline 13 of the CDNA HIP guide), fp32 math internally, bf16
+// rounding to nearest-even via the compiler's native conversion (v_cvt_pk_bf16_f32 on gfx950).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <hip/hip_fp16.h>
+#include <stdint.h>
+
+namespace penroz {
+
+constexpr int kWave = 64;
+
+using bf16 = __hip_bfloat16;
+typedef float float4_t __attribute__((ext_vector_type(4)));
+typedef short short8_t __attribute__((ext_vector_type(8)));
+typedef short short4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float bf2f(uint16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
+__device__ __forceinline__ float bf2f(bf16 v) { return __bfloat162float(v); }
+
+// fp32 -> bf16 bits, round to nearest even (NaN stays NaN through the native cvt).
+__device__ __forceinline__ uint16_t f2bf_bits(float f) {
+  bf16 b = __float2bfloat16(f);
+  return *reinterpret_cast<uint16_t*>(&b);
+}
+
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  return (uint32_t)f2bf_bits(lo) | ((uint32_t)f2bf_bits(hi) << 16);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Load 8 consecutive elements (16 B for bf16, 32 B for fp32) as floats.
+template <typename T> struct Vec8;
+template <> struct Vec8<float> {
+  __device__ __forceinline__ static void load(const float* p, float (&v)[8]) {
+    float4_t a = *reinterpret_cast<const float4_t*>(p);
+    float4_t b = *reinterpret_cast<const float4_t*>(p + 4);
+    v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+    v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+  }
+  __device__ __forceinline__ static void store(float* p, const float (&v)[8]) {
+    *reinterpret_cast<float4_t*>(p) = float4_t{v[0], v[1], v[2], v[3]};
+    *reinterpret_cast<float4_t*>(p + 4) = float4_t{v[4], v[5], v[6], v[7]};
+  }
+};
+template <> struct Vec8<bf16> {
+  __device__ __forceinline__ static void load(const bf16* p, float (&v)[8]) {
+    uint4 u = *reinterpret_cast<const uint4*>(p);
+    uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(w[i] << 16);
+      v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
+  __device__ __forceinline__ static void store(bf16* p, const float (&v)[8]) {
+    uint4 u;
+    u.x = pack_bf16x2(v[0], v[1]);
+    u.y = pack_bf16x2(v[2], v[3]);
+    u.z = pack_bf16x2(v[4], v[5]);
+    u.w = pack_bf16x2(v[6], v[7]);
+    *reinterpret_cast<uint4*>(p) = u;
+  }
+};
+template <> struct Vec8<__half> {
+  __device__ __forceinline__ static void load(const __half* p, float (&v)[8]) {
+    const __half2* h = reinterpret_cast<const __half2*>(p);
+    uint4 u = *reinterpret_cast<const uint4*>(p);
+    const __half2* hh = reinterpret_cast<const __half2*>(&u);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float2 f = __half22float2(hh[i]);
+      v[2 * i] = f.x;
+      v[2 * i + 1] = f.y;
+    }
+    (void)h;
+  }
+  __device__ __forceinline__ static void store(__half* p, const float (&v)[8]) {
+    uint4 u;
+    __half2* hh = reinterpret_cast<__half2*>(&u);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) hh[i] = __floats2half2_rn(v[2 * i], v[2 * i + 1]);
+    *reinterpret_cast<uint4*>(p) = u;
+  }
+};
+
+template <typename T> __device__ __forceinline__ float to_f(T v);
+template <> __device__ __forceinline__ float to_f<float>(float v) { return v; }
+template <> __device__ __forceinline__ float to_f<bf16>(bf16 v) { return __bfloat162float(v); }
+template <> __device__ __forceinline__ float to_f<__half>(__half v) { return __half2float(v); }
+
+template <typename T> __device__ __forceinline__ T from_f(float v);
+template <> __device__ __forceinline__ float from_f<float>(float v) { return v; }
+template <> __device__ __forceinline__ bf16 from_f<bf16>(float v) { return __float2bfloat16(v); }
+template <> __device__ __forceinline__ __half from_f<__half>(float v) { return __float2half(v); }
+
+// Counter-based RNG (splitmix/murmur finalizer) -> uniform in [0, 1).
+__device__ __forceinline__ uint32_t hash_u32(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return (uint32_t)x;
+}
+__device__ __forceinline__ float uniform01(uint64_t seed, uint64_t counter) {
+  return (hash_u32(seed * 0x9E3779B97F4A7C15ULL + counter) >> 8) * (1.0f / 16777216.0f);
+}
+
+}  // namespace penroz

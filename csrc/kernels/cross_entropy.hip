@@ -1,0 +1,158 @@
+// Fused cross-entropy forward + backward over bf16 logits, gradient written in place.
+//
+// One 1024-thread workgroup (16 waves) per row. The row (V bf16, e.g. 50304 × 2 B = 98 KiB)
+// is read ONCE into registers — 8 elements (16 B) per chunk, CPT chunks per thread, chunk k of
+// thread t covers elements 8·(t + 1024·k) — i.e. ≤ 28 VGPRs of packed bf16 per lane at GPT-2's
+// vocabulary. The register file (512 KiB/CU) holds two rows per CU at once, more than LDS
+// (160 KiB) could. max → Σexp → log-sum-exp are block reductions; the loss needs only the
+// target logit; the gradient (softmax − onehot)·scale is rounded to bf16 and stored over the
+// logits, so the lm_head backward GEMM reads it directly: one HBM read + one write per row,
+// no fp32 logits (the reference's autocast CE materialises fp32 log-softmax of [B·T, V]).
+// Rows with target == ignore_index contribute 0 loss and 0 gradient.
+#include "common.h"
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+
+namespace penroz {
+
+constexpr int kCEThreads = 1024;
+
+__device__ __forceinline__ float block_reduce(float v, float* sh, bool is_max) {
+  v = is_max ? wave_max(v) : wave_sum(v);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) sh[w] = v;
+  __syncthreads();
+  float r = lane < (kCEThreads / 64) ? sh[lane] : (is_max ? -INFINITY : 0.f);
+  r = is_max ? wave_max(r) : wave_sum(r);
+  return r;
+}
+
+template <int CPT, typename T>
+__global__ void __launch_bounds__(kCEThreads) ce_kernel(T* __restrict__ logits, const int64_t* __restrict__ targets,
+                                                        float* __restrict__ loss, int V, float scale,
+                                                        int64_t ignore_index) {
+  __shared__ float sh[16];
+  const int row = blockIdx.x;
+  T* rp = logits + (size_t)row * V;
+  const int64_t tgt = targets[row];
+  const int t = threadIdx.x;
+  float v[CPT][8];
+  float m = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    const int c = 8 * (t + kCEThreads * k);
+    if (c < V) {
+      Vec8<T>::load(rp + c, v[k]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m = fmaxf(m, v[k][j]);
+    }
+  }
+  m = block_reduce(m, sh, true);
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    const int c = 8 * (t + kCEThreads * k);
+    if (c < V) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += __expf(v[k][j] - m);
+    }
+  }
+  s = block_reduce(s, sh, false);
+  const float lse = m + __logf(s);
+  const bool valid = tgt != ignore_index && tgt >= 0 && tgt < V;
+  if (t == 0) loss[row] = valid ? lse - to_f(rp[tgt]) : 0.f;
+  if (scale == 0.f) return;
+  const float sc = valid ? scale : 0.f;
+  __syncthreads();  // the target logit is read before any thread overwrites it
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    const int c = 8 * (t + kCEThreads * k);
+    if (c < V) {
+      float g[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = (__expf(v[k][j] - lse) - (c + j == tgt ? 1.f : 0.f)) * sc;
+      Vec8<T>::store(rp + c, g);
+    }
+  }
+}
+
+// Any-V fallback (V % 8 == 0): three streamed passes through L2.
+template <typename T>
+__global__ void __launch_bounds__(kCEThreads) ce_loop_kernel(T* __restrict__ logits,
+                                                             const int64_t* __restrict__ targets,
+                                                             float* __restrict__ loss, int V, float scale,
+                                                             int64_t ignore_index) {
+  __shared__ float sh[16];
+  const int row = blockIdx.x;
+  T* rp = logits + (size_t)row * V;
+  const int64_t tgt = targets[row];
+  float m = -INFINITY;
+  for (int c = 8 * threadIdx.x; c < V; c += 8 * kCEThreads) {
+    float v[8];
+    Vec8<T>::load(rp + c, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = fmaxf(m, v[j]);
+  }
+  m = block_reduce(m, sh, true);
+  float s = 0.f;
+  for (int c = 8 * threadIdx.x; c < V; c += 8 * kCEThreads) {
+    float v[8];
+    Vec8<T>::load(rp + c, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += __expf(v[j] - m);
+  }
+  s = block_reduce(s, sh, false);
+  const float lse = m + __logf(s);
+  const bool valid = tgt != ignore_index && tgt >= 0 && tgt < V;
+  if (threadIdx.x == 0) loss[row] = valid ? lse - to_f(rp[tgt]) : 0.f;
+  if (scale == 0.f) return;
+  const float sc = valid ? scale : 0.f;
+  __syncthreads();
+  for (int c = 8 * threadIdx.x; c < V; c += 8 * kCEThreads) {
+    float v[8];
+    Vec8<T>::load(rp + c, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (__expf(v[j] - lse) - (c + j == tgt ? 1.f : 0.f)) * sc;
+    Vec8<T>::store(rp + c, v);
+  }
+}
+
+}  // namespace penroz
+
+using namespace penroz;
+
+torch::Tensor cross_entropy_fwd_bwd(torch::Tensor logits, torch::Tensor targets, double scale, int64_t ignore_index) {
+  TORCH_CHECK(logits.is_cuda() && logits.is_contiguous() && logits.dim() == 2);
+  TORCH_CHECK(targets.scalar_type() == torch::kInt64 && targets.numel() == logits.size(0));
+  const int N = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(V % 8 == 0, "vocabulary must be a multiple of 8");
+  auto loss = torch::empty({N}, logits.options().dtype(torch::kFloat32));
+  if (N == 0) return loss;
+  auto tg = targets.contiguous();
+  auto stream = at::hip::getCurrentHIPStream();
+  const int chunks = (V / 8 + kCEThreads - 1) / kCEThreads;
+  auto launch = [&](auto tag) {
+    using T = decltype(tag);
+    T* lp = reinterpret_cast<T*>(logits.data_ptr());
+    const int64_t* tp = tg.data_ptr<int64_t>();
+    float* op = loss.data_ptr<float>();
+    const float sc = (float)scale;
+    switch (chunks) {
+      case 1: hipLaunchKernelGGL((ce_kernel<1, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, sc, ignore_index); break;
+      case 2: hipLaunchKernelGGL((ce_kernel<2, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, sc, ignore_index); break;
+      case 3: hipLaunchKernelGGL((ce_kernel<3, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, sc, ignore_index); break;
+      case 4: hipLaunchKernelGGL((ce_kernel<4, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, sc, ignore_index); break;
+      case 5: hipLaunchKernelGGL((ce_kernel<5, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, sc, ignore_index); break;
+      case 6: hipLaunchKernelGGL((ce_kernel<6, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, sc, ignore_index); break;
+      case 7: hipLaunchKernelGGL((ce_kernel<7, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, sc, ignore_index); break;
+      case 8: hipLaunchKernelGGL((ce_kernel<8, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, sc, ignore_index); break;
+      default: hipLaunchKernelGGL((ce_loop_kernel<T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, sc, ignore_index);
+    }
+  };
+  if (logits.scalar_type() == torch::kBFloat16) launch(bf16{});
+  else if (logits.scalar_type() == torch::kFloat32) launch(float{});
+  else if (logits.scalar_type() == torch::kFloat16) launch(__half{});
+  else TORCH_CHECK(false, "unsupported logits dtype");
+  return loss;
+}

@@ -1,0 +1,236 @@
+// KV-cache attention for incremental decoding (memory-bound: every cached K/V byte is read
+// once per step).
+//
+// Work item = (batch b, KV head g, query row tq, split s). One 256-thread workgroup owns all
+// H/Hkv query heads that share KV head g (GQA by index math — the cache is never expanded),
+// so each K/V row is loaded once for the whole group. The keys of a split are dealt to the
+// 4 waves in 64-key blocks:
+//   scores : lane j holds key (blk + j); its K row is read as 16-B vectors and dotted with the
+//            group's query vectors (staged in LDS, fp32);
+//   softmax: running (m, l) per query head, wave-wide max/sum, causal mask by absolute
+//            position (query tq sits at q_offset + tq);
+//   PV     : lane d owns output column d (and d+64 for D=128); V row j is read coalesced and
+//            p_j is broadcast with a lane shuffle.
+// int8 caches (TurboQuant) carry per-token fp32 scales that are folded into the score and
+// the P·V weight, so the int8 cache is never dequantised to memory.
+// The 4 waves merge through LDS; with several splits the partial (m, l, O) go to a workspace
+// and a second kernel combines them. Enough splits are used to put ≥ 512 workgroups in
+// flight (256 CUs) even at batch 1.
+#include "common.h"
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+
+namespace penroz {
+
+constexpr int kMaxGroup = 16;
+
+template <typename TK> struct KRow;
+template <> struct KRow<bf16> {
+  __device__ __forceinline__ static float at(const bf16* p, int d) { return bf2f(p[d]); }
+};
+template <> struct KRow<__half> {
+  __device__ __forceinline__ static float at(const __half* p, int d) { return __half2float(p[d]); }
+};
+template <> struct KRow<float> {
+  __device__ __forceinline__ static float at(const float* p, int d) { return p[d]; }
+};
+template <> struct KRow<int8_t> {
+  __device__ __forceinline__ static float at(const int8_t* p, int d) { return (float)p[d]; }
+};
+
+template <int D, typename TQ, typename TK>
+__global__ void __launch_bounds__(256) decode_kernel(const TQ* __restrict__ q, const TK* __restrict__ kc,
+                                                     const TK* __restrict__ vc, const float* __restrict__ ks,
+                                                     const float* __restrict__ vs, TQ* __restrict__ out,
+                                                     float* __restrict__ ws_o, float* __restrict__ ws_ml, int B,
+                                                     int Tq, int H, int Hkv, int cap, int S, int q_offset,
+                                                     int splits, float scale) {
+  constexpr int DL = D / 64;  // output columns per lane
+  const int G = H / Hkv;
+  int wid_lin = blockIdx.x;
+  const int split = wid_lin % splits;
+  wid_lin /= splits;
+  const int tq = wid_lin % Tq;
+  wid_lin /= Tq;
+  const int g = wid_lin % Hkv;
+  const int b = wid_lin / Hkv;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+
+  __shared__ float qs[kMaxGroup][D];
+  __shared__ float red_m[4][kMaxGroup], red_l[4][kMaxGroup];
+  __shared__ float red_o[4][kMaxGroup][D];
+
+  for (int i = threadIdx.x; i < G * D; i += 256) {
+    const int h = g * G + i / D, d = i % D;
+    qs[i / D][d] = to_f(q[(((size_t)b * Tq + tq) * H + h) * D + d]) * scale;
+  }
+  __syncthreads();
+
+  const int kend_causal = min(S, q_offset + tq + 1);
+  const int per_split = (kend_causal + splits - 1) / splits;
+  const int k0 = split * per_split, k1 = min(kend_causal, k0 + per_split);
+  const size_t head_base = ((size_t)b * Hkv + g) * cap;
+
+  float m[kMaxGroup], l[kMaxGroup], o[kMaxGroup][DL];
+#pragma unroll
+  for (int i = 0; i < kMaxGroup; ++i) {
+    m[i] = -INFINITY;
+    l[i] = 0.f;
+#pragma unroll
+    for (int j = 0; j < DL; ++j) o[i][j] = 0.f;
+  }
+
+  for (int blk = k0 + 64 * wid; blk < k1; blk += 256) {
+    const int key = blk + lane;
+    const bool valid = key < k1;
+    float kv[D];
+    const TK* krow = kc + (head_base + (valid ? key : k0)) * D;
+#pragma unroll
+    for (int d = 0; d < D; ++d) kv[d] = KRow<TK>::at(krow, d);
+    const float kscale = ks ? ks[head_base + (valid ? key : k0)] : 1.f;
+    float p[kMaxGroup];
+#pragma unroll
+    for (int i = 0; i < kMaxGroup; ++i) {
+      if (i >= G) break;
+      float s = 0.f;
+#pragma unroll
+      for (int d = 0; d < D; ++d) s += qs[i][d] * kv[d];
+      s = valid ? s * kscale : -INFINITY;
+      const float mn = fmaxf(m[i], wave_max(s));
+      const float alpha = __expf(m[i] - mn);
+      p[i] = valid ? __expf(s - mn) : 0.f;
+      l[i] = l[i] * alpha + wave_sum(p[i]);
+      m[i] = mn;
+#pragma unroll
+      for (int j = 0; j < DL; ++j) o[i][j] *= alpha;
+    }
+    const int nk = min(64, k1 - blk);
+    for (int j = 0; j < nk; ++j) {
+      const TK* vrow = vc + (head_base + blk + j) * D;
+      const float vsc = vs ? vs[head_base + blk + j] : 1.f;
+      float vv[DL];
+#pragma unroll
+      for (int jj = 0; jj < DL; ++jj) vv[jj] = KRow<TK>::at(vrow, lane + 64 * jj) * vsc;
+#pragma unroll
+      for (int i = 0; i < kMaxGroup; ++i) {
+        if (i >= G) break;
+        const float pj = __shfl(p[i], j, 64);
+#pragma unroll
+        for (int jj = 0; jj < DL; ++jj) o[i][jj] += pj * vv[jj];
+      }
+    }
+  }
+  // merge the 4 waves
+  for (int i = 0; i < G; ++i) {
+    if (lane == 0) { red_m[wid][i] = m[i]; red_l[wid][i] = l[i]; }
+#pragma unroll
+    for (int jj = 0; jj < DL; ++jj) red_o[wid][i][lane + 64 * jj] = o[i][jj];
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < G * D; idx += 256) {
+    const int i = idx / D, d = idx % D;
+    float M = -INFINITY;
+    for (int w = 0; w < 4; ++w) M = fmaxf(M, red_m[w][i]);
+    float L = 0.f, O = 0.f;
+    for (int w = 0; w < 4; ++w) {
+      const float f = red_m[w][i] == -INFINITY ? 0.f : __expf(red_m[w][i] - M);
+      L += red_l[w][i] * f;
+      O += red_o[w][i][d] * f;
+    }
+    const int h = g * G + i;
+    if (splits == 1) {
+      out[(((size_t)b * Tq + tq) * H + h) * D + d] = from_f<TQ>(L > 0.f ? O / L : 0.f);
+    } else {
+      const size_t r = (((size_t)split * B + b) * Tq + tq) * H + h;
+      ws_o[r * D + d] = O;
+      if (d == 0) {
+        ws_ml[2 * r] = M;
+        ws_ml[2 * r + 1] = L;
+      }
+    }
+  }
+}
+
+template <typename TQ>
+__global__ void __launch_bounds__(256) decode_combine_kernel(const float* __restrict__ ws_o,
+                                                             const float* __restrict__ ws_ml, TQ* __restrict__ out,
+                                                             int rows, int D, int splits) {
+  const int64_t total = (int64_t)rows * D;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / D;
+    const int d = (int)(i - r * D);
+    float M = -INFINITY;
+    for (int s = 0; s < splits; ++s) M = fmaxf(M, ws_ml[2 * ((int64_t)s * rows + r)]);
+    float L = 0.f, O = 0.f;
+    for (int s = 0; s < splits; ++s) {
+      const int64_t rr = (int64_t)s * rows + r;
+      const float ms = ws_ml[2 * rr];
+      const float f = ms == -INFINITY ? 0.f : __expf(ms - M);
+      L += ws_ml[2 * rr + 1] * f;
+      O += ws_o[rr * D + d] * f;
+    }
+    out[i] = from_f<TQ>(L > 0.f ? O / L : 0.f);
+  }
+}
+
+}  // namespace penroz
+
+using namespace penroz;
+
+torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c10::optional<torch::Tensor> k_scale,
+                          c10::optional<torch::Tensor> v_scale, int64_t S, int64_t q_offset, double scale) {
+  TORCH_CHECK(q.is_cuda() && q.is_contiguous() && q.dim() == 4, "q must be [B, Tq, H, D]");
+  TORCH_CHECK(kc.is_contiguous() && vc.is_contiguous() && kc.dim() == 4 && kc.sizes() == vc.sizes());
+  const int B = q.size(0), Tq = q.size(1), H = q.size(2), D = q.size(3);
+  const int Hkv = kc.size(1), cap = kc.size(2);
+  TORCH_CHECK(kc.size(0) == B && kc.size(3) == D && H % Hkv == 0 && H / Hkv <= kMaxGroup);
+  TORCH_CHECK(S <= cap && q_offset >= 0 && q_offset + Tq <= S, "bad cache extent");
+  TORCH_CHECK(D == 64 || D == 128, "decode attention supports head_dim 64/128");
+  const bool quant = kc.scalar_type() == torch::kInt8;
+  TORCH_CHECK(!quant || (k_scale.has_value() && v_scale.has_value()), "int8 cache needs scales");
+  TORCH_CHECK(quant || kc.scalar_type() == q.scalar_type(), "cache dtype must match q");
+  auto out = torch::empty({B, Tq, H * D}, q.options());
+  const int items = B * Hkv * Tq;
+  int splits = std::max(1, std::min<int>((512 + items - 1) / items, (int)((S + 255) / 256)));
+  torch::Tensor ws_o, ws_ml;
+  float* wo = nullptr;
+  float* wm = nullptr;
+  if (splits > 1) {
+    ws_o = torch::empty({(int64_t)splits * B * Tq * H * D}, q.options().dtype(torch::kFloat32));
+    ws_ml = torch::empty({(int64_t)splits * B * Tq * H * 2}, q.options().dtype(torch::kFloat32));
+    wo = ws_o.data_ptr<float>();
+    wm = ws_ml.data_ptr<float>();
+  }
+  const float* ksp = quant ? k_scale->data_ptr<float>() : nullptr;
+  const float* vsp = quant ? v_scale->data_ptr<float>() : nullptr;
+  auto stream = at::hip::getCurrentHIPStream();
+  dim3 grid(items * splits);
+  auto launch = [&](auto qtag, auto ktag) {
+    using TQ = decltype(qtag);
+    using TK = decltype(ktag);
+    const TQ* qp = reinterpret_cast<const TQ*>(q.data_ptr());
+    const TK* kp = reinterpret_cast<const TK*>(kc.data_ptr());
+    const TK* vp = reinterpret_cast<const TK*>(vc.data_ptr());
+    TQ* op = reinterpret_cast<TQ*>(out.data_ptr());
+    if (D == 64)
+      hipLaunchKernelGGL((decode_kernel<64, TQ, TK>), grid, dim3(256), 0, stream, qp, kp, vp, ksp, vsp, op, wo, wm, B,
+                         Tq, H, Hkv, cap, (int)S, (int)q_offset, splits, (float)scale);
+    else
+      hipLaunchKernelGGL((decode_kernel<128, TQ, TK>), grid, dim3(256), 0, stream, qp, kp, vp, ksp, vsp, op, wo, wm, B,
+                         Tq, H, Hkv, cap, (int)S, (int)q_offset, splits, (float)scale);
+    if (splits > 1) {
+      const int rows = B * Tq * H;
+      hipLaunchKernelGGL(decode_combine_kernel<TQ>, dim3(std::min(2048, (rows * D + 255) / 256)), dim3(256), 0, stream,
+                         wo, wm, op, rows, D, splits);
+    }
+  };
+  auto with_k = [&](auto qtag) {
+    if (quant) launch(qtag, int8_t{});
+    else launch(qtag, qtag);
+  };
+  if (q.scalar_type() == torch::kBFloat16) with_k(bf16{});
+  else if (q.scalar_type() == torch::kFloat32) with_k(float{});
+  else if (q.scalar_type() == torch::kFloat16) with_k(__half{});
+  else TORCH_CHECK(false, "unsupported q dtype");
+  return out;
+}

@@ -1,0 +1,520 @@
+// Memory-bound kernels: GELU fwd/bwd (+ fused bias-gradient column sum), gated-MLP
+// activation, column sums, token+position embedding fwd/bwd, RoPE on fused QKV, int8 KV
+// quantisation, and on-device tensor statistics (moments, min/max, density histogram).
+//
+// All streams use 16-B per-lane vectors (8 bf16 or 4 fp32), grid-stride loops capped at
+// ~2048 workgroups (CDNA HIP guide, Guideline 11/13). Column-sum fusions keep each thread's
+// 8 columns fixed while it walks rows, so the partial sums live in registers; a workgroup
+// reduces its 4 waves in LDS and writes one partial row, finished by a tiny reduction.
+#include "common.h"
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+
+namespace penroz {
+
+// ------------------------------------------------------------------------------ GELU math
+__device__ __forceinline__ float gelu_f(float x, int approx) {
+  if (approx) {
+    const float k = 0.7978845608028654f;
+    const float t = tanhf(k * (x + 0.044715f * x * x * x));
+    return 0.5f * x * (1.f + t);
+  }
+  return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));
+}
+
+__device__ __forceinline__ float gelu_grad_f(float x, int approx) {
+  if (approx) {
+    const float k = 0.7978845608028654f;
+    const float x2 = x * x;
+    const float t = tanhf(k * (x + 0.044715f * x2 * x));
+    return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k * (1.f + 3.f * 0.044715f * x2);
+  }
+  const float cdf = 0.5f * (1.f + erff(x * 0.7071067811865476f));
+  const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+__device__ __forceinline__ float act_f(float x, int kind) {  // 0 gelu, 1 gelu_tanh, 2 silu
+  if (kind == 2) return x / (1.f + __expf(-x));
+  return gelu_f(x, kind);
+}
+__device__ __forceinline__ float act_grad_f(float x, int kind) {
+  if (kind == 2) {
+    const float s = 1.f / (1.f + __expf(-x));
+    return s * (1.f + x * (1.f - s));
+  }
+  return gelu_grad_f(x, kind);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) gelu_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t n8,
+                                                       int approx) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    float v[8];
+    Vec8<T>::load(x + 8 * i, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = gelu_f(v[k], approx);
+    Vec8<T>::store(y + 8 * i, v);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) gelu_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                       T* __restrict__ dx, int64_t n8, int approx) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    float g[8], v[8];
+    Vec8<T>::load(dy + 8 * i, g);
+    Vec8<T>::load(x + 8 * i, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g[k] *= gelu_grad_f(v[k], approx);
+    Vec8<T>::store(dx + 8 * i, g);
+  }
+}
+
+// MODE 0: colsum of x.  MODE 1: dx = dy*gelu'(x) written to out, colsum of dx.
+// grid = (F/512 column tiles, R row splits); block 256 = 4 waves; lane -> 8 columns.
+template <int MODE, typename T>
+__global__ void __launch_bounds__(256) rows_colsum_kernel(const T* __restrict__ a, const T* __restrict__ x,
+                                                          T* __restrict__ out, float* __restrict__ part, int N, int F,
+                                                          int approx) {
+  __shared__ float red[4][512];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int col = blockIdx.x * 512 + 8 * lane;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const bool active = col < F;
+  const int R = gridDim.y;
+  const int rows_per = (N + R - 1) / R;
+  const int r0 = blockIdx.y * rows_per, r1 = min(N, r0 + rows_per);
+  if (active) {
+    for (int r = r0 + wid; r < r1; r += 4) {
+      const size_t off = (size_t)r * F + col;
+      float v[8];
+      Vec8<T>::load(a + off, v);
+      if constexpr (MODE == 1) {
+        float xv[8];
+        Vec8<T>::load(x + off, xv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] *= gelu_grad_f(xv[k], approx);
+        Vec8<T>::store(out + off, v);
+        // accumulate the *rounded* value so dbias matches the bf16 gradient the GEMMs see
+        Vec8<T>::load(out + off, v);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += v[k];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[wid][8 * lane + k] = acc[k];
+  __syncthreads();
+  for (int c = threadIdx.x; c < 512; c += 256) {
+    const int gc = blockIdx.x * 512 + c;
+    if (gc < F) part[(size_t)blockIdx.y * F + gc] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+  }
+}
+
+__global__ void __launch_bounds__(256) finish_colsum_kernel(const float* __restrict__ part, int R, int F,
+                                                            float* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= F) return;
+  float s = 0.f;
+  for (int r = 0; r < R; ++r) s += part[(size_t)r * F + c];
+  out[c] += s;
+}
+
+// ------------------------------------------------------------------------------ gated MLP act
+template <typename T>
+__global__ void __launch_bounds__(256) gated_fwd_kernel(const T* __restrict__ g, const T* __restrict__ u,
+                                                        T* __restrict__ y, int64_t n8, int kind) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    float gv[8], uv[8];
+    Vec8<T>::load(g + 8 * i, gv);
+    Vec8<T>::load(u + 8 * i, uv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) gv[k] = act_f(gv[k], kind) * uv[k];
+    Vec8<T>::store(y + 8 * i, gv);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) gated_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ g,
+                                                        const T* __restrict__ u, T* __restrict__ dg,
+                                                        T* __restrict__ du, int64_t n8, int kind) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    float d[8], gv[8], uv[8], o1[8], o2[8];
+    Vec8<T>::load(dy + 8 * i, d);
+    Vec8<T>::load(g + 8 * i, gv);
+    Vec8<T>::load(u + 8 * i, uv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      o1[k] = d[k] * uv[k] * act_grad_f(gv[k], kind);
+      o2[k] = d[k] * act_f(gv[k], kind);
+    }
+    Vec8<T>::store(dg + 8 * i, o1);
+    Vec8<T>::store(du + 8 * i, o2);
+  }
+}
+
+// ------------------------------------------------------------------------------ embedding
+// out[n, :] = wte[idx[n], :] + wpe[off + n % T, :]   (one wave per token row, 16-B lanes)
+template <typename TW>
+__global__ void __launch_bounds__(256) embed_fwd_kernel(const int64_t* __restrict__ idx, const TW* __restrict__ wte,
+                                                        const TW* __restrict__ wpe, float* __restrict__ out, int N,
+                                                        int T, int C, int off, int V) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= N) return;
+  int64_t tok = idx[row];
+  tok = tok < 0 ? 0 : (tok >= V ? V - 1 : tok);
+  const int pos = off + row % T;
+  for (int c = 8 * lane; c < C; c += 512) {
+    float a[8], b[8];
+    Vec8<TW>::load(wte + (size_t)tok * C + c, a);
+    Vec8<TW>::load(wpe + (size_t)pos * C + c, b);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] += b[k];
+    Vec8<float>::store(out + (size_t)row * C + c, a);
+  }
+}
+
+// dwte[idx[n]] += dout[n]  (fp32 atomics; each wave instruction = 256 contiguous bytes)
+__global__ void __launch_bounds__(256) embed_bwd_tok_kernel(const float* __restrict__ dout,
+                                                            const int64_t* __restrict__ idx,
+                                                            float* __restrict__ dwte, int N, int C, int V) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= N) return;
+  const int64_t tok = idx[row];
+  if (tok < 0 || tok >= V) return;
+  float* dst = dwte + (size_t)tok * C;
+  const float* src = dout + (size_t)row * C;
+  for (int c = lane; c < C; c += 64) atomicAdd(dst + c, src[c]);
+}
+
+// dwpe[off + t] += Σ_b dout[b*T + t]   (one workgroup per position, no atomics)
+__global__ void __launch_bounds__(256) embed_bwd_pos_kernel(const float* __restrict__ dout, float* __restrict__ dwpe,
+                                                            int B, int T, int C, int off) {
+  const int t = blockIdx.x;
+  for (int c = threadIdx.x * 4; c < C; c += 1024) {
+    float4_t s = {0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < B; ++b) s += *reinterpret_cast<const float4_t*>(dout + ((size_t)b * T + t) * C + c);
+    float4_t* d = reinterpret_cast<float4_t*>(dwpe + (size_t)(off + t) * C + c);
+    *d = *d + s;
+  }
+}
+
+// ------------------------------------------------------------------------------ RoPE
+// qkv [B*T, (H+2Hkv)*D]; rotate the first H+Hkv heads (Q and K); V copied. cos/sin [T, D/2].
+template <typename T>
+__global__ void __launch_bounds__(256) rope_kernel(const T* __restrict__ in, T* __restrict__ out,
+                                                   const float* __restrict__ cosv, const float* __restrict__ sinv,
+                                                   int64_t rows, int Tlen, int H, int Hkv, int D, int inverse) {
+  const int W = (H + 2 * Hkv) * D;
+  const int half = D / 2;
+  const int64_t total = rows * (int64_t)W;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / W;
+    const int c = (int)(i - r * W);
+    const int head = c / D;
+    const int d = c - head * D;
+    if (head >= H + Hkv) {
+      out[i] = in[i];
+      continue;
+    }
+    const int t = (int)(r % Tlen);
+    const int j = d < half ? d : d - half;
+    const float cs = cosv[(size_t)t * half + j];
+    float sn = sinv[(size_t)t * half + j];
+    if (inverse) sn = -sn;
+    const int64_t hb = r * W + (int64_t)head * D;
+    const float x1 = to_f(in[hb + j]), x2 = to_f(in[hb + j + half]);
+    const float o = d < half ? (x1 * cs - x2 * sn) : (x2 * cs + x1 * sn);
+    out[i] = from_f<T>(o);
+  }
+}
+
+// ------------------------------------------------------------------------------ int8 KV quant
+// x [B, T, Hkv, D] -> q [B, Hkv, cap, D] int8 at pos.., scale [B, Hkv, cap] f32 (absmax/127)
+template <typename T>
+__global__ void __launch_bounds__(256) kv_quant_kernel(const T* __restrict__ x, int8_t* __restrict__ q,
+                                                       float* __restrict__ scale, int Bn, int Tn, int Hkv, int D,
+                                                       int cap, int pos) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);  // over B*T*Hkv
+  if (row >= Bn * Tn * Hkv) return;
+  const int h = row % Hkv;
+  const int t = (row / Hkv) % Tn;
+  const int b = row / (Hkv * Tn);
+  const T* src = x + (size_t)row * D;
+  float m = 0.f;
+  for (int d = lane; d < D; d += 64) m = fmaxf(m, fabsf(to_f(src[d])));
+  m = wave_max(m);
+  float s = m / 127.f;
+  if (s == 0.f) s = 1.f;
+  const size_t slot = ((size_t)b * Hkv + h) * cap + pos + t;
+  for (int d = lane; d < D; d += 64) {
+    float v = rintf(to_f(src[d]) / s);
+    v = fminf(fmaxf(v, -128.f), 127.f);
+    q[slot * D + d] = (int8_t)v;
+  }
+  if (lane == 0) scale[slot] = s;
+}
+
+// ------------------------------------------------------------------------------ stats
+// pass 1: per-block (sum, min, max); pass 2: per-block Σ(x-mean)^2 + LDS histogram.
+template <typename T>
+__global__ void __launch_bounds__(256) stats_pass1_kernel(const T* __restrict__ x, int64_t n,
+                                                          float* __restrict__ part) {
+  __shared__ float red[3][4];
+  float s = 0.f, mn = INFINITY, mx = -INFINITY;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = to_f(x[i]);
+    s += v;
+    mn = fminf(mn, v);
+    mx = fmaxf(mx, v);
+  }
+  s = wave_sum(s);
+  mn = wave_min(mn);
+  mx = wave_max(mx);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { red[0][w] = s; red[1][w] = mn; red[2][w] = mx; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[blockIdx.x * 3 + 0] = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    part[blockIdx.x * 3 + 1] = fminf(fminf(red[1][0], red[1][1]), fminf(red[1][2], red[1][3]));
+    part[blockIdx.x * 3 + 2] = fmaxf(fmaxf(red[2][0], red[2][1]), fmaxf(red[2][2], red[2][3]));
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) stats_pass2_kernel(const T* __restrict__ x, int64_t n,
+                                                          const float* __restrict__ mmm,  // mean, lo, hi
+                                                          float* __restrict__ part, float* __restrict__ hist,
+                                                          int bins) {
+  extern __shared__ __attribute__((aligned(16))) float lh[];
+  __shared__ float red[4];
+  for (int b = threadIdx.x; b < bins; b += blockDim.x) lh[b] = 0.f;
+  __syncthreads();
+  const float mean = mmm[0], lo = mmm[1], hi = mmm[2];
+  const float inv = bins / (hi - lo);
+  float ss = 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = to_f(x[i]);
+    ss += (v - mean) * (v - mean);
+    int b = (int)((v - lo) * inv);
+    b = b < 0 ? 0 : (b >= bins ? bins - 1 : b);
+    atomicAdd(&lh[b], 1.f);
+  }
+  ss = wave_sum(ss);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  for (int b = threadIdx.x; b < bins; b += blockDim.x)
+    if (lh[b] != 0.f) atomicAdd(&hist[b], lh[b]);
+}
+
+}  // namespace penroz
+
+// ============================================================================ host side
+using namespace penroz;
+
+#define FOR_FLOAT_TYPES(t, NAME, ...)                                               \
+  if ((t) == torch::kFloat32) { using NAME = float; __VA_ARGS__; }                  \
+  else if ((t) == torch::kBFloat16) { using NAME = bf16; __VA_ARGS__; }             \
+  else if ((t) == torch::kFloat16) { using NAME = __half; __VA_ARGS__; }            \
+  else TORCH_CHECK(false, "unsupported dtype");
+
+static inline int grid_for(int64_t work, int block = 256, int cap = 2048) {
+  int64_t g = (work + block - 1) / block;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(g, cap));
+}
+
+static void check_vec8(const torch::Tensor& t) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "expected a contiguous GPU tensor");
+  TORCH_CHECK(t.numel() % 8 == 0, "element count must be a multiple of 8");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "tensor must be 16-byte aligned");
+}
+
+void gelu_fwd(torch::Tensor x, int64_t approx, torch::Tensor y) {
+  check_vec8(x);
+  check_vec8(y);
+  TORCH_CHECK(x.scalar_type() == y.scalar_type() && x.numel() == y.numel());
+  const int64_t n8 = x.numel() / 8;
+  auto stream = at::hip::getCurrentHIPStream();
+  FOR_FLOAT_TYPES(x.scalar_type(), T,
+    hipLaunchKernelGGL(gelu_fwd_kernel<T>, dim3(grid_for(n8)), dim3(256), 0, stream,
+                       reinterpret_cast<const T*>(x.data_ptr()), reinterpret_cast<T*>(y.data_ptr()), n8, (int)approx))
+}
+
+static void colsum_impl(const torch::Tensor& a, const torch::Tensor* x, torch::Tensor* out, torch::Tensor& dst,
+                        int approx, int mode) {
+  const int N = a.size(0), F = a.size(1);
+  TORCH_CHECK(F % 8 == 0, "column count must be a multiple of 8");
+  TORCH_CHECK(dst.scalar_type() == torch::kFloat32 && dst.numel() == F && dst.is_contiguous());
+  if (N == 0) return;
+  const int ctiles = (F + 511) / 512;
+  int R = std::max(1, std::min(N / 16, 2048 / ctiles));
+  auto part = torch::empty({R, F}, a.options().dtype(torch::kFloat32));
+  auto stream = at::hip::getCurrentHIPStream();
+  FOR_FLOAT_TYPES(a.scalar_type(), T, {
+    const T* ap = reinterpret_cast<const T*>(a.data_ptr());
+    const T* xp = x ? reinterpret_cast<const T*>(x->data_ptr()) : nullptr;
+    T* op = out ? reinterpret_cast<T*>(out->data_ptr()) : nullptr;
+    if (mode == 0)
+      hipLaunchKernelGGL((rows_colsum_kernel<0, T>), dim3(ctiles, R), dim3(256), 0, stream, ap, xp, op,
+                         part.data_ptr<float>(), N, F, approx);
+    else
+      hipLaunchKernelGGL((rows_colsum_kernel<1, T>), dim3(ctiles, R), dim3(256), 0, stream, ap, xp, op,
+                         part.data_ptr<float>(), N, F, approx);
+  })
+  hipLaunchKernelGGL(finish_colsum_kernel, dim3((F + 255) / 256), dim3(256), 0, stream, part.data_ptr<float>(), R, F,
+                     dst.data_ptr<float>());
+}
+
+void gelu_bwd(torch::Tensor dy, torch::Tensor x, int64_t approx, c10::optional<torch::Tensor> dbias,
+              torch::Tensor out) {
+  check_vec8(dy);
+  check_vec8(x);
+  check_vec8(out);
+  TORCH_CHECK(dy.scalar_type() == x.scalar_type() && out.scalar_type() == x.scalar_type());
+  TORCH_CHECK(dy.numel() == x.numel() && out.numel() == x.numel());
+  auto stream = at::hip::getCurrentHIPStream();
+  if (dbias.has_value() && dbias->defined()) {
+    TORCH_CHECK(x.dim() == 2, "fused bias gradient needs a 2-D input");
+    colsum_impl(dy, &x, &out, *dbias, (int)approx, 1);
+    return;
+  }
+  const int64_t n8 = x.numel() / 8;
+  FOR_FLOAT_TYPES(x.scalar_type(), T,
+    hipLaunchKernelGGL(gelu_bwd_kernel<T>, dim3(grid_for(n8)), dim3(256), 0, stream,
+                       reinterpret_cast<const T*>(dy.data_ptr()), reinterpret_cast<const T*>(x.data_ptr()),
+                       reinterpret_cast<T*>(out.data_ptr()), n8, (int)approx))
+}
+
+void colsum(torch::Tensor x, torch::Tensor out) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.dim() == 2);
+  colsum_impl(x, nullptr, nullptr, out, 0, 0);
+}
+
+torch::Tensor gated_act_fwd(torch::Tensor g, torch::Tensor u, int64_t kind) {
+  check_vec8(g);
+  check_vec8(u);
+  auto y = torch::empty_like(g);
+  const int64_t n8 = g.numel() / 8;
+  auto stream = at::hip::getCurrentHIPStream();
+  FOR_FLOAT_TYPES(g.scalar_type(), T,
+    hipLaunchKernelGGL(gated_fwd_kernel<T>, dim3(grid_for(n8)), dim3(256), 0, stream,
+                       reinterpret_cast<const T*>(g.data_ptr()), reinterpret_cast<const T*>(u.data_ptr()),
+                       reinterpret_cast<T*>(y.data_ptr()), n8, (int)kind))
+  return y;
+}
+
+std::vector<torch::Tensor> gated_act_bwd(torch::Tensor dy, torch::Tensor g, torch::Tensor u, int64_t kind) {
+  check_vec8(dy);
+  check_vec8(g);
+  check_vec8(u);
+  auto dg = torch::empty_like(g), du = torch::empty_like(u);
+  const int64_t n8 = g.numel() / 8;
+  auto stream = at::hip::getCurrentHIPStream();
+  FOR_FLOAT_TYPES(g.scalar_type(), T,
+    hipLaunchKernelGGL(gated_bwd_kernel<T>, dim3(grid_for(n8)), dim3(256), 0, stream,
+                       reinterpret_cast<const T*>(dy.data_ptr()), reinterpret_cast<const T*>(g.data_ptr()),
+                       reinterpret_cast<const T*>(u.data_ptr()), reinterpret_cast<T*>(dg.data_ptr()),
+                       reinterpret_cast<T*>(du.data_ptr()), n8, (int)kind))
+  return {dg, du};
+}
+
+void embedding_fwd(torch::Tensor idx, torch::Tensor wte, torch::Tensor wpe, int64_t off, torch::Tensor out) {
+  TORCH_CHECK(idx.is_cuda() && idx.scalar_type() == torch::kInt64 && idx.dim() == 2);
+  const int B = idx.size(0), T = idx.size(1), C = wte.size(1), V = wte.size(0);
+  TORCH_CHECK(C % 8 == 0 && wpe.size(1) == C && wte.scalar_type() == wpe.scalar_type());
+  TORCH_CHECK(off + T <= wpe.size(0), "positions exceed the position table");
+  TORCH_CHECK(out.scalar_type() == torch::kFloat32 && out.numel() == (int64_t)B * T * C && out.is_contiguous());
+  auto idxc = idx.contiguous();
+  const int N = B * T;
+  auto stream = at::hip::getCurrentHIPStream();
+  FOR_FLOAT_TYPES(wte.scalar_type(), TW,
+    hipLaunchKernelGGL(embed_fwd_kernel<TW>, dim3((N + 3) / 4), dim3(256), 0, stream, idxc.data_ptr<int64_t>(),
+                       reinterpret_cast<const TW*>(wte.data_ptr()), reinterpret_cast<const TW*>(wpe.data_ptr()),
+                       out.data_ptr<float>(), N, T, C, (int)off, V))
+}
+
+void embedding_bwd(torch::Tensor dout, torch::Tensor idx, torch::Tensor dwte, torch::Tensor dwpe, int64_t off) {
+  const int B = idx.size(0), T = idx.size(1), C = dwte.size(1), V = dwte.size(0);
+  TORCH_CHECK(dout.scalar_type() == torch::kFloat32 && dwte.scalar_type() == torch::kFloat32 &&
+              dwpe.scalar_type() == torch::kFloat32 && C % 4 == 0);
+  TORCH_CHECK(off + T <= dwpe.size(0));
+  auto idxc = idx.contiguous();
+  const int N = B * T;
+  auto stream = at::hip::getCurrentHIPStream();
+  hipLaunchKernelGGL(embed_bwd_tok_kernel, dim3((N + 3) / 4), dim3(256), 0, stream, dout.data_ptr<float>(),
+                     idxc.data_ptr<int64_t>(), dwte.data_ptr<float>(), N, C, V);
+  hipLaunchKernelGGL(embed_bwd_pos_kernel, dim3(T), dim3(256), 0, stream, dout.data_ptr<float>(), dwpe.data_ptr<float>(),
+                     B, T, C, (int)off);
+}
+
+torch::Tensor rope_qkv(torch::Tensor qkv, torch::Tensor cosv, torch::Tensor sinv, int64_t H, int64_t Hkv, int64_t D,
+                       bool inverse) {
+  TORCH_CHECK(qkv.is_cuda() && qkv.is_contiguous() && qkv.dim() == 3);
+  const int64_t B = qkv.size(0), T = qkv.size(1);
+  TORCH_CHECK(qkv.size(2) == (H + 2 * Hkv) * D && cosv.size(0) == T && cosv.size(1) == D / 2);
+  auto out = torch::empty_like(qkv);
+  const int64_t rows = B * T;
+  auto stream = at::hip::getCurrentHIPStream();
+  FOR_FLOAT_TYPES(qkv.scalar_type(), TT,
+    hipLaunchKernelGGL(rope_kernel<TT>, dim3(grid_for(rows * qkv.size(2))), dim3(256), 0, stream,
+                       reinterpret_cast<const TT*>(qkv.data_ptr()), reinterpret_cast<TT*>(out.data_ptr()),
+                       cosv.data_ptr<float>(), sinv.data_ptr<float>(), rows, (int)T, (int)H, (int)Hkv, (int)D,
+                       inverse ? 1 : 0))
+  return out;
+}
+
+void kv_quantize(torch::Tensor x, torch::Tensor q, torch::Tensor scale, int64_t pos) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.dim() == 4);
+  const int B = x.size(0), T = x.size(1), Hkv = x.size(2), D = x.size(3);
+  TORCH_CHECK(q.scalar_type() == torch::kInt8 && q.size(0) == B && q.size(1) == Hkv && q.size(3) == D);
+  const int cap = q.size(2);
+  TORCH_CHECK(pos + T <= cap, "cache overflow");
+  const int rows = B * T * Hkv;
+  auto stream = at::hip::getCurrentHIPStream();
+  FOR_FLOAT_TYPES(x.scalar_type(), TT,
+    hipLaunchKernelGGL(kv_quant_kernel<TT>, dim3((rows + 3) / 4), dim3(256), 0, stream,
+                       reinterpret_cast<const TT*>(x.data_ptr()), q.data_ptr<int8_t>(), scale.data_ptr<float>(), B,
+                       T, Hkv, D, cap, (int)pos))
+}
+
+std::vector<torch::Tensor> tensor_stats(torch::Tensor x, int64_t bins) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous());
+  const int64_t n = x.numel();
+  auto fopt = x.options().dtype(torch::kFloat32);
+  if (n == 0) {
+    auto z = torch::zeros({}, fopt);
+    return {z, z, z, z, torch::zeros({bins}, fopt), torch::zeros({bins + 1}, fopt)};
+  }
+  const int G = grid_for(n, 256, 1024);
+  auto p1 = torch::empty({G, 3}, fopt);
+  auto stream = at::hip::getCurrentHIPStream();
+  FOR_FLOAT_TYPES(x.scalar_type(), T,
+    hipLaunchKernelGGL(stats_pass1_kernel<T>, dim3(G), dim3(256), 0, stream, reinterpret_cast<const T*>(x.data_ptr()),
+                       n, p1.data_ptr<float>()))
+  auto sum = p1.select(1, 0).to(torch::kFloat64).sum();
+  auto mean = (sum / (double)n).to(torch::kFloat32);
+  auto mn = p1.select(1, 1).min();
+  auto mx = p1.select(1, 2).max();
+  // torch.histogram widens an empty range by +-0.5 around a constant input
+  auto same = mn.eq(mx);
+  auto lo = torch::where(same, mn - 0.5f, mn);
+  auto hi = torch::where(same, mx + 0.5f, mx);
+  auto mmm = torch::stack({mean, lo, hi}).contiguous();
+  auto p2 = torch::empty({G}, fopt);
+  auto hist = torch::zeros({bins}, fopt);
+  FOR_FLOAT_TYPES(x.scalar_type(), T,
+    hipLaunchKernelGGL(stats_pass2_kernel<T>, dim3(G), dim3(256), bins * sizeof(float), stream,
+                       reinterpret_cast<const T*>(x.data_ptr()), n, mmm.data_ptr<float>(), p2.data_ptr<float>(),
+                       hist.data_ptr<float>(), (int)bins))
+  auto var = p2.to(torch::kFloat64).sum() / (double)std::max<int64_t>(1, n - 1);
+  auto stdv = var.sqrt().to(torch::kFloat32);
+  auto edges = torch::linspace(0.0, 1.0, bins + 1, fopt) * (hi - lo) + lo;
+  auto width = (hi - lo) / (double)bins;
+  auto density = hist / ((double)n * width);
+  return {mean, stdv, mn, mx, density, edges};
+}

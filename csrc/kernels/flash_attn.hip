@@ -1,0 +1,579 @@
+// Causal flash attention for CDNA4 (gfx950), head_dim 64, bf16 in/out, fp32 accumulate.
+//
+// Operates directly on the fused QKV projection [B, T, (H + 2·Hkv)·D] (no split / transpose
+// copies) and writes O head-merged [B, T, H·D] — the layout the following projection GEMM
+// reads. GQA: kv head = q head / (H/Hkv), never expanded.
+//
+// MFMA: v_mfma_f32_32x32x16_bf16 throughout. C/D layout: col = lane&31,
+// row = (i&3) + 8(i>>2) + 4(lane>>5) for accumulator register i.
+//
+// forward (one 256-thread workgroup = 4 waves × 32 query rows = 128 rows of one (b, h)):
+//   Sᵀ = K·Qᵀ — K (A operand) from an XOR-swizzled LDS tile, Q (B operand) resident in 16
+//   VGPRs — so each lane owns ONE query row: the row max needs one cross-half exchange, the
+//   row sum stays lane-local until the epilogue;
+//   Oᵀ += Vᵀ·Pᵀ — P goes from the accumulator straight into the B operand (pairs of
+//   registers → bf16), Vᵀ (A operand) comes from the row-major V tile through
+//   ds_read_b64_tr_b16 (hardware transposed read), and the per-row rescale of Oᵀ is
+//   lane-local too;
+//   K/V tiles of 64 keys are double-buffered in LDS and staged through registers (the global
+//   loads of tile j+1 are issued before tile j's MFMAs, written to LDS after them);
+//   heaviest (latest) query blocks launch first; fully-masked tiles are skipped per wave.
+// backward (deterministic, no atomics):
+//   dK/dV kernel — a wave keeps 32 keys' K, V fragments and dKᵀ, dVᵀ accumulators in
+//   registers while sweeping 32-row query slices staged in LDS (all query heads of its KV
+//   group): S = Q·Kᵀ and dP = dO·Vᵀ put the key on the lane, so P and dS feed dVᵀ = dOᵀ·P and
+//   dKᵀ = Qᵀ·dS from registers (Qᵀ, dOᵀ by transposed LDS reads);
+//   dQ kernel — forward-shaped: a wave keeps 32 query rows' Q, dO, LSE, δ and dQᵀ in
+//   registers while sweeping K/V tiles; dQᵀ = Kᵀ·dSᵀ.
+//
+// LDS tiles are [rows][64 bf16] = 128-B rows; 16-B chunk ch of row r lives at chunk
+// ch ^ f(r), f(r) = ((r>>1)&1)<<2 | ((r>>2)&3). This single swizzle makes both the
+// ds_read_b128 row reads (16 lanes on 16 distinct rows, same chunk) and the
+// ds_read_b64_tr_b16 transposed reads (4 consecutive rows × 4 chunks per half-wave)
+// bank-conflict-free.
+//
+// Dropout (attn_pdrop) uses a counter-based hash of (b, h, q, k): the backward regenerates
+// the identical mask; the softmax normaliser uses the undropped probabilities (SDPA
+// semantics).
+#include "common.h"
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+
+namespace penroz {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int kD = 64;
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+__device__ __forceinline__ f32x16 mfma32(uint4 a, uint4 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
+                                                 0, 0, 0);
+}
+
+__device__ __forceinline__ int tile_off(int row, int ch) {
+  return row * 128 + ((ch ^ ((((row >> 1) & 1) << 2) | ((row >> 2) & 3))) << 4);
+}
+
+// element j = tile[rbase + (lane&31)][16s + 8·hh + j]
+__device__ __forceinline__ uint4 row_frag(const char* tile, int rbase, int s, int lane) {
+  return *reinterpret_cast<const uint4*>(tile + tile_off(rbase + (lane & 31), 2 * s + (lane >> 5)));
+}
+
+__device__ __forceinline__ uint2 tr_read(const char* tile, int row, int col) {
+  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s16x4*)(tile + tile_off(row, col >> 3) + ((col & 4) << 1)));
+  return __builtin_bit_cast(uint2, v);
+}
+
+// element j = tile[rbase + 8(j>>2) + 4·hh + (j&3)][cbase + (lane&31)]  (transposed read)
+__device__ __forceinline__ uint4 tr_frag(const char* tile, int rbase, int cbase, int lane) {
+  const int hh = lane >> 5, q = (lane & 15) >> 2, p = lane & 3;
+  const int col = cbase + 16 * ((lane >> 4) & 1) + 4 * p;
+  const uint2 a = tr_read(tile, rbase + 4 * hh + q, col);
+  const uint2 b = tr_read(tile, rbase + 8 + 4 * hh + q, col);
+  return uint4{a.x, a.y, b.x, b.y};
+}
+
+// accumulator registers 8ss..8ss+7 -> bf16x8 operand
+__device__ __forceinline__ uint4 acc_frag(const f32x16& a, int ss) {
+  const int o = 8 * ss;
+  return uint4{pack_bf16x2(a[o], a[o + 1]), pack_bf16x2(a[o + 2], a[o + 3]), pack_bf16x2(a[o + 4], a[o + 5]),
+               pack_bf16x2(a[o + 6], a[o + 7])};
+}
+
+__device__ __forceinline__ int acc_row(int i, int lane) { return (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5); }
+
+__device__ __forceinline__ bool dropout_keep(uint64_t seed, int b, int h, int H, int T, int q, int k, float p) {
+  const uint64_t ctr = (((uint64_t)b * H + h) * (uint64_t)T + (uint64_t)q) * (uint64_t)T + (uint64_t)k;
+  return uniform01(seed, ctr) >= p;
+}
+
+__device__ __forceinline__ uint4 zero4() { return uint4{0u, 0u, 0u, 0u}; }
+
+// stores 4 consecutive bf16 (8 bytes)
+__device__ __forceinline__ void store4(bf16* p, float a, float b, float c, float d) {
+  *reinterpret_cast<uint2*>(p) = uint2{pack_bf16x2(a, b), pack_bf16x2(c, d)};
+}
+
+// ------------------------------------------------------------------------------------------
+// forward
+template <bool DROPOUT>
+__global__ void __launch_bounds__(256) fa_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+                                                     float* __restrict__ lse, int T, int H, int Hkv, float scale,
+                                                     float p_drop, uint64_t seed) {
+  constexpr int BM = 128, BN = 64;
+  __shared__ __attribute__((aligned(16))) char smem[2][2][BN * 128];
+  const int nqb = (T + BM - 1) / BM;
+  const int qb = nqb - 1 - blockIdx.x;
+  const int b = blockIdx.y / H, h = blockIdx.y % H, hk = h / (H / Hkv);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5;
+  const size_t RS = (size_t)(H + 2 * Hkv) * kD;
+  const bf16* qbase = qkv + (size_t)b * T * RS + (size_t)h * kD;
+  const bf16* kbase = qkv + (size_t)b * T * RS + (size_t)(H + hk) * kD;
+  const bf16* vbase = qkv + (size_t)b * T * RS + (size_t)(H + Hkv + hk) * kD;
+  const int q0 = qb * BM + 32 * w;
+  const int qrow = q0 + (lane & 31);
+  const float c = scale * kLog2e;
+  const float inv_keep = DROPOUT ? 1.f / (1.f - p_drop) : 1.f;
+
+  uint4 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+    qf[s] = qrow < T ? *reinterpret_cast<const uint4*>(qbase + (size_t)qrow * RS + 16 * s + 8 * hh) : zero4();
+
+  const int sr = threadIdx.x >> 2, sc = 2 * (threadIdx.x & 3);
+  uint4 kst[2], vst[2];
+  auto gload = [&](int kt0) {
+    const int key = kt0 + sr;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      kst[i] = key < T ? *reinterpret_cast<const uint4*>(kbase + (size_t)key * RS + 8 * (sc + i)) : zero4();
+      vst[i] = key < T ? *reinterpret_cast<const uint4*>(vbase + (size_t)key * RS + 8 * (sc + i)) : zero4();
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      *reinterpret_cast<uint4*>(smem[buf][0] + tile_off(sr, sc + i)) = kst[i];
+      *reinterpret_cast<uint4*>(smem[buf][1] + tile_off(sr, sc + i)) = vst[i];
+    }
+  };
+
+  const int kend = min(T, qb * BM + BM);
+  const int ntiles = (kend + BN - 1) / BN;
+  f32x16 o[2];
+#pragma unroll
+  for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[dh][i] = 0.f;
+  float m = -1e30f, l = 0.f;
+
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int j = 0; j < ntiles; ++j) {
+    const int kt0 = j * BN;
+    if (j + 1 < ntiles) gload(kt0 + BN);
+    const char* Kt = smem[j & 1][0];
+    const char* Vt = smem[j & 1][1];
+    if (kt0 <= q0 + 31) {
+      f32x16 s[2];
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[kh][i] = 0.f;
+#pragma unroll
+        for (int st = 0; st < 4; ++st) s[kh] = mfma32(row_frag(Kt, 32 * kh, st, lane), qf[st], s[kh]);
+      }
+      const bool need_mask = (kt0 + BN - 1 > q0) || (kt0 + BN > T);
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float v = s[kh][i] * c;
+          if (need_mask) {
+            const int key = kt0 + 32 * kh + acc_row(i, lane);
+            if (key > qrow || key >= T) v = -INFINITY;
+          }
+          s[kh][i] = v;
+          tmax = fmaxf(tmax, v);
+        }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float mnew = fmaxf(m, tmax);
+      const float alpha = exp2f(m - mnew);
+      m = mnew;
+      float rs = 0.f;
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float p = exp2f(s[kh][i] - mnew);
+          rs += p;
+          if constexpr (DROPOUT) {
+            const int key = kt0 + 32 * kh + acc_row(i, lane);
+            s[kh][i] = dropout_keep(seed, b, h, H, T, qrow, key, p_drop) ? p * inv_keep : 0.f;
+          } else {
+            s[kh][i] = p;
+          }
+        }
+      l = l * alpha + rs;
+#pragma unroll
+      for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[dh][i] *= alpha;
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          const uint4 pf = acc_frag(s[kh], ss);
+#pragma unroll
+          for (int dh = 0; dh < 2; ++dh) o[dh] = mfma32(tr_frag(Vt, 32 * kh + 16 * ss, 32 * dh, lane), pf, o[dh]);
+        }
+    }
+    if (j + 1 < ntiles) lstore((j + 1) & 1);
+    __syncthreads();
+  }
+  l += __shfl_xor(l, 32, 64);
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  if (qrow < T) {
+    bf16* orow = out + ((size_t)b * T + qrow) * H * kD + (size_t)h * kD;
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        store4(orow + 32 * dh + 8 * g + 4 * hh, o[dh][4 * g] * inv, o[dh][4 * g + 1] * inv, o[dh][4 * g + 2] * inv,
+               o[dh][4 * g + 3] * inv);
+    if (hh == 0) lse[((size_t)b * H + h) * T + qrow] = (m + log2f(l)) * kLn2;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// backward preprocessing: delta[b, h, q] = Σ_d dO·O  (8 lanes per row, 16-B loads)
+__global__ void __launch_bounds__(256) fa_bwd_pre_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ out,
+                                                         float* __restrict__ delta, int B, int T, int H) {
+  const int gid = blockIdx.x * 256 + threadIdx.x;
+  const int row = gid >> 3, part = gid & 7;  // row over B*T*H in [b][t][h] order
+  const bool ok = row < B * T * H;
+  float s = 0.f;
+  if (ok) {
+    float a[8], o[8];
+    Vec8<bf16>::load(dout + (size_t)row * kD + 8 * part, a);
+    Vec8<bf16>::load(out + (size_t)row * kD + 8 * part, o);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += a[k] * o[k];
+  }
+  s += __shfl_xor(s, 1, 64);
+  s += __shfl_xor(s, 2, 64);
+  s += __shfl_xor(s, 4, 64);
+  if (ok && part == 0) {
+    const int h = row % H, t = (row / H) % T, b = row / (H * T);
+    delta[((size_t)b * H + h) * T + t] = s;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// dK / dV: grid (ceil(T/128) key blocks, B*Hkv); wave w owns keys kb*128 + 32w + (lane&31)
+template <bool DROPOUT>
+__global__ void __launch_bounds__(256) fa_bwd_dkdv_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+                                                          const float* __restrict__ lse,
+                                                          const float* __restrict__ delta, bf16* __restrict__ dqkv,
+                                                          int T, int H, int Hkv, float scale, float p_drop,
+                                                          uint64_t seed) {
+  constexpr int BK = 128, QS = 32;
+  __shared__ __attribute__((aligned(16))) char qt[2][QS * 128];
+  __shared__ __attribute__((aligned(16))) char dot[2][QS * 128];
+  __shared__ __attribute__((aligned(16))) float lse2s[2][QS];
+  __shared__ __attribute__((aligned(16))) float dels[2][QS];
+  const int kb = blockIdx.x;
+  const int b = blockIdx.y / Hkv, hk = blockIdx.y % Hkv;
+  const int G = H / Hkv;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5;
+  const size_t RS = (size_t)(H + 2 * Hkv) * kD;
+  const size_t ORS = (size_t)H * kD;
+  const int kw0 = kb * BK + 32 * w;
+  const int key = kw0 + (lane & 31);
+  const float c = scale * kLog2e;
+  const float inv_keep = DROPOUT ? 1.f / (1.f - p_drop) : 1.f;
+
+  const bf16* kbase = qkv + (size_t)b * T * RS + (size_t)(H + hk) * kD;
+  const bf16* vbase = qkv + (size_t)b * T * RS + (size_t)(H + Hkv + hk) * kD;
+  uint4 kf[4], vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    kf[s] = key < T ? *reinterpret_cast<const uint4*>(kbase + (size_t)key * RS + 16 * s + 8 * hh) : zero4();
+    vf[s] = key < T ? *reinterpret_cast<const uint4*>(vbase + (size_t)key * RS + 16 * s + 8 * hh) : zero4();
+  }
+  f32x16 dk[2], dv[2];
+#pragma unroll
+  for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dk[dh][i] = dv[dh][i] = 0.f;
+
+  // staging: threads 0..127 -> Q slice, 128..255 -> dO slice; row (t>>2)&31, chunks 2(t&3), +1
+  const int st_tile = threadIdx.x >> 7, sr = (threadIdx.x >> 2) & 31, sc = 2 * (threadIdx.x & 3);
+  const int s_first = (kb * BK) / QS;
+  const int nslices = (T + QS - 1) / QS;
+  const int total = G * (nslices - s_first);
+  uint4 st[2];
+  float st_scalar = 0.f;
+  auto gload = [&](int it) {
+    const int hq = hk * G + it / (nslices - s_first);
+    const int qs0 = (s_first + it % (nslices - s_first)) * QS;
+    const int q = qs0 + sr;
+    const bf16* src = st_tile == 0 ? qkv + (size_t)b * T * RS + (size_t)hq * kD + (size_t)q * RS
+                                   : dout + (size_t)b * T * ORS + (size_t)hq * kD + (size_t)q * ORS;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) st[i] = q < T ? *reinterpret_cast<const uint4*>(src + 8 * (sc + i)) : zero4();
+    if (threadIdx.x < 2 * QS) {
+      const int qq = qs0 + (threadIdx.x & 31);
+      const size_t r = ((size_t)b * H + hq) * T + qq;
+      st_scalar = qq < T ? (threadIdx.x < QS ? lse[r] * kLog2e : delta[r]) : 0.f;
+    }
+  };
+  auto lstore = [&](int buf) {
+    char* dst = st_tile == 0 ? qt[buf] : dot[buf];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) *reinterpret_cast<uint4*>(dst + tile_off(sr, sc + i)) = st[i];
+    if (threadIdx.x < QS) lse2s[buf][threadIdx.x] = st_scalar;
+    else if (threadIdx.x < 2 * QS) dels[buf][threadIdx.x - QS] = st_scalar;
+  };
+
+  if (total > 0) {
+    gload(0);
+    lstore(0);
+  }
+  __syncthreads();
+  for (int it = 0; it < total; ++it) {
+    if (it + 1 < total) gload(it + 1);
+    const int buf = it & 1;
+    const int hq = hk * G + it / (nslices - s_first);
+    const int qs0 = (s_first + it % (nslices - s_first)) * QS;
+    if (qs0 + QS - 1 >= kw0 && kw0 < T) {
+      const char* Qt = qt[buf];
+      const char* Dt = dot[buf];
+      f32x16 sp, dp;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sp[i] = dp[i] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        sp = mfma32(row_frag(Qt, 0, s, lane), kf[s], sp);
+        dp = mfma32(row_frag(Dt, 0, s, lane), vf[s], dp);
+      }
+      f32x16 pd, ds;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int r0 = 8 * g + 4 * hh;
+        const float4_t l2 = *reinterpret_cast<const float4_t*>(&lse2s[buf][r0]);
+        const float4_t dl = *reinterpret_cast<const float4_t*>(&dels[buf][r0]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int i = 4 * g + k;
+          const int q = qs0 + r0 + k;
+          float p = exp2f(sp[i] * c - l2[k]);
+          if (key > q || q >= T || key >= T) p = 0.f;
+          float dpi = dp[i];
+          float pdrop = p;
+          if constexpr (DROPOUT) {
+            const bool keep = dropout_keep(seed, b, hq, H, T, q, key, p_drop);
+            pdrop = keep ? p * inv_keep : 0.f;
+            dpi = keep ? dpi * inv_keep : 0.f;
+          }
+          pd[i] = pdrop;
+          ds[i] = p * (dpi - dl[k]);
+        }
+      }
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const uint4 pf = acc_frag(pd, ss), sf = acc_frag(ds, ss);
+#pragma unroll
+        for (int dh = 0; dh < 2; ++dh) {
+          dv[dh] = mfma32(tr_frag(Dt, 16 * ss, 32 * dh, lane), pf, dv[dh]);
+          dk[dh] = mfma32(tr_frag(Qt, 16 * ss, 32 * dh, lane), sf, dk[dh]);
+        }
+      }
+    }
+    if (it + 1 < total) lstore((it + 1) & 1);
+    __syncthreads();
+  }
+  if (key < T) {
+    bf16* dkrow = dqkv + ((size_t)b * T + key) * RS + (size_t)(H + hk) * kD;
+    bf16* dvrow = dqkv + ((size_t)b * T + key) * RS + (size_t)(H + Hkv + hk) * kD;
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = 32 * dh + 8 * g + 4 * hh;
+        store4(dkrow + d, dk[dh][4 * g] * scale, dk[dh][4 * g + 1] * scale, dk[dh][4 * g + 2] * scale,
+               dk[dh][4 * g + 3] * scale);
+        store4(dvrow + d, dv[dh][4 * g], dv[dh][4 * g + 1], dv[dh][4 * g + 2], dv[dh][4 * g + 3]);
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// dQ: grid (ceil(T/128) query blocks, heaviest first, B*H); forward-shaped
+template <bool DROPOUT>
+__global__ void __launch_bounds__(256) fa_bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+                                                        const float* __restrict__ lse,
+                                                        const float* __restrict__ delta, bf16* __restrict__ dqkv,
+                                                        int T, int H, int Hkv, float scale, float p_drop,
+                                                        uint64_t seed) {
+  constexpr int BM = 128, BN = 64;
+  __shared__ __attribute__((aligned(16))) char smem[2][2][BN * 128];
+  const int nqb = (T + BM - 1) / BM;
+  const int qb = nqb - 1 - blockIdx.x;
+  const int b = blockIdx.y / H, h = blockIdx.y % H, hk = h / (H / Hkv);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5;
+  const size_t RS = (size_t)(H + 2 * Hkv) * kD;
+  const size_t ORS = (size_t)H * kD;
+  const bf16* kbase = qkv + (size_t)b * T * RS + (size_t)(H + hk) * kD;
+  const bf16* vbase = qkv + (size_t)b * T * RS + (size_t)(H + Hkv + hk) * kD;
+  const int q0 = qb * BM + 32 * w;
+  const int qrow = q0 + (lane & 31);
+  const float c = scale * kLog2e;
+  const float inv_keep = DROPOUT ? 1.f / (1.f - p_drop) : 1.f;
+
+  uint4 qf[4], dof[4];
+  const bool qok = qrow < T;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    qf[s] = qok ? *reinterpret_cast<const uint4*>(qkv + (size_t)b * T * RS + (size_t)h * kD + (size_t)qrow * RS + 16 * s +
+                                                  8 * hh)
+                : zero4();
+    dof[s] = qok ? *reinterpret_cast<const uint4*>(dout + (size_t)b * T * ORS + (size_t)h * kD + (size_t)qrow * ORS +
+                                                   16 * s + 8 * hh)
+                 : zero4();
+  }
+  const size_t rr = ((size_t)b * H + h) * T + qrow;
+  const float l2 = qok ? lse[rr] * kLog2e : 0.f;
+  const float dl = qok ? delta[rr] : 0.f;
+
+  const int sr = threadIdx.x >> 2, sc = 2 * (threadIdx.x & 3);
+  uint4 kst[2], vst[2];
+  auto gload = [&](int kt0) {
+    const int k = kt0 + sr;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      kst[i] = k < T ? *reinterpret_cast<const uint4*>(kbase + (size_t)k * RS + 8 * (sc + i)) : zero4();
+      vst[i] = k < T ? *reinterpret_cast<const uint4*>(vbase + (size_t)k * RS + 8 * (sc + i)) : zero4();
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      *reinterpret_cast<uint4*>(smem[buf][0] + tile_off(sr, sc + i)) = kst[i];
+      *reinterpret_cast<uint4*>(smem[buf][1] + tile_off(sr, sc + i)) = vst[i];
+    }
+  };
+  const int kend = min(T, qb * BM + BM);
+  const int ntiles = (kend + BN - 1) / BN;
+  f32x16 dq[2];
+#pragma unroll
+  for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dq[dh][i] = 0.f;
+
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int j = 0; j < ntiles; ++j) {
+    const int kt0 = j * BN;
+    if (j + 1 < ntiles) gload(kt0 + BN);
+    const char* Kt = smem[j & 1][0];
+    const char* Vt = smem[j & 1][1];
+    if (kt0 <= q0 + 31) {
+      f32x16 s[2], dp[2];
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[kh][i] = dp[kh][i] = 0.f;
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+          s[kh] = mfma32(row_frag(Kt, 32 * kh, st, lane), qf[st], s[kh]);
+          dp[kh] = mfma32(row_frag(Vt, 32 * kh, st, lane), dof[st], dp[kh]);
+        }
+      }
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int k = kt0 + 32 * kh + acc_row(i, lane);
+          float p = exp2f(s[kh][i] * c - l2);
+          if (k > qrow || k >= T || !qok) p = 0.f;
+          float dpi = dp[kh][i];
+          if constexpr (DROPOUT) {
+            const bool keep = dropout_keep(seed, b, h, H, T, qrow, k, p_drop);
+            dpi = keep ? dpi * inv_keep : 0.f;
+          }
+          s[kh][i] = p * (dpi - dl);
+        }
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          const uint4 sf = acc_frag(s[kh], ss);
+#pragma unroll
+          for (int dh = 0; dh < 2; ++dh) dq[dh] = mfma32(tr_frag(Kt, 32 * kh + 16 * ss, 32 * dh, lane), sf, dq[dh]);
+        }
+    }
+    if (j + 1 < ntiles) lstore((j + 1) & 1);
+    __syncthreads();
+  }
+  if (qok) {
+    bf16* dqrow = dqkv + ((size_t)b * T + qrow) * RS + (size_t)h * kD;
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        store4(dqrow + 32 * dh + 8 * g + 4 * hh, dq[dh][4 * g] * scale, dq[dh][4 * g + 1] * scale,
+               dq[dh][4 * g + 2] * scale, dq[dh][4 * g + 3] * scale);
+  }
+}
+
+}  // namespace penroz
+
+// ============================================================================ host side
+using namespace penroz;
+
+static void check_qkv(const torch::Tensor& qkv, int64_t H, int64_t Hkv, int64_t D) {
+  TORCH_CHECK(qkv.is_cuda() && qkv.is_contiguous() && qkv.dim() == 3, "qkv must be a contiguous [B, T, W] GPU tensor");
+  TORCH_CHECK(qkv.scalar_type() == torch::kBFloat16, "flash attention expects bf16");
+  TORCH_CHECK(D == kD, "flash attention kernel is built for head_dim 64");
+  TORCH_CHECK(H % Hkv == 0 && qkv.size(2) == (H + 2 * Hkv) * D, "qkv width must be (H + 2*Hkv)*D");
+}
+
+void flash_attn_fwd(torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int64_t H, int64_t Hkv, int64_t D,
+                    double scale, double p_drop, int64_t seed) {
+  check_qkv(qkv, H, Hkv, D);
+  const int B = qkv.size(0), T = qkv.size(1);
+  TORCH_CHECK(out.is_contiguous() && out.scalar_type() == torch::kBFloat16 && out.numel() == (int64_t)B * T * H * D);
+  TORCH_CHECK(lse.is_contiguous() && lse.scalar_type() == torch::kFloat32 && lse.numel() == (int64_t)B * H * T);
+  if (B == 0 || T == 0) return;
+  dim3 grid((T + 127) / 128, B * H);
+  auto stream = at::hip::getCurrentHIPStream();
+  const bf16* q = reinterpret_cast<const bf16*>(qkv.data_ptr());
+  bf16* o = reinterpret_cast<bf16*>(out.data_ptr());
+  if (p_drop > 0.0)
+    hipLaunchKernelGGL(fa_fwd_kernel<true>, grid, dim3(256), 0, stream, q, o, lse.data_ptr<float>(), T, (int)H,
+                       (int)Hkv, (float)scale, (float)p_drop, (uint64_t)seed);
+  else
+    hipLaunchKernelGGL(fa_fwd_kernel<false>, grid, dim3(256), 0, stream, q, o, lse.data_ptr<float>(), T, (int)H,
+                       (int)Hkv, (float)scale, 0.f, (uint64_t)seed);
+}
+
+void flash_attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, torch::Tensor dqkv,
+                    int64_t H, int64_t Hkv, int64_t D, double scale, double p_drop, int64_t seed) {
+  check_qkv(qkv, H, Hkv, D);
+  const int B = qkv.size(0), T = qkv.size(1);
+  TORCH_CHECK(dout.is_contiguous() && dout.scalar_type() == torch::kBFloat16 && dout.numel() == (int64_t)B * T * H * D);
+  TORCH_CHECK(out.is_contiguous() && out.numel() == dout.numel());
+  TORCH_CHECK(dqkv.is_contiguous() && dqkv.scalar_type() == torch::kBFloat16 && dqkv.numel() == qkv.numel());
+  if (B == 0 || T == 0) return;
+  auto delta = torch::empty({B, H, T}, qkv.options().dtype(torch::kFloat32));
+  auto stream = at::hip::getCurrentHIPStream();
+  const int rows = B * T * H;
+  hipLaunchKernelGGL(fa_bwd_pre_kernel, dim3((rows * 8 + 255) / 256), dim3(256), 0, stream,
+                     reinterpret_cast<const bf16*>(dout.data_ptr()), reinterpret_cast<const bf16*>(out.data_ptr()),
+                     delta.data_ptr<float>(), B, T, (int)H);
+  const bf16* q = reinterpret_cast<const bf16*>(qkv.data_ptr());
+  const bf16* d = reinterpret_cast<const bf16*>(dout.data_ptr());
+  bf16* g = reinterpret_cast<bf16*>(dqkv.data_ptr());
+  dim3 gkv((T + 127) / 128, B * Hkv), gq((T + 127) / 128, B * H);
+  if (p_drop > 0.0) {
+    hipLaunchKernelGGL(fa_bwd_dkdv_kernel<true>, gkv, dim3(256), 0, stream, q, d, lse.data_ptr<float>(),
+                       delta.data_ptr<float>(), g, T, (int)H, (int)Hkv, (float)scale, (float)p_drop, (uint64_t)seed);
+    hipLaunchKernelGGL(fa_bwd_dq_kernel<true>, gq, dim3(256), 0, stream, q, d, lse.data_ptr<float>(),
+                       delta.data_ptr<float>(), g, T, (int)H, (int)Hkv, (float)scale, (float)p_drop, (uint64_t)seed);
+  } else {
+    hipLaunchKernelGGL(fa_bwd_dkdv_kernel<false>, gkv, dim3(256), 0, stream, q, d, lse.data_ptr<float>(),
+                       delta.data_ptr<float>(), g, T, (int)H, (int)Hkv, (float)scale, 0.f, (uint64_t)seed);
+    hipLaunchKernelGGL(fa_bwd_dq_kernel<false>, gq, dim3(256), 0, stream, q, d, lse.data_ptr<float>(),
+                       delta.data_ptr<float>(), g, T, (int)H, (int)Hkv, (float)scale, 0.f, (uint64_t)seed);
+  }
+}

@@ -1,0 +1,415 @@
+"""Fused GPT-2 training/eval executor for MI355X.
+
+A layer list that matches the GPT-2 pattern of the reference's example/HF-import layout
+(``main.py:57-83``, ``mappers.py:122-176``) is *lowered* to this executor while the
+``nn.Module`` tree (and therefore every state_dict key) stays exactly as compiled.  Instead of
+per-module autograd it runs an explicit forward and backward:
+
+forward, per layer (N = B·T tokens, fp32 residual stream — the reference's autocast numerics)
+  LN1 (HIP, → bf16) → QKV GEMM+bias (hipBLASLt) → flash attention (HIP, reads the fused QKV
+  tensor, writes head-merged O + LSE) → proj GEMM+bias → residual-add+LN2 (one HIP pass)
+  → fc GEMM+bias → GELU (HIP) → fc2 GEMM+bias → (residual-add fused into the next LN)
+head: final LN → lm_head GEMM → cross-entropy (HIP: one LDS-resident pass per row, writes
+  the logits gradient in place, no fp32 logits)
+backward mirrors it: dgrad/wgrad GEMMs (wgrad accumulated in fp32), GELU backward fused with
+  the fc bias-gradient column sum, LayerNorm backward fused with dγ/dβ, the residual-gradient
+  accumulation, its bf16 copy for the next GEMM, and the bias gradient of the preceding
+  linear; flash-attention backward; embedding backward (dwte scatter, dwpe reduction).
+
+Parameters, gradients and AdamW moments live in flat fp32 buffers laid out in backward
+completion order (lm_head … wte) so gradient buckets are contiguous slices: the reducer
+launches each bucket's RCCL all-reduce as soon as the layers in it finish, overlapped with
+the remaining backward.  A flat bf16 shadow of every parameter feeds the GEMMs and is
+refreshed by the fused AdamW kernel in the same pass that updates the fp32 masters.
+"""
+from __future__ import annotations
+
+import logging
+import math
+from dataclasses import dataclass, field
+
+import torch
+import torch.nn as nn
+from torch import Tensor
+
+from penroz.models import layers as L
+from penroz.ops import attention as attn_ops
+from penroz.ops import activations as act_ops
+from penroz.ops import fused as fused_ops
+from penroz.ops import norms as norm_ops
+from penroz.ops import _ext
+
+log = logging.getLogger(__name__)
+
+
+@dataclass
+class _Block:
+    ln1: nn.LayerNorm
+    qkv: nn.Linear
+    attn: L.CausalSelfAttention
+    proj: nn.Linear
+    ln2: nn.LayerNorm
+    fc: nn.Linear
+    act: nn.GELU
+    fc2: nn.Linear
+
+
+@dataclass
+class GPTSpec:
+    V: int
+    C: int
+    H: int
+    D: int
+    F: int
+    P: int
+    wte: nn.Embedding
+    wpe: L.PositionEmbedding
+    blocks: list = field(default_factory=list)
+    lnf: nn.LayerNorm = None
+    head: nn.Linear = None
+    gelu_approx: str = "none"
+
+
+def _is(m, cls):
+    return isinstance(m, cls)
+
+
+def _dropout_zero(m) -> bool:
+    return _is(m, nn.Dropout) and m.p == 0.0
+
+
+class GPTExecutor:
+    # ------------------------------------------------------------------ pattern match
+    @staticmethod
+    def match(model) -> GPTSpec | None:
+        ls = list(model.layers)
+        if len(ls) < 5:
+            return None
+        emb = ls[0]
+        if not (_is(emb, L.Summation) and len(emb) == 2 and type(emb[0]) is nn.Embedding
+                and _is(emb[1], L.PositionEmbedding)):
+            return None
+        if not _dropout_zero(ls[1]):
+            return None
+        tail = ls[-3:] if _is(ls[-1], L.SoftmaxOnLast) else ls[-2:]
+        if len(tail) < 2 or not _is(tail[0], nn.LayerNorm) or not _is(tail[1], nn.Linear) or tail[1].bias is not None:
+            return None
+        body = ls[2:len(ls) - len(tail)]
+        if not body:
+            return None
+        C = emb[0].embedding_dim
+        spec = GPTSpec(V=emb[0].num_embeddings, C=C, H=0, D=0, F=0, P=emb[1].num_embeddings,
+                       wte=emb[0], wpe=emb[1], lnf=tail[0], head=tail[1])
+        approx = None
+        for blk in body:
+            if not (_is(blk, L.ResidualConnection) and len(blk) == 2):
+                return None
+            a, m = blk[0], blk[1]
+            if not (_is(a, nn.Sequential) and len(a) == 5 and _is(m, nn.Sequential) and len(m) == 5):
+                return None
+            ln1, qkv, att, proj, d1 = a
+            ln2, fc, act, fc2, d2 = m
+            ok = (_is(ln1, nn.LayerNorm) and _is(qkv, nn.Linear) and _is(att, L.CausalSelfAttention)
+                  and _is(proj, nn.Linear) and _dropout_zero(d1) and _is(ln2, nn.LayerNorm)
+                  and _is(fc, nn.Linear) and _is(act, nn.GELU) and _is(fc2, nn.Linear) and _dropout_zero(d2))
+            if not ok:
+                return None
+            if att.rope_theta is not None or att.num_kv_heads != att.num_heads:
+                return None
+            H = att.num_heads
+            D = C // H
+            if (qkv.in_features, qkv.out_features) != (C, 3 * C) or (proj.in_features, proj.out_features) != (C, C):
+                return None
+            if fc.in_features != C or fc2.out_features != C or fc2.in_features != fc.out_features:
+                return None
+            if any(x.bias is None for x in (qkv, proj, fc, fc2)) or any(
+                    x.weight is None or x.bias is None or tuple(x.normalized_shape) != (C,) for x in (ln1, ln2)):
+                return None
+            if approx is None:
+                approx = act.approximate
+            if act.approximate != approx:
+                return None
+            spec.H, spec.D, spec.F = H, D, fc.out_features
+            spec.blocks.append(_Block(ln1, qkv, att, proj, ln2, fc, act, fc2))
+        if spec.D not in attn_ops.SUPPORTED_HEAD_DIMS or C % 64 != 0 or spec.F % 64 != 0:
+            return None
+        if tuple(spec.lnf.normalized_shape) != (C,) or spec.head.in_features != C:
+            return None
+        if any(p.dtype != torch.float32 for p in model.parameters()):
+            return None
+        spec.gelu_approx = approx
+        return spec
+
+    # ------------------------------------------------------------------ setup
+    def __init__(self, model, device):
+        spec = self.match(model)
+        if spec is None:
+            raise ValueError("model does not match the GPT-2 pattern")
+        _ext.kernels()  # hard requirement on GPU
+        self.model = model
+        self.spec = spec
+        self.device = device
+        self.L = len(spec.blocks)
+        self._flatten()
+        self._acts_shape = None
+        self.reducer = None
+        self._captured = None
+        self._step_seed = 0
+
+    def _param_order(self):
+        s = self.spec
+        segs = [[s.head.weight, s.lnf.weight, s.lnf.bias]]
+        for b in reversed(s.blocks):
+            segs.append([b.fc2.weight, b.fc2.bias, b.fc.weight, b.fc.bias, b.ln2.weight, b.ln2.bias,
+                         b.proj.weight, b.proj.bias, b.qkv.weight, b.qkv.bias, b.ln1.weight, b.ln1.bias])
+        segs.append([s.wpe.weight, s.wte.weight])
+        return segs
+
+    def _flatten(self):
+        """Re-point every parameter at a view of flat fp32 / grad / bf16-shadow buffers."""
+        segs = self._param_order()
+        params = [p for seg in segs for p in seg]
+        if len({id(p) for p in params}) != len(params) or len(params) != len(list(self.model.parameters())):
+            raise ValueError("executor needs every parameter exactly once (no tying)")
+        total = sum(p.numel() for p in params)
+        dev = self.device
+        self.flat = torch.empty(total, dtype=torch.float32, device=dev)
+        self.flat_grad = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.shadow = torch.empty(total, dtype=torch.bfloat16, device=dev)
+        self.offsets = {}
+        self.segments = []
+        off = 0
+        for seg in segs:
+            start = off
+            for p in seg:
+                n = p.numel()
+                self.flat[off:off + n].copy_(p.data.reshape(-1))
+                p.data = self.flat[off:off + n].view_as(p)
+                p.grad = self.flat_grad[off:off + n].view_as(p)
+                self.offsets[id(p)] = off
+                off += n
+            self.segments.append((start, off))
+        self.params_in_order = params
+        self.refresh_shadow()
+        opt = self.model.optimizer
+        if hasattr(opt, "attach_flat") and len(opt.param_groups) == 1:
+            opt.attach_flat(params, self.flat, self.flat_grad, self.shadow, [self.offsets[id(p)] for p in params])
+            self._opt_flat = True
+        else:
+            self._opt_flat = False
+
+    def refresh_shadow(self):
+        self.shadow.copy_(self.flat)
+
+    def bf16(self, p: Tensor) -> Tensor:
+        off = self.offsets[id(p)]
+        return self.shadow[off:off + p.numel()].view(p.shape)
+
+    def grad(self, p: Tensor) -> Tensor:
+        off = self.offsets[id(p)]
+        return self.flat_grad[off:off + p.numel()].view(p.shape)
+
+    # ------------------------------------------------------------------ buffers
+    def _alloc(self, B: int, T: int):
+        if self._acts_shape == (B, T):
+            return
+        s, dev = self.spec, self.device
+        N, C, F, V = B * T, s.C, s.F, s.V
+        bf, f32 = torch.bfloat16, torch.float32
+        self.resid = [torch.empty(N, C, dtype=f32, device=dev) for _ in range(self.L + 1)]
+        self.resid_mid = [torch.empty(N, C, dtype=f32, device=dev) for _ in range(self.L)]
+        self.ln1 = [torch.empty(N, C, dtype=bf, device=dev) for _ in range(self.L)]
+        self.ln2 = [torch.empty(N, C, dtype=bf, device=dev) for _ in range(self.L)]
+        self.stats = [tuple(torch.empty(N, dtype=f32, device=dev) for _ in range(4)) for _ in range(self.L)]
+        self.statsf = (torch.empty(N, dtype=f32, device=dev), torch.empty(N, dtype=f32, device=dev))
+        self.qkv = [torch.empty(N, 3 * C, dtype=bf, device=dev) for _ in range(self.L)]
+        self.att = [torch.empty(N, C, dtype=bf, device=dev) for _ in range(self.L)]
+        self.lse = [torch.empty(B, s.H, T, dtype=f32, device=dev) for _ in range(self.L)]
+        self.fcpre = [torch.empty(N, F, dtype=bf, device=dev) for _ in range(self.L)]
+        self.fcact = [torch.empty(N, F, dtype=bf, device=dev) for _ in range(self.L)]
+        self.lnf_out = torch.empty(N, C, dtype=bf, device=dev)
+        self.logits = torch.empty(N, V, dtype=bf, device=dev)
+        self.tmp_c = torch.empty(N, C, dtype=bf, device=dev)
+        self.dresid = torch.empty(N, C, dtype=f32, device=dev)
+        self.dresid_bf = torch.empty(N, C, dtype=bf, device=dev)
+        self.d_f = torch.empty(N, F, dtype=bf, device=dev)
+        self.d_c = torch.empty(N, C, dtype=bf, device=dev)
+        self.dqkv = torch.empty(N, 3 * C, dtype=bf, device=dev)
+        self._acts_shape = (B, T)
+
+    def free_buffers(self):
+        for name in ("resid", "resid_mid", "ln1", "ln2", "qkv", "fcpre", "fcact", "lnf_out", "logits", "tmp_c",
+                     "dresid", "dresid_bf", "d_f", "d_c", "dqkv", "att", "lse", "stats", "statsf"):
+            if hasattr(self, name):
+                delattr(self, name)
+        self._acts_shape = None
+
+    # ------------------------------------------------------------------ forward
+    def _linear(self, x: Tensor, lin: nn.Linear, out: Tensor | None = None) -> Tensor:
+        w = self.bf16(lin.weight)
+        if lin.bias is not None:
+            return torch.addmm(self.bf16(lin.bias), x, w.t(), out=out) if out is not None else \
+                torch.addmm(self.bf16(lin.bias), x, w.t())
+        return torch.mm(x, w.t(), out=out) if out is not None else torch.mm(x, w.t())
+
+    def _forward(self, idx: Tensor, training: bool, dropout_seed: int = 0):
+        s = self.spec
+        B, T = idx.shape
+        if T > s.P:
+            raise ValueError(f"sequence length {T} exceeds the position table {s.P}")
+        self._alloc(B, T)
+        H, D, C = s.H, s.D, s.C
+        fused_ops.embedding_fwd(idx, s.wte.weight, s.wpe.weight, s.wpe.position_offset, out=self.resid[0])
+        for l, b in enumerate(s.blocks):
+            mean1, rstd1, mean2, rstd2 = self.stats[l]
+            if l == 0:
+                norm_ops.ln_fwd(self.resid[0], b.ln1.weight, b.ln1.bias, b.ln1.eps, y=self.ln1[0],
+                                mean=mean1, rstd=rstd1)
+            else:  # resid[l] = resid_mid[l-1] + fc2(l-1), LN1(l) in the same pass
+                norm_ops.add_ln_fwd(self.resid_mid[l - 1], self.tmp_c, self.resid[l], b.ln1.weight, b.ln1.bias,
+                                    b.ln1.eps, y=self.ln1[l], mean=mean1, rstd=rstd1)
+            self._linear(self.ln1[l], b.qkv, out=self.qkv[l])
+            p = b.attn.dropout if training else 0.0
+            attn_ops.flash_fwd(self.qkv[l].view(B, T, 3 * C), H, H, D, p, dropout_seed + l,
+                               out=self.att[l].view(B, T, C), lse=self.lse[l])
+            self._linear(self.att[l], b.proj, out=self.tmp_c)
+            norm_ops.add_ln_fwd(self.resid[l], self.tmp_c, self.resid_mid[l], b.ln2.weight, b.ln2.bias, b.ln2.eps,
+                                y=self.ln2[l], mean=mean2, rstd=rstd2)
+            self._linear(self.ln2[l], b.fc, out=self.fcpre[l])
+            act_ops.gelu_fwd(self.fcpre[l], s.gelu_approx, out=self.fcact[l])
+            self._linear(self.fcact[l], b.fc2, out=self.tmp_c)
+        Lc = self.L
+        meanf, rstdf = self.statsf
+        norm_ops.add_ln_fwd(self.resid_mid[Lc - 1], self.tmp_c, self.resid[Lc], s.lnf.weight, s.lnf.bias, s.lnf.eps,
+                            y=self.lnf_out, mean=meanf, rstd=rstdf)
+        torch.mm(self.lnf_out, self.bf16(s.head.weight).t(), out=self.logits)
+
+    # ------------------------------------------------------------------ public API
+    @torch.no_grad()
+    def eval_loss(self, idx: Tensor, targets: Tensor) -> Tensor:
+        self._forward(idx, training=False)
+        rows = fused_ops.cross_entropy_fwd_bwd(self.logits, targets.reshape(-1), 0.0)
+        return rows.mean()
+
+    @torch.no_grad()
+    def logits_for(self, idx: Tensor) -> Tensor:
+        self._forward(idx, training=False)
+        return self.logits.view(idx.shape[0], idx.shape[1], -1)
+
+    def setup_training(self, distributed: bool):
+        from penroz.parallel.reducer import GradReducer, plan_buckets, DEFAULT_BUCKET_MB
+        import torch.distributed as dist
+        self.refresh_shadow()
+        self.reducer = None
+        if distributed and dist.is_initialized() and dist.get_world_size() > 1:
+            buckets = plan_buckets(self.segments, DEFAULT_BUCKET_MB * 2**20)
+            self.reducer = GradReducer(self.flat_grad, buckets)
+            self.reducer.broadcast_params(self.flat)
+            self.refresh_shadow()
+            self._seg_bucket = [self.reducer.bucket_of(s) for s, _ in self.segments]
+            self._bucket_last_seg = {}
+            for i, bkt in enumerate(self._seg_bucket):
+                self._bucket_last_seg[bkt] = i
+
+    def end_training(self):
+        self.reducer = None
+
+    def zero_grad(self):
+        self.flat_grad.zero_()
+        self._captured = None
+
+    def _segment_done(self, seg_index: int, sync: bool):
+        if self.reducer is None or not sync:
+            return
+        bkt = self._seg_bucket[seg_index]
+        if self._bucket_last_seg[bkt] == seg_index:
+            self.reducer.bucket_ready(bkt)
+
+    def _wgrad(self, dy: Tensor, x: Tensor, p: Tensor):
+        self.grad(p).add_(torch.mm(dy.t(), x, out_dtype=torch.float32))
+
+    @torch.no_grad()
+    def train_micro_step(self, idx: Tensor, targets: Tensor, scale: float, sync: bool = True,
+                         capture: bool = False) -> Tensor:
+        """Forward + backward of one micro-batch; gradients accumulate into the flat buffer.
+
+        Returns the (scaled) mean loss as a device scalar.
+        """
+        s = self.spec
+        B, T = idx.shape
+        N, C = B * T, s.C
+        seed = self._step_seed
+        self._step_seed += 1000
+        self._forward(idx, training=True, dropout_seed=seed)
+        cap = capture and self._captured is None
+        if cap:
+            acts = [self.resid[0].view(B, T, C).clone()] * 2 + [r.view(B, T, C).clone() for r in self.resid[1:]] + \
+                   [self.lnf_out.view(B, T, C).float().clone(), self.logits.view(B, T, -1).clone()]
+        # ---- head: CE (in place -> dlogits), lm_head backward, final LN backward
+        rows = fused_ops.cross_entropy_fwd_bwd(self.logits, targets.reshape(-1), scale / N)
+        loss = rows.sum() * (scale / N)
+        torch.mm(self.logits, self.bf16(s.head.weight), out=self.d_c)
+        self._wgrad(self.logits, self.lnf_out, s.head.weight)
+        mean, rstd = self.statsf
+        last = s.blocks[-1]
+        norm_ops.ln_bwd(self.d_c, self.resid[self.L], mean, rstd, s.lnf.weight, self.dresid, False,
+                        self.dresid_bf, self.grad(s.lnf.weight), self.grad(s.lnf.bias), self.grad(last.fc2.bias))
+        grads_cap = []
+        if cap:
+            grads_cap = [self.logits.view(B, T, -1).clone(), self.d_c.view(B, T, C).float().clone(),
+                         self.dresid.view(B, T, C).clone()]
+        self._segment_done(0, sync)
+        for l in range(self.L - 1, -1, -1):
+            b = s.blocks[l]
+            # ---- MLP branch
+            torch.mm(self.dresid_bf, self.bf16(b.fc2.weight), out=self.d_f)
+            self._wgrad(self.dresid_bf, self.fcact[l], b.fc2.weight)
+            act_ops.gelu_bwd(self.d_f, self.fcpre[l], s.gelu_approx, self.grad(b.fc.bias), out=self.d_f)
+            torch.mm(self.d_f, self.bf16(b.fc.weight), out=self.d_c)
+            self._wgrad(self.d_f, self.ln2[l], b.fc.weight)
+            _, _, mean, rstd = self.stats[l]
+            norm_ops.ln_bwd(self.d_c, self.resid_mid[l], mean, rstd, b.ln2.weight, self.dresid, True,
+                            self.dresid_bf, self.grad(b.ln2.weight), self.grad(b.ln2.bias), self.grad(b.proj.bias))
+            # ---- attention branch
+            torch.mm(self.dresid_bf, self.bf16(b.proj.weight), out=self.d_c)
+            self._wgrad(self.dresid_bf, self.att[l], b.proj.weight)
+            attn_ops.flash_bwd(self.d_c.view(B, T, C), self.qkv[l].view(B, T, 3 * C), self.att[l].view(B, T, C),
+                               self.lse[l], s.H, s.H, s.D, b.attn.dropout, seed + l, dqkv=self.dqkv.view(B, T, 3 * C))
+            fused_ops.colsum(self.dqkv, self.grad(b.qkv.bias))
+            torch.mm(self.dqkv, self.bf16(b.qkv.weight), out=self.d_c)
+            self._wgrad(self.dqkv, self.ln1[l], b.qkv.weight)
+            mean, rstd, _, _ = self.stats[l]
+            prev_bias = self.grad(s.blocks[l - 1].fc2.bias) if l > 0 else None
+            norm_ops.ln_bwd(self.d_c, self.resid[l], mean, rstd, b.ln1.weight, self.dresid, True,
+                            self.dresid_bf if l > 0 else None, self.grad(b.ln1.weight), self.grad(b.ln1.bias),
+                            prev_bias)
+            if cap:
+                grads_cap.append(self.dresid.view(B, T, C).clone())
+            self._segment_done(self.L - l, sync)
+        fused_ops.embedding_bwd(self.dresid, idx, self.grad(s.wte.weight), self.grad(s.wpe.weight),
+                                s.wpe.position_offset)
+        self._segment_done(self.L + 1, sync)
+        if sync and self.reducer is not None:
+            self.reducer.finish()
+        if cap:
+            # grads_cap: [dlogits, d_lnf, d_resid[L], d_resid[L-1], ..., d_resid[0]]
+            dlog, dlnf, dres = grads_cap[0], grads_cap[1], grads_cap[2:]
+            dres = list(reversed(dres))  # d_resid[0] ... d_resid[L]
+            act_grads = [dres[0], dres[0]] + dres[1:] + [dlnf, dlog]
+            algos = [l.__class__.__name__.lower() for l in self.model.layers]
+            pairs = list(zip(acts, act_grads))
+            self._captured = (algos, pairs[:len(algos)])
+        return loss
+
+    def optimizer_step(self):
+        opt = self.model.optimizer
+        if self._opt_flat:
+            opt.step()
+        else:
+            opt.step()
+            self.refresh_shadow()
+
+    def captured(self):
+        if self._captured is None:
+            return [l.__class__.__name__.lower() for l in self.model.layers], []
+        return self._captured

@@ -1,0 +1,634 @@
+"""Model runtime: create / persist / import / forward / evaluate / generate / train / diagnose.
+
+API parity with the reference ``NeuralNetworkModel`` (``neural_net_model.py:28-779``) so the
+service layer and checkpoints interoperate: same constructor, attributes (``progress``,
+``avg_cost``, ``avg_cost_history``, ``stats``, ``status``), ``serialize / deserialize /
+delete / from_huggingface``, ``forward(input, target, skip_softmax) -> (activations, cost)``,
+``compute_output``, ``evaluate_model``, ``generate_tokens[_stream]``,
+``train_model_on_device`` (distributed worker entry) and ``train_model``.
+
+Training engines (``PENROZ_ENGINE``, default ``auto``):
+  * ``fused`` — GPT-2-pattern models on GPU lower to :class:`penroz.models.executor.GPTExecutor`
+    (hand-written HIP kernels + hipBLASLt GEMMs, explicit backward, flat fp32 master/grad
+    buffers, fused AdamW, bucketed RCCL all-reduce overlapped with backward);
+  * ``generic`` — any layer list: module forward (HIP kernels through autograd), bf16 autocast
+    on GPU, our bucketed reducer for DDP;
+  * ``reference`` — stock PyTorch eager + autocast + ``torch.nn.parallel.DDP`` + foreach AdamW
+    (the reference's exact semantics; used as the on-device baseline).
+``auto`` = fused when the pattern matches on GPU, else generic.
+
+Semantics kept: ``num_steps = max(1, B·T // (step_size·T·world))`` micro-steps, loss = mean of
+micro-step losses all-reduced as an average, rank data stride ``B·T·rank`` /
+``B·T·world``, progress/stats schemas and caps, status codes, ``speedPerSec = B·T/epoch_secs``
+(rank-0 micro-step view, kept for compatibility) plus a true whole-job ``tokensPerSec``.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import random
+import time
+from contextlib import nullcontext
+from datetime import datetime as dt
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+import torch.nn as nn
+from torch import Tensor
+import torch.distributed as dist
+
+from penroz.models.kv_cache import KVCache, create_kv_cache
+from penroz.models.layers import CausalSelfAttention, PositionEmbedding, SoftmaxOnLast
+from penroz.models.mapper import Mapper
+from penroz.ops import sampling as samp_ops
+from penroz.parallel import dist as ddp
+from penroz.parallel.launcher import maybe_inject_fault
+from penroz.utils import checkpoint as ckpt
+from penroz.utils import diagnostics
+
+log = logging.getLogger(__name__)
+MODELS_FOLDER = ckpt.MODELS_FOLDER
+
+
+def _status(code: str, message: str) -> dict:
+    return {"code": code, "dt": dt.now().isoformat(), "message": message}
+
+
+class NeuralNetworkModel(nn.Module):
+    _detect_shm_path = staticmethod(ckpt.detect_shm_path)
+    SHM_PATH = ckpt.detect_shm_path()
+
+    def __init__(self, model_id: str, mapper: Mapper):
+        super().__init__()
+        self.model_id = model_id
+        self.mapper = mapper
+        self.layers = nn.ModuleList(self.mapper.to_layers())
+        self._is_softmax_last = isinstance(self.layers[-1], nn.Softmax)
+        self.optimizer = self.mapper.to_optimizer(self.parameters())
+        self.progress = []
+        self.avg_cost = None
+        self.avg_cost_history = []
+        self.stats = None
+        self.status = _status("Created", "Model created but not yet trained.")
+        self._executor = None
+
+    # ------------------------------------------------------------------ properties
+    @property
+    def _weights(self) -> list[Tensor | None]:
+        return [p if p.ndim == 2 else None for p in self.parameters()]
+
+    @property
+    def num_params(self) -> int:
+        return sum(p.numel() for p in self.parameters())
+
+    def to(self, device: str = None, dtype: torch.dtype = None):
+        if device is not None:
+            if ddp.is_ddp() and device == "cuda":
+                device = f"cuda:{ddp.ddp_local_rank()}"
+                torch.cuda.set_device(device)
+            super().to(device)
+        if dtype is not None:
+            super().to(dtype=dtype)
+        return self
+
+    # ------------------------------------------------------------------ persistence
+    @classmethod
+    def get_model_path(cls, model_id):
+        return os.path.join(MODELS_FOLDER, f"model_{model_id}.pth")
+
+    def _progress_doc(self) -> dict:
+        return {"progress": self.progress, "average_cost": self.avg_cost,
+                "average_cost_history": self.avg_cost_history, "status": self.status}
+
+    def serialize(self):
+        os.makedirs(MODELS_FOLDER, exist_ok=True)
+        model_path = self.get_model_path(self.model_id)
+        shm_path = os.path.join(self.SHM_PATH, model_path)
+        data = {
+            "layers": self.mapper.layers,
+            "state": {k: v.detach().cpu() for k, v in self.state_dict().items()},
+            "optim": self.mapper.optimizer,
+            "optim_state": _optim_state_to_cpu(self.optimizer.state_dict()),
+            "progress": self.progress,
+            "average_cost": self.avg_cost,
+            "average_cost_history": self.avg_cost_history,
+            "stats": self.stats,
+            "status": self.status,
+        }
+        if ddp.master_proc():
+            log.info(f"Caching model to {shm_path}...")
+        ckpt.atomic_torch_save(data, shm_path)
+        ckpt.atomic_json(self._progress_doc(), ckpt.sidecar_path(shm_path))
+        ckpt.flush_async(shm_path, model_path)
+        ckpt.atomic_json(self._progress_doc(), ckpt.sidecar_path(model_path))
+
+    @classmethod
+    def _ensure_cached(cls, model_id: str) -> str:
+        model_path = cls.get_model_path(model_id)
+        shm_path = os.path.join(cls.SHM_PATH, model_path)
+        if not os.path.exists(shm_path):
+            if ddp.master_proc():
+                log.info(f"Cache miss: copying from {model_path}")
+                ckpt.atomic_copy(model_path, shm_path)
+                side = ckpt.sidecar_path(model_path)
+                if os.path.exists(side):
+                    ckpt.atomic_copy(side, ckpt.sidecar_path(shm_path))
+            if ddp.is_ddp() and dist.is_available() and dist.is_initialized():
+                dist.barrier()
+        return shm_path
+
+    @classmethod
+    def deserialize(cls, model_id: str):
+        try:
+            shm_path = cls._ensure_cached(model_id)
+            data = ckpt.load(shm_path)
+        except FileNotFoundError as e:
+            log.error(f"File not found error occurred: {e}")
+            raise KeyError(f"Model {model_id} not created yet.")
+        model = cls(model_id, Mapper(data["layers"], data["optim"]))
+        saved_dtype = next((v.dtype for v in data["state"].values()
+                            if isinstance(v, Tensor) and v.is_floating_point()), None)
+        if saved_dtype is not None and saved_dtype != torch.float32:
+            model.to(dtype=saved_dtype)
+        model.load_state_dict(data["state"])
+        model.optimizer.load_state_dict(data["optim_state"])
+        model.progress = data["progress"]
+        model.avg_cost = data["average_cost"]
+        model.avg_cost_history = data["average_cost_history"]
+        model.stats = data["stats"]
+        model.status = data["status"]
+        return model
+
+    @classmethod
+    def read_progress(cls, model_id: str) -> dict:
+        """Progress/status without loading weights (sidecar), falling back to the checkpoint."""
+        model_path = cls.get_model_path(model_id)
+        for p in (ckpt.sidecar_path(os.path.join(cls.SHM_PATH, model_path)), ckpt.sidecar_path(model_path)):
+            if os.path.exists(p):
+                import json
+                with open(p) as f:
+                    return json.load(f)
+        m = cls.deserialize(model_id)
+        return m._progress_doc()
+
+    @classmethod
+    def delete(cls, model_id: str):
+        model_path = cls.get_model_path(model_id)
+        shm_path = os.path.join(cls.SHM_PATH, model_path)
+        for p in (shm_path, ckpt.sidecar_path(shm_path), model_path, ckpt.sidecar_path(model_path)):
+            try:
+                os.remove(p)
+            except FileNotFoundError as e:
+                if p == shm_path:
+                    log.warning(f"Failed to delete: {e}")
+
+    @classmethod
+    def from_huggingface(cls, model_id: str, hf_repo_id: str, revision: Optional[str] = None,
+                         device: str = "cpu") -> "NeuralNetworkModel":
+        from transformers import AutoConfig, AutoModelForCausalLM
+        log.info(f"Fetching HuggingFace config for {hf_repo_id} (revision={revision})")
+        hf_config = AutoConfig.from_pretrained(hf_repo_id, revision=revision)
+        hf_model = AutoModelForCausalLM.from_pretrained(hf_repo_id, revision=revision, dtype=torch.bfloat16,
+                                                        low_cpu_mem_usage=True)
+        hf_sd = hf_model.state_dict()
+        del hf_model
+        n_layer = Mapper.detect_hf_n_layer(hf_sd)
+        if n_layer == 0:
+            tc = getattr(hf_config, "text_config", hf_config)
+            n_layer = getattr(tc, "n_layer", None) or getattr(tc, "num_hidden_layers", None)
+        layers = Mapper.from_hf_config(hf_config, n_layer_override=n_layer)
+        mapper = Mapper(layers, {"adamw": {"lr": 6e-4, "betas": [0.9, 0.95], "eps": 1e-8}})
+        model = cls(model_id, mapper)
+        model.to(dtype=torch.bfloat16)
+        model.to(device)
+        model.load_state_dict(Mapper.map_hf_state_dict_to_custom(hf_sd, n_layer, hf_config), strict=True)
+        model.status = _status("Imported", f"Model imported from HuggingFace: {hf_repo_id}")
+        model.serialize()
+        return model
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, input_tensor: Tensor, target: Tensor = None, skip_softmax=False) -> Tuple[list[Tensor], Tensor]:
+        activations = []
+        x = prev = input_tensor
+        layers = self.layers[:-1] if skip_softmax and self._is_softmax_last else self.layers
+        for layer in layers:
+            prev = x
+            x = layer(prev)
+            activations.append(x)
+        if target is None:
+            cost = torch.empty(0)
+        elif self._is_softmax_last:
+            logits = x if skip_softmax else prev
+            if logits.ndim > 2 and target.ndim > 1:
+                logits = logits.reshape(-1, logits.size(-1))
+                target = target.reshape(-1)
+            cost = nn.functional.cross_entropy(logits, target)
+        else:
+            cost = nn.functional.mse_loss(x, target)
+        return activations, cost
+
+    @torch.no_grad()
+    def compute_output(self, input_data: list, target: list | int | None = None) -> Tuple[list, float | None]:
+        self.eval()
+        p0 = next(self.parameters())
+        x = torch.tensor(input_data, device=p0.device)
+        if x.is_floating_point():
+            x = x.to(p0.dtype)
+        if target is not None:
+            target = torch.tensor(target, device=p0.device)
+            if target.is_floating_point():
+                target = target.to(p0.dtype)
+        activations, cost = self(x, target)
+        return activations[-1].float().tolist(), (cost.item() if cost.numel() > 0 else None)
+
+    # ------------------------------------------------------------------ evaluation
+    @torch.no_grad()
+    def evaluate_model(self, dataset_id: str, target_dataset_id: str | None, shard: int,
+                       epochs: int, batch_size: int, block_size: int, step_size: int) -> float:
+        from penroz.utils.loaders import Loader
+        self.eval()
+        buffer_size = batch_size * block_size
+        world = ddp.ddp_world_size()
+        num_steps = max(1, buffer_size // (step_size * block_size * world))
+        begin_idx, idx_offset = buffer_size * ddp.ddp_rank(), buffer_size * world
+        loader = Loader(dataset_id, shard, begin_idx, buffer_size, idx_offset)
+        target_loader = Loader(target_dataset_id, shard, begin_idx, buffer_size, idx_offset) \
+            if target_dataset_id is not None else None
+        device = next(self.parameters()).device
+        executor = self._get_executor(device)
+        total = torch.zeros((), device=device, dtype=torch.float32)
+        for _ in range(epochs):
+            if target_loader is None:
+                inp, tgt = loader.next_batch()
+            else:
+                inp, _ = loader.next_batch(target_offset=0)
+                tgt, _ = target_loader.next_batch(target_offset=0)
+            x = torch.as_tensor(np.asarray(inp), dtype=torch.long).view(batch_size, block_size).to(device)
+            y = torch.as_tensor(np.asarray(tgt), dtype=torch.long).view(batch_size, block_size).to(device)
+            for _ in range(num_steps):
+                if executor is not None:
+                    step_cost = executor.eval_loss(x, y)
+                else:
+                    with self._autocast(device):
+                        _, step_cost = self(x, y, skip_softmax=True)
+                total += step_cost.float() / (epochs * num_steps)
+        if ddp.use_ddp(device.type) and dist.is_initialized():
+            ddp.ddp_all_reduce(total)
+        avg = total.item()
+        if ddp.master_proc():
+            log.info(f"Model {self.model_id}: For {epochs} evaluation(s) Avg Cost: {avg:.4f}")
+        return avg
+
+    # ------------------------------------------------------------------ generation
+    def _find_attention_layers(self) -> list[CausalSelfAttention]:
+        return [m for m in self.modules() if isinstance(m, CausalSelfAttention)]
+
+    def _find_position_embeddings(self) -> list[PositionEmbedding]:
+        return [m for m in self.modules() if isinstance(m, PositionEmbedding)]
+
+    def _attach_kv_cache(self, capacity: int | None = None) -> tuple[KVCache | None, list[PositionEmbedding]]:
+        attn = self._find_attention_layers()
+        pos = self._find_position_embeddings()
+        if not attn:
+            return None, pos
+        cache = create_kv_cache(len(attn), capacity)
+        for i, a in enumerate(attn):
+            a.set_kv_cache(cache, i)
+        return cache, pos
+
+    def _detach_kv_cache(self, pos_embeddings=None):
+        for a in self._find_attention_layers():
+            a.set_kv_cache(None, 0)
+        for p in (pos_embeddings or self._find_position_embeddings()):
+            p.position_offset = 0
+
+    def _prepare_generation(self, input_context: list, max_new_tokens: int, temperature: float, top_k: int | None):
+        self.eval()
+        device = next(self.parameters()).device
+        context = torch.tensor(input_context, dtype=torch.long, device=device)
+        if context.ndim == 1:
+            context = context.unsqueeze(0)
+        top_k_msg = "" if top_k is None else f" top {top_k}"
+        log.info(f"Generating at most {max_new_tokens}{top_k_msg} tokens with {temperature} temperature "
+                 f"using device {device}")
+        softmax_layer = self.layers[-1] if self._is_softmax_last else SoftmaxOnLast(dim=-1)
+        return context, softmax_layer
+
+    @torch.inference_mode()
+    def _generate_next_token(self, context: Tensor, block_size: int, temperature: float, top_k: int | None,
+                             softmax_layer=None, kv_cache: KVCache | None = None,
+                             pos_embeddings: list[PositionEmbedding] | None = None) -> Tensor:
+        if kv_cache is not None and kv_cache.seq_len() > 0:
+            if kv_cache.seq_len() >= block_size:
+                # sliding window: clear and re-prefill the last block_size tokens
+                kv_cache.clear()
+                model_input = context[:, -block_size:]
+                for p in (pos_embeddings or []):
+                    p.position_offset = 0
+            else:
+                model_input = context[:, -1:]
+                for p in (pos_embeddings or []):
+                    p.position_offset = kv_cache.seq_len()
+        else:
+            model_input = context[:, -block_size:]
+        activations, _ = self(model_input, skip_softmax=True)
+        logits = activations[-1]
+        last = logits[:, -1, :] if logits.ndim == 3 else logits
+        return samp_ops.sample(last, temperature, top_k)
+
+    @torch.inference_mode()
+    def generate_tokens(self, input_context: list, block_size: int, max_new_tokens: int,
+                        temperature=1.0, top_k: int | None = None, stop_token: int | None = None) -> list:
+        return [t for t in self._generate(input_context, block_size, max_new_tokens, temperature, top_k,
+                                          stop_token, full_context=True)][-1]
+
+    @torch.inference_mode()
+    def generate_tokens_stream(self, input_context: list, block_size: int, max_new_tokens: int,
+                               temperature=1.0, top_k: int | None = None, stop_token: int | None = None):
+        log.info("Streaming token generation started")
+        for tok in self._generate(input_context, block_size, max_new_tokens, temperature, top_k, stop_token,
+                                  full_context=False):
+            yield tok
+        log.info("Streaming token generation completed")
+
+    def _generate(self, input_context, block_size, max_new_tokens, temperature, top_k, stop_token, full_context):
+        context, softmax_layer = self._prepare_generation(input_context, max_new_tokens, temperature, top_k)
+        cache, pos = self._attach_kv_cache(capacity=block_size)
+        rows = context.shape[0]
+        generated = []
+        done = torch.zeros(rows, dtype=torch.bool)
+        try:
+            with torch.inference_mode():
+                for _ in range(max_new_tokens):
+                    nxt = self._generate_next_token(context, block_size, temperature, top_k, softmax_layer, cache, pos)
+                    context = torch.cat((context, nxt.to(context.device)), dim=1)
+                    toks = nxt.view(-1).tolist()
+                    generated.append(toks[0])
+                    if not full_context:
+                        yield toks[0]
+                    if stop_token is not None:
+                        done |= torch.tensor([t == stop_token for t in toks])
+                        if bool(done[0]) and (rows == 1 or bool(done.all())):
+                            break
+        finally:
+            if cache is not None:
+                cache.log_metrics()
+            self._detach_kv_cache(pos)
+        if full_context:
+            yield context[0].tolist()
+
+    @torch.inference_mode()
+    def generate_batch(self, input_context: list, block_size: int, max_new_tokens: int, temperature=1.0,
+                       top_k: int | None = None, stop_token: int | None = None) -> list[list[int]]:
+        """All rows' contexts (the reference returns row 0 only — bug 5)."""
+        context, sm = self._prepare_generation(input_context, max_new_tokens, temperature, top_k)
+        cache, pos = self._attach_kv_cache(capacity=block_size)
+        try:
+            for _ in range(max_new_tokens):
+                nxt = self._generate_next_token(context, block_size, temperature, top_k, sm, cache, pos)
+                context = torch.cat((context, nxt.to(context.device)), dim=1)
+                if stop_token is not None and bool((nxt == stop_token).all()):
+                    break
+        finally:
+            self._detach_kv_cache(pos)
+        return context.tolist()
+
+    # ------------------------------------------------------------------ training
+    @classmethod
+    def train_model_on_device(cls, model_id: str, device: str, dataset_id: str, shard: int,
+                              epochs: int, batch_size: int, block_size: int, step_size: int):
+        if ddp.is_ddp():
+            ddp.reconfig_logging()
+            log.info(f"DDP local rank {ddp.ddp_local_rank()} - training model {model_id} on device {device} "
+                     f"with backend {ddp.backend_for(device)}")
+            if str(device).startswith("cuda"):
+                torch.cuda.set_device(ddp.ddp_local_rank())
+            ddp.init_process_group(device)
+        model = cls.deserialize(model_id)
+        model.to(device)
+        actual = next(model.parameters()).device
+        for state in model.optimizer.state.values():
+            for k, v in state.items():
+                if isinstance(v, Tensor) and k != "step":
+                    state[k] = v.to(actual)
+        try:
+            model.train_model(dataset_id, shard, epochs, batch_size, block_size, step_size)
+        finally:
+            ckpt.wait_flushes()
+            if ddp.is_ddp() and dist.is_initialized():
+                dist.destroy_process_group()
+
+    @staticmethod
+    def _autocast(device):
+        if device.type == "cuda":
+            return torch.amp.autocast("cuda", dtype=torch.bfloat16)
+        return nullcontext()
+
+    def _engine(self, device) -> str:
+        eng = os.environ.get("PENROZ_ENGINE", "auto")
+        if eng == "auto":
+            from penroz.models.executor import GPTExecutor
+            return "fused" if device.type == "cuda" and GPTExecutor.match(self) is not None else "generic"
+        return eng
+
+    def _get_executor(self, device):
+        if device.type != "cuda" or self._engine(device) != "fused":
+            return None
+        from penroz.models.executor import GPTExecutor
+        if self._executor is None or self._executor.device != device:
+            self._executor = GPTExecutor(self, device)
+        return self._executor
+
+    def train_model(self, dataset_id: str, shard: int, epochs: int, batch_size: int, block_size: int,
+                    step_size: int):
+        from penroz.utils.loaders import Loader
+        device = next(self.parameters()).device
+        engine = self._engine(device)
+        if ddp.master_proc():
+            log.info(f"Training model using device {device} (engine {engine})")
+        world = ddp.ddp_world_size()
+        buffer_size = batch_size * block_size
+        num_steps = max(1, buffer_size // (step_size * block_size * world))
+        begin_idx, idx_offset = buffer_size * ddp.ddp_rank(), buffer_size * world
+        log.info(f"Training starts from idx {begin_idx} of ds {dataset_id} at shard {shard} offset every {idx_offset}")
+        loader = Loader(dataset_id, begin_shard=shard, begin_idx=begin_idx, buffer_size=buffer_size,
+                        idx_offset=idx_offset)
+
+        self.progress = []
+        self.stats = None
+        self.status = _status("Training", "Model is currently being trained.")
+        last_serialized = None
+        if ddp.master_proc():
+            self.serialize()
+            last_serialized = time.time()
+
+        distributed = ddp.use_ddp(device.type) and dist.is_initialized()
+        runner = _make_runner(self, engine, device, distributed)
+        self.train()
+
+        for epoch in range(epochs):
+            t0 = time.time()
+            long_training = last_serialized is not None and (t0 - last_serialized >= 10)
+            capture = ddp.master_proc() and (epoch + 1 == epochs or long_training)
+            prev = [w.detach().clone() if w is not None else None for w in self._weights] \
+                if ddp.master_proc() else []
+            runner.zero_grad()
+            cost = torch.zeros((), device=device, dtype=torch.float32)
+            try:
+                for step in range(num_steps):
+                    maybe_inject_fault(epoch * num_steps + step)
+                    inp, tgt = loader.next_batch()
+                    x = torch.as_tensor(np.asarray(inp), dtype=torch.long).view(batch_size, block_size)
+                    y = torch.as_tensor(np.asarray(tgt), dtype=torch.long).view(batch_size, block_size)
+                    if device.type == "cuda":
+                        x, y = x.pin_memory().to(device, non_blocking=True), y.pin_memory().to(device, non_blocking=True)
+                    else:
+                        x, y = x.to(device), y.to(device)
+                    cost += runner.micro_step(x, y, 1.0 / num_steps, first=step == 0,
+                                              last=step == num_steps - 1, capture=capture)
+            except Exception as exc:
+                if ddp.master_proc():
+                    log.error(f"Model {self.model_id}: Training Epoch {epoch + 1} failed: {exc}")
+                    self.status = _status("Error", f"Training epoch {epoch + 1} failed: {exc}")
+                    self.serialize()
+                raise
+            if distributed:
+                ddp.ddp_all_reduce(cost)
+            runner.step()
+            if device.type == "cuda":
+                torch.cuda.synchronize()
+            if ddp.master_proc():
+                secs = time.time() - t0
+                progress_cost = cost.item()
+                if epoch % max(1, epochs // 100) == 0:
+                    self.progress.append({
+                        "dt": dt.now().isoformat(), "epoch": epoch + 1, "durationInSecs": secs,
+                        "speedPerSec": buffer_size / secs,
+                        "tokensPerSec": num_steps * world * buffer_size / secs,
+                        "cost": progress_cost,
+                        "weight_upd_ratio": diagnostics.weight_update_ratios(prev, self._weights),
+                    })
+                log.info(f"Model {self.model_id}: Training Epoch {epoch + 1}, Cost: {progress_cost:.4f}, "
+                         f"Duration: {secs:.2f} secs, Speed: {buffer_size / secs:.2f} tokens/sec")
+            if ddp.master_proc() and long_training:
+                self._record_training_overall_progress(runner.captured())
+                self.serialize()
+                last_serialized = time.time()
+
+        if ddp.master_proc():
+            self.status = _status("Trained", f"Model trained for {epochs} epochs.")
+            log.info(f"Model {self.model_id}: Done training for {epochs} epochs.")
+            self._record_training_overall_progress(runner.captured())
+            self.serialize()
+        runner.close()
+
+    @torch.no_grad()
+    def _record_training_overall_progress(self, captured):
+        costs = [p["cost"] for p in self.progress]
+        avg_progress_cost = sum(costs) / len(costs) if costs else 0.0
+        self.avg_cost = ((self.avg_cost or avg_progress_cost) + avg_progress_cost) / 2.0
+        self.avg_cost_history.append(self.avg_cost)
+        if len(self.avg_cost_history) > 100:
+            self.avg_cost_history.pop(random.randint(1, 98))
+        algos, acts = captured
+        self.stats = diagnostics.training_stats(algos, acts, self._weights)
+        log.info(f"Model {self.model_id} - Cost: {avg_progress_cost:.4f} Overall Cost: {self.avg_cost:.4f}")
+
+
+def _optim_state_to_cpu(sd: dict) -> dict:
+    out = {"state": {}, "param_groups": sd["param_groups"]}
+    for k, st in sd["state"].items():
+        out["state"][k] = {n: (v.detach().cpu().clone() if isinstance(v, Tensor) else v) for n, v in st.items()}
+    return out
+
+
+# ---------------------------------------------------------------------------- step runners
+class _GenericRunner:
+    """Module forward + autograd backward (+ our bucketed reducer under DDP)."""
+
+    def __init__(self, model: NeuralNetworkModel, device, distributed: bool, reference: bool = False):
+        self.model = model
+        self.device = device
+        self.reference = reference
+        self.amp = NeuralNetworkModel._autocast(device)
+        self.reducer = None
+        self.ddp_model = None
+        if distributed:
+            if reference:
+                self.ddp_model = nn.parallel.DistributedDataParallel(model)
+            else:
+                from penroz.parallel.reducer import HookedReducer
+                self._broadcast_params()
+                self.reducer = HookedReducer(list(model.parameters()))
+        self._acts: list[Tensor] = []
+        self._algos = [l.__class__.__name__.lower() for l in model.layers]
+
+    def _broadcast_params(self):
+        for p in self.model.parameters():
+            dist.broadcast(p.data, src=0)
+
+    def zero_grad(self):
+        if self.reducer is not None:
+            self.reducer.zero_grad()
+        else:
+            self.model.optimizer.zero_grad()
+        self._acts = []
+
+    def micro_step(self, x, y, scale, first, last, capture):
+        fwd = self.ddp_model if self.ddp_model is not None else self.model
+        if self.ddp_model is not None:
+            self.ddp_model.require_backward_grad_sync = last
+        if self.reducer is not None:
+            self.reducer.sync = last
+        with self.amp if self.device.type == "cuda" else nullcontext():
+            acts, loss = fwd(x, y, skip_softmax=True)
+            scaled = loss * scale if scale != 1.0 else loss
+        if capture:
+            for a in acts:
+                a.retain_grad()
+            self._acts.extend(acts)
+        scaled.backward()
+        if last and self.reducer is not None:
+            self.reducer.finish()
+        return scaled.detach().float()
+
+    def step(self):
+        self.model.optimizer.step()
+
+    def captured(self):
+        return self._algos, [(a, a.grad) for a in self._acts[:len(self._algos)]] if self._acts else []
+
+    def close(self):
+        if self.reducer is not None:
+            self.reducer.remove()
+
+
+class _FusedRunner:
+    def __init__(self, model: NeuralNetworkModel, device, distributed: bool):
+        self.model = model
+        self.exec = model._get_executor(device)
+        self.exec.setup_training(distributed)
+
+    def zero_grad(self):
+        self.exec.zero_grad()
+
+    def micro_step(self, x, y, scale, first, last, capture):
+        return self.exec.train_micro_step(x, y, scale, sync=last, capture=capture)
+
+    def step(self):
+        self.exec.optimizer_step()
+
+    def captured(self):
+        return self.exec.captured()
+
+    def close(self):
+        self.exec.end_training()
+
+
+def _make_runner(model, engine, device, distributed):
+    from penroz.ops import _ext
+    _ext.FORCE_TORCH = engine == "reference"
+    if engine == "fused":
+        return _FusedRunner(model, device, distributed)
+    return _GenericRunner(model, device, distributed, reference=(engine == "reference"))

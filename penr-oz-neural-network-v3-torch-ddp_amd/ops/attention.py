@@ -1,0 +1,142 @@
+"""Causal self-attention over a fused QKV tensor, and KV-cache (decode) attention.
+
+GPU: hand-written CDNA4 flash attention (``csrc/kernels/flash_attn.hip``):
+  * forward reads Q/K/V straight out of the fused ``[B, T, (H + 2·Hkv)·D]`` projection (no
+    split/transpose copies), keeps Q in registers, stages K/V tiles through XOR-swizzled LDS,
+    computes Sᵀ = K·Qᵀ with ``v_mfma_f32_32x32x16_bf16`` so each lane owns one query row's
+    scores (softmax in registers, one cross-half exchange), feeds P straight from the
+    accumulators into Oᵀ = Vᵀ·Pᵀ (V read with ``ds_read_b64_tr_b16``), and writes O already
+    head-merged ``[B, T, H·D]`` plus the row log-sum-exp;
+  * backward keeps each wave's 32 keys (K, V, dKᵀ, dVᵀ) in registers while sweeping the query
+    blocks; dQ is accumulated with fp32 atomics and converted once.
+  GQA is handled by index math (kv head = q head // group) — K/V are never expanded.
+  Dropout (``attn_pdrop``) uses a counter-based hash RNG regenerated in the backward pass.
+CPU: ``torch.nn.functional.scaled_dot_product_attention`` (math) with GQA expansion.
+
+Replaces the reference's SDPA call (``neural_net_layers.py:59-95``).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+from torch import Tensor
+import torch.nn.functional as F
+
+from penroz.ops._ext import use_kernels, kernels
+
+SUPPORTED_HEAD_DIMS = (64, 128)
+
+
+def reference_causal_attention_qkv(qkv: Tensor, H: int, Hkv: int, D: int, dropout_p: float = 0.0) -> Tensor:
+    B, T, _ = qkv.shape
+    q, k, v = qkv.split([H * D, Hkv * D, Hkv * D], dim=2)
+    q = q.reshape(B, T, H, D).transpose(1, 2)
+    k = k.reshape(B, T, Hkv, D).transpose(1, 2)
+    v = v.reshape(B, T, Hkv, D).transpose(1, 2)
+    if Hkv < H:
+        rep = H // Hkv
+        k = k.repeat_interleave(rep, dim=1)
+        v = v.repeat_interleave(rep, dim=1)
+    o = F.scaled_dot_product_attention(q, k, v, dropout_p=dropout_p, is_causal=True)
+    return o.transpose(1, 2).reshape(B, T, H * D)
+
+
+def reference_attention_lse(qkv: Tensor, H: int, Hkv: int, D: int):
+    """fp32 math reference returning (out [B,T,H*D], lse [B,H,T]) for kernel parity tests."""
+    B, T, _ = qkv.shape
+    q, k, v = qkv.float().split([H * D, Hkv * D, Hkv * D], dim=2)
+    q = q.reshape(B, T, H, D).transpose(1, 2)
+    k = k.reshape(B, T, Hkv, D).transpose(1, 2).repeat_interleave(H // Hkv, dim=1)
+    v = v.reshape(B, T, Hkv, D).transpose(1, 2).repeat_interleave(H // Hkv, dim=1)
+    s = (q @ k.transpose(-1, -2)) / math.sqrt(D)
+    mask = torch.ones(T, T, dtype=torch.bool, device=qkv.device).triu(1)
+    s = s.masked_fill(mask, float("-inf"))
+    lse = torch.logsumexp(s, dim=-1)
+    p = torch.softmax(s, dim=-1)
+    o = p @ v
+    return o.transpose(1, 2).reshape(B, T, H * D), lse
+
+
+def flash_fwd(qkv: Tensor, H: int, Hkv: int, D: int, dropout_p: float = 0.0, seed: int = 0,
+              out: Tensor | None = None, lse: Tensor | None = None):
+    """bf16 qkv [B,T,(H+2Hkv)D] -> (out bf16 [B,T,H*D], lse f32 [B,H,T])."""
+    B, T, _ = qkv.shape
+    out = torch.empty(B, T, H * D, dtype=torch.bfloat16, device=qkv.device) if out is None else out
+    lse = torch.empty(B, H, T, dtype=torch.float32, device=qkv.device) if lse is None else lse
+    kernels().flash_attn_fwd(qkv, out, lse, H, Hkv, D, 1.0 / math.sqrt(D), float(dropout_p), int(seed))
+    return out, lse
+
+
+def flash_bwd(dout: Tensor, qkv: Tensor, out: Tensor, lse: Tensor, H: int, Hkv: int, D: int,
+              dropout_p: float = 0.0, seed: int = 0, dqkv: Tensor | None = None) -> Tensor:
+    """-> dqkv bf16 [B,T,(H+2Hkv)D] (written into ``dqkv`` when given)."""
+    dqkv = torch.empty_like(qkv) if dqkv is None else dqkv
+    kernels().flash_attn_bwd(dout, qkv, out, lse, dqkv, H, Hkv, D, 1.0 / math.sqrt(D), float(dropout_p), int(seed))
+    return dqkv
+
+
+def new_seed() -> int:
+    return int(torch.randint(0, 2**31 - 1, (1,)).item())
+
+
+class _FlashAttnFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, H, Hkv, D, dropout_p):
+        in_dtype = qkv.dtype
+        x = qkv.to(torch.bfloat16).contiguous()
+        seed = new_seed() if dropout_p > 0 else 0
+        out, lse = flash_fwd(x, H, Hkv, D, dropout_p, seed)
+        ctx.save_for_backward(x, out, lse)
+        ctx.meta = (H, Hkv, D, dropout_p, seed, in_dtype)
+        return out if in_dtype == torch.bfloat16 else out.to(in_dtype)
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, out, lse = ctx.saved_tensors
+        H, Hkv, D, p, seed, in_dtype = ctx.meta
+        dqkv = flash_bwd(dout.to(torch.bfloat16).contiguous(), x, out, lse, H, Hkv, D, p, seed)
+        return dqkv.to(in_dtype), None, None, None, None
+
+
+def causal_attention_qkv(qkv: Tensor, H: int, Hkv: int, D: int, dropout_p: float = 0.0) -> Tensor:
+    """Causal attention of a fused-QKV tensor ``[B, T, (H + 2·Hkv)·D]`` -> ``[B, T, H·D]``."""
+    if use_kernels(qkv) and D in SUPPORTED_HEAD_DIMS:
+        return _FlashAttnFn.apply(qkv, H, Hkv, D, dropout_p)
+    return reference_causal_attention_qkv(qkv, H, Hkv, D, dropout_p)
+
+
+# --------------------------------------------------------------------------- decode / cache
+def reference_cache_attention(q: Tensor, k: Tensor, v: Tensor, q_offset: int) -> Tensor:
+    """q [B,Tq,H,D], k/v [B,Hkv,S,D] (S = q_offset + Tq); query i sits at q_offset + i."""
+    B, Tq, H, D = q.shape
+    Hkv, S = k.shape[1], k.shape[2]
+    qh = q.transpose(1, 2).float()
+    kh = k.float().repeat_interleave(H // Hkv, dim=1)
+    vh = v.float().repeat_interleave(H // Hkv, dim=1)
+    s = (qh @ kh.transpose(-1, -2)) / math.sqrt(D)
+    qpos = torch.arange(q_offset, q_offset + Tq, device=q.device).unsqueeze(1)
+    kpos = torch.arange(S, device=q.device).unsqueeze(0)
+    s = s.masked_fill(kpos > qpos, float("-inf"))
+    o = torch.softmax(s, dim=-1) @ vh
+    return o.transpose(1, 2).reshape(B, Tq, H * D).to(q.dtype)
+
+
+def decode_attention(q: Tensor, k_cache: Tensor, v_cache: Tensor, seq_len: int,
+                     k_scale: Tensor | None = None, v_scale: Tensor | None = None) -> Tensor:
+    """Attention of ``q [B, Tq, H, D]`` against the first ``seq_len`` cache slots.
+
+    Cache layout ``[B, Hkv, cap, D]`` (bf16/fp16/fp32, or int8 with per-token fp32 scales
+    ``[B, Hkv, cap]`` — TurboQuant; dequantisation fused into the kernel).
+    GPU: split-K decode kernel (``csrc/kernels/decode_attn.hip``).
+    """
+    Tq = q.shape[1]
+    if use_kernels(q):
+        return kernels().decode_attn(q.contiguous(), k_cache, v_cache, k_scale, v_scale, int(seq_len),
+                                     int(seq_len - Tq), 1.0 / math.sqrt(q.shape[-1]))
+    k = k_cache[:, :, :seq_len]
+    v = v_cache[:, :, :seq_len]
+    if k_scale is not None:
+        k = k.float() * k_scale[:, :, :seq_len, None]
+        v = v.float() * v_scale[:, :, :seq_len, None]
+    return reference_cache_attention(q, k, v, seq_len - Tq)

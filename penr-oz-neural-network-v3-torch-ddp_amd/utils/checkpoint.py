@@ -1,0 +1,91 @@
+"""Checkpoint IO: atomic writes, shared-memory cache, background disk flush, progress sidecar.
+
+Format parity with the reference (``neural_net_model.py:98-174``): ``torch.save`` of a dict
+with ``layers, state, optim, optim_state, progress, average_cost, average_cost_history,
+stats, status`` at ``models/model_{id}.pth``, cached under ``{SHM}/models/``.
+
+Fixes (SURVEY §5.2/§7.4 bug 10): every write goes to a temp file + ``os.replace`` (readers
+never see a torn checkpoint); the disk flush copies atomically on a background *thread*
+(never a fork of a GPU-initialised process); a small JSON sidecar carries progress/status so
+``/progress`` does not ``torch.load`` a multi-GB file.  Loads use ``weights_only=True``.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+import platform
+import shutil
+import tempfile
+import threading
+
+import torch
+
+log = logging.getLogger(__name__)
+
+MODELS_FOLDER = "models"
+
+
+def detect_shm_path() -> str:
+    system = platform.system()
+    if system == "Linux":
+        if os.path.isdir("/dev/shm") and os.access("/dev/shm", os.W_OK):
+            return "/dev/shm"
+    elif system == "Darwin":
+        if os.path.isdir("/Volumes/RAMDisk") and os.access("/Volumes/RAMDisk", os.W_OK):
+            return "/Volumes/RAMDisk"
+    return tempfile.gettempdir()
+
+
+def _atomic_write(path: str, writer):
+    d = os.path.dirname(path) or "."
+    os.makedirs(d, exist_ok=True)
+    fd, tmp = tempfile.mkstemp(prefix=".tmp_", dir=d)
+    os.close(fd)
+    try:
+        writer(tmp)
+        os.replace(tmp, path)
+    except BaseException:
+        if os.path.exists(tmp):
+            os.remove(tmp)
+        raise
+
+
+def atomic_torch_save(obj, path: str):
+    _atomic_write(path, lambda tmp: torch.save(obj, tmp, pickle_protocol=5))
+
+
+def atomic_copy(src: str, dst: str):
+    _atomic_write(dst, lambda tmp: shutil.copyfile(src, tmp))
+
+
+def atomic_json(obj, path: str):
+    def w(tmp):
+        with open(tmp, "w") as f:
+            json.dump(obj, f)
+    _atomic_write(path, w)
+
+
+_flushers: list[threading.Thread] = []
+
+
+def flush_async(src: str, dst: str) -> threading.Thread:
+    t = threading.Thread(target=atomic_copy, args=(src, dst), name=f"flush-{os.path.basename(dst)}")
+    t.start()
+    _flushers.append(t)
+    _flushers[:] = [x for x in _flushers if x.is_alive()]
+    return t
+
+
+def wait_flushes():
+    for t in list(_flushers):
+        t.join()
+    _flushers.clear()
+
+
+def sidecar_path(pth_path: str) -> str:
+    return pth_path[:-4] + ".progress.json" if pth_path.endswith(".pth") else pth_path + ".progress.json"
+
+
+def load(path: str) -> dict:
+    return torch.load(path, weights_only=True, map_location="cpu")

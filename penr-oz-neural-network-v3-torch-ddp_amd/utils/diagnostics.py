@@ -1,0 +1,87 @@
+"""Training diagnostics for the dashboard: weight-update ratios and layer/weight statistics.
+
+Schema parity with the reference (``neural_net_model.py:690-700, 735-777``):
+``weight_upd_ratio`` = std(Δw)/(std(w)+1e-8) per 2-D weight (None otherwise);
+stats = ``{"layers": [{algo, activation: {mean, std, saturated, histogram: {x, y}},
+gradient: {mean, std, histogram} | None}], "weights": [{shape, data: {mean, std},
+gradient: {mean, std, histogram}} | None]}`` with 100-bin density histograms and the same
+per-algo saturation rules.
+
+MI355X-first: every statistic is computed on the device (``tensor_stats`` HIP kernel: one
+fused moments + min/max pass and one histogram pass) and copied back in ONE transfer per
+tensor; the reference does ``torch.histogram(a.cpu())`` — including a full copy of the
+``[B, T, V]`` logits to the host — and one ``.item()`` sync per weight.
+"""
+from __future__ import annotations
+
+import torch
+from torch import Tensor
+
+from penroz.ops import fused as fused_ops
+
+
+@torch.no_grad()
+def weight_update_ratios(prev: list, weights: list) -> list:
+    vals = []
+    idx = []
+    for i, (pw, w) in enumerate(zip(prev, weights)):
+        if pw is None or w is None:
+            continue
+        vals.append(torch.stack([(w - pw).float().std(), w.float().std()]))
+        idx.append(i)
+    out: list = [None] * len(weights)
+    if vals:
+        host = torch.stack(vals).cpu().tolist()
+        for i, (d, s) in zip(idx, host):
+            out[i] = d / (s + 1e-8)
+    return out
+
+
+def _hist(x: Tensor, bins: int = 100):
+    mean, std, mn, mx, hist, edges = fused_ops.tensor_stats(x, bins)
+    return float(mean), float(std), edges[:-1].tolist(), hist.tolist()
+
+
+@torch.no_grad()
+def _saturation(algo: str, a: Tensor) -> float:
+    a = a.float()
+    if algo == "embedding":
+        sat = torch.norm(a, dim=-1) > 5.0
+    elif algo == "batchnorm1d":
+        sat = a.abs() > 3.0
+    elif algo in ("tanh", "sigmoid"):
+        sat = a.abs() > 0.97
+    elif algo == "relu":
+        sat = a <= 0
+    elif algo == "softmax":
+        sat = a.max(dim=-1).values > 0.97
+    else:
+        sat = a.abs() > 5.0
+    return float(sat.float().mean())
+
+
+@torch.no_grad()
+def training_stats(algos: list[str], acts: list, weights: list) -> dict:
+    layers = []
+    for algo, pair in zip(algos, acts):
+        a, g = pair
+        mean, std, hx, hy = _hist(a)
+        entry = {"algo": algo, "activation": {"mean": mean, "std": std, "saturated": _saturation(algo, a),
+                                               "histogram": {"x": hx, "y": hy}},
+                 "gradient": None}
+        if g is not None:
+            gm, gs, gx, gy = _hist(g)
+            entry["gradient"] = {"mean": gm, "std": gs, "histogram": {"x": gx, "y": gy}}
+        layers.append(entry)
+    wstats = []
+    for w in weights:
+        if w is None:
+            wstats.append(None)
+            continue
+        wm, ws = float(w.float().mean()), float(w.float().std())
+        grad = {"mean": None, "std": None, "histogram": {"x": [], "y": []}}
+        if w.grad is not None:
+            gm, gs, gx, gy = _hist(w.grad)
+            grad = {"mean": gm, "std": gs, "histogram": {"x": gx, "y": gy}}
+        wstats.append({"shape": str(tuple(w.shape)), "data": {"mean": wm, "std": ws}, "gradient": grad})
+    return {"layers": layers, "weights": wstats}

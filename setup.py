@@ -1,0 +1,110 @@
+"""Build the penroz native extensions in-tree for gfx950 with hipcc (no hipify, no CUDA).
+
+    python setup.py build_ext        # -> build_ext/penroz_kernels*.so, build_ext/penroz_comm*.so
+
+Each ``csrc/kernels/*.hip`` is compiled with ``hipcc --offload-arch=gfx950`` in parallel and
+linked together with the pybind11 bindings against PyTorch's own libraries (including the
+HIP runtime PyTorch bundles, so exactly one ``libamdhip64`` is mapped in the process).
+``csrc/comm/*.cpp`` (RCCL communicator) links PyTorch's bundled ``librccl``.
+Objects are rebuilt only when a source or header is newer.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+import sysconfig
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(ROOT, "csrc")
+OUT = os.path.join(ROOT, "build_ext")
+OBJ = os.path.join(OUT, "obj")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+
+
+def _torch_paths():
+    import torch
+    from torch.utils import cpp_extension as ce
+    tdir = os.path.dirname(torch.__file__)
+    return ce.include_paths(), os.path.join(tdir, "lib"), int(torch._C._GLIBCXX_USE_CXX11_ABI)
+
+
+def _flags(name: str):
+    incs, _, abi = _torch_paths()
+    py_inc = sysconfig.get_paths()["include"]
+    f = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-D__HIP_PLATFORM_AMD__=1",
+         "-DUSE_ROCM=1", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", f"-DTORCH_EXTENSION_NAME={name}",
+         "-DTORCH_API_INCLUDE_EXTENSION_H", "-Wno-unused-result", "-Wno-unused-variable",
+         "-Wno-deprecated-declarations", f"-I{py_inc}", f"-I{CSRC}", f"-I{os.path.join(CSRC, 'kernels')}"]
+    f += [f"-I{p}" for p in incs]
+    return f
+
+
+def _ext_suffix() -> str:
+    return sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def _newer(src: str, obj: str, deps: list[str]) -> bool:
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    return any(os.path.getmtime(d) > t for d in [src] + deps)
+
+
+def _compile(src: str, obj: str, flags: list[str]):
+    cmd = [HIPCC] + flags + ["-c", src, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {src}\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return obj
+
+
+def build_module(name: str, sources: list[str], extra_libs: list[str], jobs: int) -> str:
+    os.makedirs(OBJ, exist_ok=True)
+    flags = _flags(name)
+    headers = [os.path.join(CSRC, "kernels", h) for h in os.listdir(os.path.join(CSRC, "kernels")) if h.endswith(".h")]
+    todo = []
+    objs = []
+    for s in sources:
+        obj = os.path.join(OBJ, f"{name}__{os.path.basename(s)}.o")
+        objs.append(obj)
+        if _newer(s, obj, headers):
+            todo.append((s, obj))
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        for fut in cf.as_completed([ex.submit(_compile, s, o, flags) for s, o in todo]):
+            print(f"[build] compiled {os.path.basename(fut.result())}", flush=True)
+    _, tlib, _ = _torch_paths()
+    target = os.path.join(OUT, name + _ext_suffix())
+    if todo or not os.path.exists(target):
+        link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", target] + objs + [
+            f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
+            "-lamdhip64", f"-Wl,-rpath,{tlib}"] + extra_libs
+        r = subprocess.run(link, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed for {name}\n{' '.join(link)}\n{r.stdout}\n{r.stderr}")
+        print(f"[build] linked {target}", flush=True)
+    return target
+
+
+def build_all(jobs: int | None = None) -> list[str]:
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    kdir = os.path.join(CSRC, "kernels")
+    ksrc = sorted(os.path.join(kdir, f) for f in os.listdir(kdir) if f.endswith(".hip"))
+    ksrc.append(os.path.join(CSRC, "bindings.cpp"))
+    built = [build_module("penroz_kernels", ksrc, [], jobs)]
+    cdir = os.path.join(CSRC, "comm")
+    csrc = sorted(os.path.join(cdir, f) for f in os.listdir(cdir) if f.endswith(".cpp")) if os.path.isdir(cdir) else []
+    if csrc:
+        _, tlib, _ = _torch_paths()
+        built.append(build_module("penroz_comm", csrc, [f"{tlib}/librccl.so"], jobs))
+    return built
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] not in ("build_ext", "build"):
+        print(__doc__)
+        sys.exit(2)
+    for p in build_all():
+        print(p)

@@ -1,0 +1,320 @@
+"""HIP kernel parity: every kernel vs a plain PyTorch fp32 reference of the same op (MI355X)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # pragma: no cover - CPU runner
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from penroz.ops import _ext, attention as A, norms as Nm, activations as Ac, fused as Fu, sampling as Sa, rope as Ro
+
+DEV = "cuda"
+
+
+def test_extension_is_native():
+    assert _ext.available(), "penroz_kernels must be importable on the GPU box"
+    import penroz_kernels
+    assert penroz_kernels.__file__.endswith(".so")
+
+
+def _close(a, b, atol, rtol=0.0, msg=""):
+    err = (a.float() - b.float()).abs().max().item()
+    lim = atol + rtol * b.float().abs().max().item()
+    assert err <= lim, f"{msg} max err {err} > {lim}"
+
+
+@pytest.mark.parametrize("C", [768, 1600, 256, 100])
+@pytest.mark.parametrize("xdt", [torch.float32, torch.bfloat16])
+def test_layernorm_fwd(C, xdt):
+    torch.manual_seed(0)
+    x = (torch.randn(300, C, device=DEV) * 3 + 1).to(xdt)
+    w, b = torch.randn(C, device=DEV), torch.randn(C, device=DEV)
+    y, mean, rstd = Nm.ln_fwd(x, w, b, 1e-5, torch.float32)
+    ry, rm, rr = Nm.reference_layer_norm(x, w, b, 1e-5)
+    _close(y, ry, 2e-4, 1e-4)
+    _close(mean, rm, 1e-4)
+    _close(rstd, rr, 1e-3, 1e-4)
+    yb, _, _ = Nm.ln_fwd(x, w, b, 1e-5, torch.bfloat16)
+    _close(yb, ry, 0.05, 0.01)
+
+
+@pytest.mark.parametrize("C", [768, 1600])
+def test_add_layernorm_fwd(C):
+    x = torch.randn(257, C, device=DEV)
+    d = torch.randn(257, C, device=DEV).to(torch.bfloat16)
+    w, b = torch.randn(C, device=DEV), torch.randn(C, device=DEV)
+    out = torch.empty_like(x)
+    y, _, _ = Nm.add_ln_fwd(x, d, out, w, b, 1e-5)
+    ref = x + d.float()
+    _close(out, ref, 1e-6)
+    ry, _, _ = Nm.reference_layer_norm(ref, w, b, 1e-5)
+    _close(y, ry, 0.06, 0.01)
+
+
+@pytest.mark.parametrize("C", [768, 1600])
+def test_layernorm_bwd(C):
+    torch.manual_seed(1)
+    N = 1000
+    x = torch.randn(N, C, device=DEV) * 2
+    w, b = torch.randn(C, device=DEV), torch.randn(C, device=DEV)
+    dy = torch.randn(N, C, device=DEV).to(torch.bfloat16)
+    _, mean, rstd = Nm.ln_fwd(x, w, b, 1e-5, torch.float32)
+    base = torch.randn(N, C, device=DEV)
+    dres = base.clone()
+    dres_bf = torch.empty(N, C, device=DEV, dtype=torch.bfloat16)
+    dw, db, dbp = (torch.ones(C, device=DEV) for _ in range(3))
+    Nm.ln_bwd(dy, x, mean, rstd, w, dres, True, dres_bf, dw, db, dbp)
+    rdx, rdw, rdb = Nm.reference_layer_norm_bwd(dy, x, mean, rstd, w)
+    _close(dres, base + rdx, 2e-3, 1e-4, "dx")
+    _close(dres_bf, base + rdx, 0.05, 0.01, "dx bf16")
+    _close(dw, 1 + rdw, 1e-2, 1e-4, "dw")
+    _close(db, 1 + rdb, 1e-2, 1e-4, "db")
+    _close(dbp, 1 + (base + rdx).sum(0), 1e-2, 1e-4, "dbias")
+
+
+@pytest.mark.parametrize("approx", ["none", "tanh"])
+def test_gelu(approx):
+    x = (torch.randn(512, 3072, device=DEV) * 3).to(torch.bfloat16)
+    y = Ac.gelu_fwd(x, approx)
+    _close(y, F.gelu(x.float(), approximate=approx), 0.03, 0.01)
+    dy = torch.randn_like(x)
+    ref = Ac.reference_gelu_bwd(dy, x, approx)
+    dx = Ac.gelu_bwd(dy, x, approx)
+    _close(dx, ref, 0.05, 0.01)
+    dbias = torch.zeros(3072, device=DEV)
+    out = dy.clone()
+    Ac.gelu_bwd(out, x, approx, dbias, out=out)  # in place + fused column sum
+    _close(out, ref, 0.05, 0.01)
+    _close(dbias, out.float().sum(0), 0.05, 1e-3)
+
+
+def test_colsum():
+    x = torch.randn(4099, 2304, device=DEV).to(torch.bfloat16)
+    out = torch.full((2304,), 2.0, device=DEV)
+    Fu.colsum(x, out)
+    _close(out, 2 + x.float().sum(0), 0.05, 1e-4)
+
+
+def test_embedding():
+    V, P, C, B, T = 1000, 64, 768, 3, 50
+    wte, wpe = torch.randn(V, C, device=DEV), torch.randn(P, C, device=DEV)
+    idx = torch.randint(0, V, (B, T), device=DEV)
+    idx[0, :5] = 7  # repeated tokens exercise the scatter-add
+    out = Fu.embedding_fwd(idx, wte, wpe, 3)
+    _close(out, Fu.reference_embedding_fwd(idx, wte, wpe, 3), 1e-6)
+    dout = torch.randn(B * T, C, device=DEV)
+    dwte, dwpe = torch.zeros(V, C, device=DEV), torch.zeros(P, C, device=DEV)
+    Fu.embedding_bwd(dout, idx, dwte, dwpe, 3)
+    w1, w2 = wte.clone().requires_grad_(), wpe.clone().requires_grad_()
+    (Fu.reference_embedding_fwd(idx, w1, w2, 3) * dout).sum().backward()
+    _close(dwte, w1.grad, 1e-4)
+    _close(dwpe, w2.grad, 1e-4)
+
+
+@pytest.mark.parametrize("V", [50304, 50257 - 1, 1000])
+def test_cross_entropy(V):
+    V = V - V % 8
+    N = 64
+    logits = (torch.randn(N, V, device=DEV) * 3).to(torch.bfloat16)
+    tgt = torch.randint(0, V, (N,), device=DEV)
+    tgt[3] = -100
+    ref_loss = F.cross_entropy(logits.float(), tgt, reduction="none", ignore_index=-100)
+    lf = logits.float().requires_grad_()
+    F.cross_entropy(lf, tgt, ignore_index=-100, reduction="sum").backward()
+    g = logits.clone()
+    loss = Fu.cross_entropy_fwd_bwd(g, tgt, 0.5)
+    _close(loss, ref_loss, 2e-3, 1e-4, "loss")
+    _close(g, 0.5 * lf.grad, 2e-3, 1e-2, "grad")
+    g2 = logits.clone()
+    Fu.cross_entropy_fwd_bwd(g2, tgt, 0.0)
+    assert torch.equal(g2, logits), "eval mode must not modify logits"
+
+
+def test_adamw_flat_matches_torch():
+    torch.manual_seed(0)
+    n = 10007
+    p = torch.randn(n, device=DEV)
+    ref = p.clone().requires_grad_()
+    opt = torch.optim.AdamW([ref], lr=1e-2, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    m, v = torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    shadow = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    for step in range(1, 6):
+        g = torch.randn(n, device=DEV)
+        ref.grad = g.clone()
+        opt.step()
+        Fu.adamw_step(p, g, m, v, shadow, 1e-2, 0.9, 0.95, 1e-8, 0.1, step)
+    _close(p, ref.detach(), 1e-5, 1e-5)
+    _close(shadow, ref.detach(), 0.02, 0.01)
+
+
+def test_fused_optimizer_list_mode():
+    from penroz.models.optim import FusedAdamW, FusedAdam
+    torch.manual_seed(0)
+    for cls, tcls in ((FusedAdamW, torch.optim.AdamW), (FusedAdam, torch.optim.Adam)):
+        ps = [torch.randn(s, device=DEV, requires_grad=True) for s in ((33, 17), (5,), (70000,))]
+        rs = [p.detach().clone().requires_grad_() for p in ps]
+        o1, o2 = cls(ps, lr=3e-3, weight_decay=0.05), tcls(rs, lr=3e-3, weight_decay=0.05)
+        for _ in range(3):
+            for p, r in zip(ps, rs):
+                g = torch.randn_like(p)
+                p.grad, r.grad = g.clone(), g.clone()
+            o1.step()
+            o2.step()
+        for p, r in zip(ps, rs):
+            _close(p, r, 1e-5, 1e-5)
+        assert set(o1.state_dict()["state"][0].keys()) == set(o2.state_dict()["state"][0].keys())
+
+
+def _qkv(B, T, H, Hkv, D=64, scale=1.0):
+    return (torch.randn(B, T, (H + 2 * Hkv) * D, device=DEV) * scale).to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("B,T,H,Hkv", [(2, 1024, 4, 4), (1, 200, 3, 3), (2, 130, 4, 2), (1, 64, 2, 1), (1, 5, 2, 2)])
+def test_flash_fwd(B, T, H, Hkv):
+    torch.manual_seed(0)
+    qkv = _qkv(B, T, H, Hkv, scale=1.5)
+    out, lse = A.flash_fwd(qkv, H, Hkv, 64)
+    ro, rl = A.reference_attention_lse(qkv, H, Hkv, 64)
+    _close(out, ro, 0.02, 0.01, "out")
+    _close(lse, rl, 2e-3, 1e-4, "lse")
+
+
+@pytest.mark.parametrize("B,T,H,Hkv", [(2, 512, 4, 4), (1, 200, 3, 3), (2, 130, 4, 2), (1, 7, 2, 1)])
+def test_flash_bwd(B, T, H, Hkv):
+    torch.manual_seed(0)
+    qkv = _qkv(B, T, H, Hkv)
+    out, lse = A.flash_fwd(qkv, H, Hkv, 64)
+    dout = torch.randn(B, T, H * 64, device=DEV).to(torch.bfloat16)
+    dq = A.flash_bwd(dout, qkv, out, lse, H, Hkv, 64)
+    x = qkv.float().requires_grad_()
+    ro, _ = A.reference_attention_lse(x, H, Hkv, 64)
+    (ro * dout.float()).sum().backward()
+    ref = x.grad
+    for name, sl in (("dq", slice(0, H * 64)), ("dk", slice(H * 64, (H + Hkv) * 64)), ("dv", slice((H + Hkv) * 64, None))):
+        a, r = dq[..., sl].float(), ref[..., sl]
+        rel = (a - r).norm() / r.norm()
+        assert rel < 0.02, f"{name} relative error {rel}"
+
+
+def test_flash_dropout_matches_masked_reference():
+    """With one-hot V rows the forward output reveals the dropout mask exactly; the backward
+    must reproduce the gradients of softmax -> mask/(1-p) -> @V with that same mask."""
+    torch.manual_seed(0)
+    B, T, H, D, p = 1, 64, 1, 64, 0.3
+    qkv = _qkv(B, T, H, H)
+    qkv[..., 2 * D:] = torch.eye(T, D, device=DEV).to(torch.bfloat16)  # V[key] = e_key
+    out, lse = A.flash_fwd(qkv, H, H, D, p, seed=99)
+    out2, _ = A.flash_fwd(qkv, H, H, D, p, seed=99)
+    assert torch.equal(out, out2)
+    causal = torch.ones(T, T, device=DEV, dtype=torch.bool).tril()
+    mask = (out[0].float() != 0) & causal
+    frac = mask.sum() / causal.sum()
+    assert 0.55 < frac < 0.85, frac
+    x = qkv.float().requires_grad_()
+    q, k, v = x[0, :, :D], x[0, :, D:2 * D], x[0, :, 2 * D:]
+    s = (q @ k.t()) / math.sqrt(D)
+    s = s.masked_fill(~causal, float("-inf"))
+    pd = torch.softmax(s, -1) * mask / (1 - p)
+    ref = pd @ v
+    _close(out[0], ref, 0.02, 0.01, "dropout fwd")
+    dout = torch.randn(B, T, H * D, device=DEV).to(torch.bfloat16)
+    (ref * dout[0].float()).sum().backward()
+    g = A.flash_bwd(dout, qkv, out, lse, H, H, D, p, seed=99).float()
+    rel = (g - x.grad).norm() / x.grad.norm()
+    assert rel < 0.02, rel
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("B,H,Hkv,S,Tq", [(2, 4, 4, 300, 1), (1, 8, 2, 1024, 1), (3, 4, 4, 64, 5)])
+def test_decode_attention(dtype, B, H, Hkv, S, Tq):
+    D, cap = 64, 1100
+    q = torch.randn(B, Tq, H, D, device=DEV).to(dtype)
+    kc = torch.randn(B, Hkv, cap, D, device=DEV).to(dtype)
+    vc = torch.randn(B, Hkv, cap, D, device=DEV).to(dtype)
+    out = A.decode_attention(q, kc, vc, S)
+    ref = A.reference_cache_attention(q.float(), kc[:, :, :S].float(), vc[:, :, :S].float(), S - Tq)
+    _close(out, ref, 0.02, 0.01)
+
+
+def test_decode_attention_int8():
+    B, H, S, D, cap = 2, 4, 200, 64, 256
+    q = torch.randn(B, 1, H, D, device=DEV).to(torch.bfloat16)
+    k = torch.randn(B, S, H, D, device=DEV).to(torch.bfloat16)
+    v = torch.randn(B, S, H, D, device=DEV).to(torch.bfloat16)
+    kq, vq = torch.empty(B, H, cap, D, dtype=torch.int8, device=DEV), torch.empty(B, H, cap, D, dtype=torch.int8, device=DEV)
+    ks, vs = torch.ones(B, H, cap, device=DEV), torch.ones(B, H, cap, device=DEV)
+    Sa.kv_quantize_into(k, kq, ks, 0)
+    Sa.kv_quantize_into(v, vq, vs, 0)
+    rq, rs = Sa.reference_quantize(k.float().transpose(1, 2))
+    assert (kq[:, :, :S].int() - rq.int()).abs().max() <= 1
+    _close(ks[:, :, :S], rs.squeeze(-1), 1e-6)
+    out = A.decode_attention(q, kq, vq, S, ks, vs)
+    ref = A.reference_cache_attention(q.float(), k.transpose(1, 2).float(), v.transpose(1, 2).float(), S - 1)
+    _close(out, ref, 0.05, 0.02)
+
+
+def test_sampling():
+    torch.manual_seed(0)
+    logits = torch.randn(8, 50304, device=DEV).to(torch.bfloat16)
+    g = Sa.sample(logits, 0.0, None)
+    assert torch.equal(g.view(-1), logits.float().argmax(-1))
+    for _ in range(5):
+        t = Sa.sample(logits, 1.0, 5)
+        top = logits.float().topk(5, dim=-1).indices
+        assert all(t[i, 0] in top[i] for i in range(8))
+    # distribution: a peaked 4-way row sampled many times matches its softmax
+    row = torch.full((1, 64), -30.0, device=DEV)
+    row[0, :4] = torch.tensor([2.0, 1.0, 0.0, -1.0], device=DEV)
+    counts = torch.zeros(64)
+    for _ in range(4000):
+        counts[Sa.sample(row, 1.0, None).item()] += 1
+    probs = torch.softmax(row[0, :4].cpu(), -1)
+    assert torch.allclose(counts[:4] / 4000, probs, atol=0.03)
+    # kernel and CPU reference pick the same token for the same uniforms
+    u = torch.rand(8)
+    a = Sa.reference_sample(logits.float().cpu(), 0.8, 40, u)
+    b = _ext.kernels().sample_tokens(logits.float(), u.to(DEV), 0.8, 40).cpu()
+    assert (a == b).float().mean() >= 0.75  # fp rounding may flip a boundary draw
+
+
+@pytest.mark.parametrize("xdt,wdt", [(torch.float32, torch.float32), (torch.bfloat16, torch.bfloat16)])
+def test_rmsnorm(xdt, wdt):
+    x = torch.randn(100, 640, device=DEV).to(xdt)
+    w = torch.randn(640, device=DEV).to(wdt)
+    y = Nm.rms_norm(x, w, 1e-6)
+    _close(y, Nm.reference_rms_norm(x, w, 1e-6), 0.03, 0.01)
+    xr, wr = x.float().requires_grad_(), w.float().requires_grad_()
+    dy = torch.randn(100, 640, device=DEV)
+    Nm.reference_rms_norm(xr, wr, 1e-6).backward(dy)
+    xg, wg = x.clone().requires_grad_(), w.clone().requires_grad_()
+    Nm.rms_norm(xg, wg, 1e-6).backward(dy.to(y.dtype))
+    _close(xg.grad, xr.grad, 0.05, 0.02)
+    _close(wg.grad, wr.grad, 0.5, 0.02)
+
+
+def test_rope():
+    H, Hkv, D = 4, 2, 64
+    qkv = torch.randn(2, 33, (H + 2 * Hkv) * D, device=DEV)
+    inv = 1.0 / (10000 ** (torch.arange(0, D, 2, device=DEV).float() / D))
+    out = Ro.apply_rope_qkv(qkv, H, Hkv, D, inv, 7)
+    ref = Ro.reference_apply_rope_qkv(qkv, H, Hkv, D, inv, 7)
+    _close(out, ref, 1e-4)
+    x = qkv.clone().requires_grad_()
+    Ro.apply_rope_qkv(x, H, Hkv, D, inv, 7).sum().backward()
+    xr = qkv.clone().requires_grad_()
+    Ro.reference_apply_rope_qkv(xr, H, Hkv, D, inv, 7).sum().backward()
+    _close(x.grad, xr.grad, 1e-4)
+
+
+def test_tensor_stats():
+    x = torch.randn(100000, device=DEV) * 2 + 1
+    mean, std, mn, mx, hist, edges = Fu.tensor_stats(x, 100)
+    h = torch.histogram(x.cpu(), bins=100, density=True)
+    _close(mean, x.mean(), 1e-4)
+    _close(std, x.std(), 1e-3)
+    _close(edges.cpu(), h.bin_edges, 1e-4)
+    _close(hist.cpu(), h.hist, 2e-3, 0.01)
