@@ -1,0 +1,45 @@
+"""Micro-benchmarks of the penroz HIP kernels vs their PyTorch/hipBLASLt counterparts (one MI355X).
+
+Prints one JSON line per measurement: GPT-2 124M shapes at B=64, T=1024.
+"""
+import json, math, sys, time, os
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+import torch.nn.functional as F
+from penroz.ops import _ext, attention as A
+
+def timeit(fn, iters=10, warmup=3):
+    for _ in range(warmup): fn()
+    torch.cuda.synchronize(); t0 = time.perf_counter()
+    for _ in range(iters): fn()
+    torch.cuda.synchronize(); return (time.perf_counter() - t0) / iters
+
+def emit(**kw): print(json.dumps(kw), flush=True)
+
+k = _ext.kernels()
+N = 65536
+which = sys.argv[1:] or ["wgrad", "attn"]
+if "wgrad" in which:
+    for name, (m, n) in {"qkv": (2304, 768), "proj": (768, 768), "fc": (3072, 768), "fc2": (768, 3072), "lm_head": (50304, 768)}.items():
+        dy = torch.randn(N, m, device="cuda", dtype=torch.bfloat16)
+        x = torch.randn(N, n, device="cuda", dtype=torch.bfloat16)
+        g = torch.zeros(m, n, device="cuda")
+        fl = 2 * N * m * n
+        tn = timeit(lambda: k.wgrad_gemm(dy, x, g))
+        tt = timeit(lambda: g.add_(torch.mm(dy.t(), x, out_dtype=torch.float32)))
+        emit(kernel="wgrad", shape=name, native_TF=round(fl / tn / 1e12, 1), hipblaslt_TF=round(fl / tt / 1e12, 1),
+             native_us=round(tn * 1e6, 1), hipblaslt_us=round(tt * 1e6, 1))
+if "attn" in which:
+    B, T, H, D = 64, 1024, 12, 64
+    qkv = torch.randn(B, T, 3 * H * D, device="cuda", dtype=torch.bfloat16)
+    fl = 4 * B * H * T * T * D / 2
+    out, lse = A.flash_fwd(qkv, H, H, D)
+    tf = timeit(lambda: A.flash_fwd(qkv, H, H, D, out=out, lse=lse))
+    dout = torch.randn_like(out)
+    dq = torch.empty_like(qkv)
+    tb = timeit(lambda: A.flash_bwd(dout, qkv, out, lse, H, H, D, dqkv=dq))
+    q, kk, v = (t.view(B, T, H, D).transpose(1, 2) for t in qkv.split(H * D, dim=2))
+    ts = timeit(lambda: F.scaled_dot_product_attention(q, kk, v, is_causal=True))
+    emit(kernel="flash_fwd", native_us=round(tf * 1e6, 1), native_TF=round(fl / tf / 1e12, 1),
+         sdpa_us=round(ts * 1e6, 1), sdpa_TF=round(fl / ts / 1e12, 1))
+    emit(kernel="flash_bwd", native_us=round(tb * 1e6, 1), native_TF=round(2.5 * fl / tb / 1e12, 1))

@@ -7,6 +7,7 @@
 // 8 columns fixed while it walks rows, so the partial sums live in registers; a workgroup
 // reduces its 4 waves in LDS and writes one partial row, finished by a tiny reduction.
 #include "common.h"
+#include "reduce.h"
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 
@@ -94,10 +95,9 @@ __global__ void __launch_bounds__(256) rows_colsum_kernel(const T* __restrict__ 
         float xv[8];
         Vec8<T>::load(x + off, xv);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] *= gelu_grad_f(xv[k], approx);
+        for (int k = 0; k < 8; ++k) v[k] = to_f(from_f<T>(v[k] * gelu_grad_f(xv[k], approx)));
+        // v now holds the *rounded* values: dbias matches the bf16 gradient the GEMMs see
         Vec8<T>::store(out + off, v);
-        // accumulate the *rounded* value so dbias matches the bf16 gradient the GEMMs see
-        Vec8<T>::load(out + off, v);
       }
 #pragma unroll
       for (int k = 0; k < 8; ++k) acc[k] += v[k];
@@ -110,15 +110,6 @@ __global__ void __launch_bounds__(256) rows_colsum_kernel(const T* __restrict__ 
     const int gc = blockIdx.x * 512 + c;
     if (gc < F) part[(size_t)blockIdx.y * F + gc] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
   }
-}
-
-__global__ void __launch_bounds__(256) finish_colsum_kernel(const float* __restrict__ part, int R, int F,
-                                                            float* __restrict__ out) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= F) return;
-  float s = 0.f;
-  for (int r = 0; r < R; ++r) s += part[(size_t)r * F + c];
-  out[c] += s;
 }
 
 // ------------------------------------------------------------------------------ gated MLP act
@@ -366,8 +357,10 @@ static void colsum_impl(const torch::Tensor& a, const torch::Tensor* x, torch::T
       hipLaunchKernelGGL((rows_colsum_kernel<1, T>), dim3(ctiles, R), dim3(256), 0, stream, ap, xp, op,
                          part.data_ptr<float>(), N, F, approx);
   })
-  hipLaunchKernelGGL(finish_colsum_kernel, dim3((F + 255) / 256), dim3(256), 0, stream, part.data_ptr<float>(), R, F,
-                     dst.data_ptr<float>());
+  const int S = reduce_slices(R);
+  auto mid = torch::empty({S, F}, a.options().dtype(torch::kFloat32));
+  float* outs[1] = {dst.data_ptr<float>()};
+  reduce_partials_add(part.data_ptr<float>(), 1, R, F, outs, mid.data_ptr<float>(), S, stream);
 }
 
 void gelu_bwd(torch::Tensor dy, torch::Tensor x, int64_t approx, c10::optional<torch::Tensor> dbias,

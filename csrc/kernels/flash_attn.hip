@@ -95,6 +95,28 @@ __device__ __forceinline__ bool dropout_keep(uint64_t seed, int b, int h, int H,
 
 __device__ __forceinline__ uint4 zero4() { return uint4{0u, 0u, 0u, 0u}; }
 
+// raw v_exp_f32 (no denormal range fix-up: softmax weights that small are 0 anyway)
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// wave index, provably wave-uniform for the compiler (keeps causal-mask branches scalar)
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
+// Combine a value across the two 32-lane halves (lane l and l^32) with one
+// v_permlane32_swap instead of a ds_bpermute round trip. The swap of (v, v) returns
+// {[lo|lo], [hi|hi]}, so op(r0, r1) is the full-row result in every lane.
+__device__ __forceinline__ float halves_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float halves_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// defer-rescale threshold (log2 units): the running max is only raised when some row's max
+// grows by more than 2^8, so most tiles skip the O rescale (P then stays <= 256: bf16-safe)
+constexpr float kRescaleThr = 8.0f;
+
 // stores 4 consecutive bf16 (8 bytes)
 __device__ __forceinline__ void store4(bf16* p, float a, float b, float c, float d) {
   *reinterpret_cast<uint2*>(p) = uint2{pack_bf16x2(a, b), pack_bf16x2(c, d)};
@@ -103,7 +125,7 @@ __device__ __forceinline__ void store4(bf16* p, float a, float b, float c, float
 // ------------------------------------------------------------------------------------------
 // forward
 template <bool DROPOUT>
-__global__ void __launch_bounds__(256) fa_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+__global__ void __launch_bounds__(256, 2) fa_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
                                                      float* __restrict__ lse, int T, int H, int Hkv, float scale,
                                                      float p_drop, uint64_t seed) {
   constexpr int BM = 128, BN = 64;
@@ -111,7 +133,7 @@ __global__ void __launch_bounds__(256) fa_fwd_kernel(const bf16* __restrict__ qk
   const int nqb = (T + BM - 1) / BM;
   const int qb = nqb - 1 - blockIdx.x;
   const int b = blockIdx.y / H, h = blockIdx.y % H, hk = h / (H / Hkv);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5;
+  const int lane = threadIdx.x & 63, w = wave_id(), hh = lane >> 5;
   const size_t RS = (size_t)(H + 2 * Hkv) * kD;
   const bf16* qbase = qkv + (size_t)b * T * RS + (size_t)h * kD;
   const bf16* kbase = qkv + (size_t)b * T * RS + (size_t)(H + hk) * kD;
@@ -179,22 +201,28 @@ __global__ void __launch_bounds__(256) fa_fwd_kernel(const bf16* __restrict__ qk
           float v = s[kh][i] * c;
           if (need_mask) {
             const int key = kt0 + 32 * kh + acc_row(i, lane);
-            if (key > qrow || key >= T) v = -INFINITY;
+            v = (key > qrow || key >= T) ? -INFINITY : v;
           }
           s[kh][i] = v;
           tmax = fmaxf(tmax, v);
         }
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      const float mnew = fmaxf(m, tmax);
-      const float alpha = exp2f(m - mnew);
-      m = mnew;
-      float rs = 0.f;
+      tmax = halves_max(tmax);
+      if (!__all(tmax <= m + kRescaleThr)) {  // wave-uniform: rare after the first tiles
+        const float mnew = fmaxf(m, tmax);
+        const float alpha = fexp2(m - mnew);
+        m = mnew;
+        l *= alpha;
+#pragma unroll
+        for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) o[dh][i] *= alpha;
+      }
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const float p = exp2f(s[kh][i] - mnew);
-          rs += p;
+          const float p = fexp2(s[kh][i] - m);
+          l += p;
           if constexpr (DROPOUT) {
             const int key = kt0 + 32 * kh + acc_row(i, lane);
             s[kh][i] = dropout_keep(seed, b, h, H, T, qrow, key, p_drop) ? p * inv_keep : 0.f;
@@ -202,11 +230,6 @@ __global__ void __launch_bounds__(256) fa_fwd_kernel(const bf16* __restrict__ qk
             s[kh][i] = p;
           }
         }
-      l = l * alpha + rs;
-#pragma unroll
-      for (int dh = 0; dh < 2; ++dh)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) o[dh][i] *= alpha;
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
@@ -219,7 +242,7 @@ __global__ void __launch_bounds__(256) fa_fwd_kernel(const bf16* __restrict__ qk
     if (j + 1 < ntiles) lstore((j + 1) & 1);
     __syncthreads();
   }
-  l += __shfl_xor(l, 32, 64);
+  l = halves_sum(l);
   const float inv = l > 0.f ? 1.f / l : 0.f;
   if (qrow < T) {
     bf16* orow = out + ((size_t)b * T + qrow) * H * kD + (size_t)h * kD;
@@ -258,14 +281,17 @@ __global__ void __launch_bounds__(256) fa_bwd_pre_kernel(const bf16* __restrict_
 }
 
 // ------------------------------------------------------------------------------------------
-// dK / dV: grid (ceil(T/128) key blocks, B*Hkv); wave w owns keys kb*128 + 32w + (lane&31)
+// dK / dV: grid (ceil(T/128) key blocks, B*Hkv); wave w owns keys kb*128 + 32w + (lane&31).
+// Query slices of 64 rows (two 32-row halves per barrier) are staged through registers into
+// double-buffered LDS; P / dS are computed in place in the S / dP accumulators.
 template <bool DROPOUT>
-__global__ void __launch_bounds__(256) fa_bwd_dkdv_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
-                                                          const float* __restrict__ lse,
-                                                          const float* __restrict__ delta, bf16* __restrict__ dqkv,
-                                                          int T, int H, int Hkv, float scale, float p_drop,
-                                                          uint64_t seed) {
-  constexpr int BK = 128, QS = 32;
+__global__ void __launch_bounds__(256, 2) fa_bwd_dkdv_kernel(const bf16* __restrict__ qkv,
+                                                             const bf16* __restrict__ dout,
+                                                             const float* __restrict__ lse,
+                                                             const float* __restrict__ delta, bf16* __restrict__ dqkv,
+                                                             int T, int H, int Hkv, float scale, float p_drop,
+                                                             uint64_t seed) {
+  constexpr int BK = 128, QS = 64;
   __shared__ __attribute__((aligned(16))) char qt[2][QS * 128];
   __shared__ __attribute__((aligned(16))) char dot[2][QS * 128];
   __shared__ __attribute__((aligned(16))) float lse2s[2][QS];
@@ -273,7 +299,7 @@ __global__ void __launch_bounds__(256) fa_bwd_dkdv_kernel(const bf16* __restrict
   const int kb = blockIdx.x;
   const int b = blockIdx.y / Hkv, hk = blockIdx.y % Hkv;
   const int G = H / Hkv;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5;
+  const int lane = threadIdx.x & 63, w = wave_id(), hh = lane >> 5;
   const size_t RS = (size_t)(H + 2 * Hkv) * kD;
   const size_t ORS = (size_t)H * kD;
   const int kw0 = kb * BK + 32 * w;
@@ -295,23 +321,25 @@ __global__ void __launch_bounds__(256) fa_bwd_dkdv_kernel(const bf16* __restrict
 #pragma unroll
     for (int i = 0; i < 16; ++i) dk[dh][i] = dv[dh][i] = 0.f;
 
-  // staging: threads 0..127 -> Q slice, 128..255 -> dO slice; row (t>>2)&31, chunks 2(t&3), +1
-  const int st_tile = threadIdx.x >> 7, sr = (threadIdx.x >> 2) & 31, sc = 2 * (threadIdx.x & 3);
+  // staging: threads 0..127 -> Q slice, 128..255 -> dO slice; each thread 4 chunks of one row
+  // half: row (t>>1)&63, chunks 4(t&1)..+3
+  const int st_tile = threadIdx.x >> 7, sr = (threadIdx.x >> 1) & 63, sc = 4 * (threadIdx.x & 1);
   const int s_first = (kb * BK) / QS;
   const int nslices = (T + QS - 1) / QS;
-  const int total = G * (nslices - s_first);
-  uint4 st[2];
+  const int per_head = nslices - s_first;
+  const int total = G * per_head;
+  uint4 st[4];
   float st_scalar = 0.f;
   auto gload = [&](int it) {
-    const int hq = hk * G + it / (nslices - s_first);
-    const int qs0 = (s_first + it % (nslices - s_first)) * QS;
+    const int hq = hk * G + it / per_head;
+    const int qs0 = (s_first + it % per_head) * QS;
     const int q = qs0 + sr;
     const bf16* src = st_tile == 0 ? qkv + (size_t)b * T * RS + (size_t)hq * kD + (size_t)q * RS
                                    : dout + (size_t)b * T * ORS + (size_t)hq * kD + (size_t)q * ORS;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) st[i] = q < T ? *reinterpret_cast<const uint4*>(src + 8 * (sc + i)) : zero4();
+    for (int i = 0; i < 4; ++i) st[i] = q < T ? *reinterpret_cast<const uint4*>(src + 8 * (sc + i)) : zero4();
     if (threadIdx.x < 2 * QS) {
-      const int qq = qs0 + (threadIdx.x & 31);
+      const int qq = qs0 + (threadIdx.x & (QS - 1));
       const size_t r = ((size_t)b * H + hq) * T + qq;
       st_scalar = qq < T ? (threadIdx.x < QS ? lse[r] * kLog2e : delta[r]) : 0.f;
     }
@@ -319,7 +347,7 @@ __global__ void __launch_bounds__(256) fa_bwd_dkdv_kernel(const bf16* __restrict
   auto lstore = [&](int buf) {
     char* dst = st_tile == 0 ? qt[buf] : dot[buf];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) *reinterpret_cast<uint4*>(dst + tile_off(sr, sc + i)) = st[i];
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(dst + tile_off(sr, sc + i)) = st[i];
     if (threadIdx.x < QS) lse2s[buf][threadIdx.x] = st_scalar;
     else if (threadIdx.x < 2 * QS) dels[buf][threadIdx.x - QS] = st_scalar;
   };
@@ -332,49 +360,53 @@ __global__ void __launch_bounds__(256) fa_bwd_dkdv_kernel(const bf16* __restrict
   for (int it = 0; it < total; ++it) {
     if (it + 1 < total) gload(it + 1);
     const int buf = it & 1;
-    const int hq = hk * G + it / (nslices - s_first);
-    const int qs0 = (s_first + it % (nslices - s_first)) * QS;
-    if (qs0 + QS - 1 >= kw0 && kw0 < T) {
-      const char* Qt = qt[buf];
-      const char* Dt = dot[buf];
-      f32x16 sp, dp;
+    const int hq = hk * G + it / per_head;
+    const int qs0 = (s_first + it % per_head) * QS;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) sp[i] = dp[i] = 0.f;
+    for (int half = 0; half < 2; ++half) {
+      const int qh0 = qs0 + 32 * half;  // first query row of this 32-row half
+      if (qh0 + 31 >= kw0 && kw0 < T && qh0 < T) {
+        const char* Qt = qt[buf] + half * 32 * 128;
+        const char* Dt = dot[buf] + half * 32 * 128;
+        f32x16 sp, dp;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        sp = mfma32(row_frag(Qt, 0, s, lane), kf[s], sp);
-        dp = mfma32(row_frag(Dt, 0, s, lane), vf[s], dp);
-      }
-      f32x16 pd, ds;
+        for (int i = 0; i < 16; ++i) sp[i] = dp[i] = 0.f;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int r0 = 8 * g + 4 * hh;
-        const float4_t l2 = *reinterpret_cast<const float4_t*>(&lse2s[buf][r0]);
-        const float4_t dl = *reinterpret_cast<const float4_t*>(&dels[buf][r0]);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int i = 4 * g + k;
-          const int q = qs0 + r0 + k;
-          float p = exp2f(sp[i] * c - l2[k]);
-          if (key > q || q >= T || key >= T) p = 0.f;
-          float dpi = dp[i];
-          float pdrop = p;
-          if constexpr (DROPOUT) {
-            const bool keep = dropout_keep(seed, b, hq, H, T, q, key, p_drop);
-            pdrop = keep ? p * inv_keep : 0.f;
-            dpi = keep ? dpi * inv_keep : 0.f;
-          }
-          pd[i] = pdrop;
-          ds[i] = p * (dpi - dl[k]);
+        for (int s = 0; s < 4; ++s) {
+          sp = mfma32(row_frag(Qt, 0, s, lane), kf[s], sp);
+          dp = mfma32(row_frag(Dt, 0, s, lane), vf[s], dp);
         }
-      }
+        const bool need_mask = (kw0 + 31 > qh0) || (qh0 + 32 > T) || (kw0 + 32 > T);
 #pragma unroll
-      for (int ss = 0; ss < 2; ++ss) {
-        const uint4 pf = acc_frag(pd, ss), sf = acc_frag(ds, ss);
+        for (int g = 0; g < 4; ++g) {
+          const int r0 = 8 * g + 4 * hh;
+          const float4_t l2 = *reinterpret_cast<const float4_t*>(&lse2s[buf][32 * half + r0]);
+          const float4_t dl = *reinterpret_cast<const float4_t*>(&dels[buf][32 * half + r0]);
 #pragma unroll
-        for (int dh = 0; dh < 2; ++dh) {
-          dv[dh] = mfma32(tr_frag(Dt, 16 * ss, 32 * dh, lane), pf, dv[dh]);
-          dk[dh] = mfma32(tr_frag(Qt, 16 * ss, 32 * dh, lane), sf, dk[dh]);
+          for (int k = 0; k < 4; ++k) {
+            const int i = 4 * g + k;
+            const int q = qh0 + r0 + k;
+            float p = fexp2(sp[i] * c - l2[k]);
+            if (need_mask) p = (key > q || q >= T || key >= T) ? 0.f : p;
+            float dpi = dp[i];
+            float pdrop = p;
+            if constexpr (DROPOUT) {
+              const bool keep = dropout_keep(seed, b, hq, H, T, q, key, p_drop);
+              pdrop = keep ? p * inv_keep : 0.f;
+              dpi = keep ? dpi * inv_keep : 0.f;
+            }
+            sp[i] = pdrop;
+            dp[i] = p * (dpi - dl[k]);
+          }
+        }
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          const uint4 pf = acc_frag(sp, ss), sf = acc_frag(dp, ss);
+#pragma unroll
+          for (int dh = 0; dh < 2; ++dh) {
+            dv[dh] = mfma32(tr_frag(Dt, 16 * ss, 32 * dh, lane), pf, dv[dh]);
+            dk[dh] = mfma32(tr_frag(Qt, 16 * ss, 32 * dh, lane), sf, dk[dh]);
+          }
         }
       }
     }
@@ -399,7 +431,7 @@ __global__ void __launch_bounds__(256) fa_bwd_dkdv_kernel(const bf16* __restrict
 // ------------------------------------------------------------------------------------------
 // dQ: grid (ceil(T/128) query blocks, heaviest first, B*H); forward-shaped
 template <bool DROPOUT>
-__global__ void __launch_bounds__(256) fa_bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+__global__ void __launch_bounds__(256, 2) fa_bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                                         const float* __restrict__ lse,
                                                         const float* __restrict__ delta, bf16* __restrict__ dqkv,
                                                         int T, int H, int Hkv, float scale, float p_drop,
@@ -409,7 +441,7 @@ __global__ void __launch_bounds__(256) fa_bwd_dq_kernel(const bf16* __restrict__
   const int nqb = (T + BM - 1) / BM;
   const int qb = nqb - 1 - blockIdx.x;
   const int b = blockIdx.y / H, h = blockIdx.y % H, hk = h / (H / Hkv);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5;
+  const int lane = threadIdx.x & 63, w = wave_id(), hh = lane >> 5;
   const size_t RS = (size_t)(H + 2 * Hkv) * kD;
   const size_t ORS = (size_t)H * kD;
   const bf16* kbase = qkv + (size_t)b * T * RS + (size_t)(H + hk) * kD;
@@ -484,8 +516,8 @@ __global__ void __launch_bounds__(256) fa_bwd_dq_kernel(const bf16* __restrict__
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int k = kt0 + 32 * kh + acc_row(i, lane);
-          float p = exp2f(s[kh][i] * c - l2);
-          if (k > qrow || k >= T || !qok) p = 0.f;
+          float p = fexp2(s[kh][i] * c - l2);
+          p = (k > qrow || k >= T || !qok) ? 0.f : p;
           float dpi = dp[kh][i];
           if constexpr (DROPOUT) {
             const bool keep = dropout_keep(seed, b, h, H, T, qrow, k, p_drop);

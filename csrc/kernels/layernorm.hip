@@ -13,6 +13,7 @@
 // gradient of the linear that fed this residual — are reduced per workgroup in LDS and
 // finished by a small column-reduction kernel (deterministic, no atomics).
 #include "common.h"
+#include "reduce.h"
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 
@@ -246,23 +247,6 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const TDY* __restrict__ dy,
   }
 }
 
-// out[c] += Σ_g part[g][c] for `arrays` consecutive [G, C] blocks (one output per array).
-__global__ void __launch_bounds__(256) colreduce_kernel(const float* __restrict__ part, int G, int C,
-                                                        float* __restrict__ o0, float* __restrict__ o1,
-                                                        float* __restrict__ o2) {
-  __shared__ float red[4][64];
-  const int a = blockIdx.y;
-  float* out = a == 0 ? o0 : (a == 1 ? o1 : o2);
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int r0 = threadIdx.x >> 6;
-  float s = 0.f;
-  if (c < C)
-    for (int g = r0; g < G; g += 4) s += part[((size_t)a * G + g) * C + c];
-  red[r0][threadIdx.x & 63] = s;
-  __syncthreads();
-  if (threadIdx.x < 64 && c < C) out[c] += red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-}
-
 }  // namespace penroz
 
 // ============================================================================ host side
@@ -386,7 +370,9 @@ void layernorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor mean, torch:
                                          rstd.data_ptr<float>(), w.data_ptr<float>(), dresid.data_ptr<float>(), dbf,
                                          part.data_ptr<float>(), (int)N, (int)C, accumulate ? 1 : 0,
                                          want_bias ? 1 : 0))))
-  dim3 rgrid((C + 63) / 64, want_bias ? 3 : 2);
-  hipLaunchKernelGGL(colreduce_kernel, rgrid, dim3(256), 0, stream, part.data_ptr<float>(), grid, (int)C,
-                     dw.data_ptr<float>(), db.data_ptr<float>(), want_bias ? dbias_prev->data_ptr<float>() : nullptr);
+  const int A = want_bias ? 3 : 2;
+  const int S = reduce_slices(grid);
+  auto mid = torch::empty({A, S, C}, x.options().dtype(torch::kFloat32));
+  float* outs[3] = {dw.data_ptr<float>(), db.data_ptr<float>(), want_bias ? dbias_prev->data_ptr<float>() : nullptr};
+  reduce_partials_add(part.data_ptr<float>(), A, grid, (int)C, outs, mid.data_ptr<float>(), S, stream);
 }

@@ -37,6 +37,7 @@ from penroz.ops import attention as attn_ops
 from penroz.ops import activations as act_ops
 from penroz.ops import fused as fused_ops
 from penroz.ops import norms as norm_ops
+from penroz.ops import gemm as gemm_ops
 from penroz.ops import _ext
 
 log = logging.getLogger(__name__)
@@ -326,7 +327,7 @@ class GPTExecutor:
             self.reducer.bucket_ready(bkt)
 
     def _wgrad(self, dy: Tensor, x: Tensor, p: Tensor):
-        self.grad(p).add_(torch.mm(dy.t(), x, out_dtype=torch.float32))
+        gemm_ops.wgrad(dy, x, self.grad(p))
 
     @torch.no_grad()
     def train_micro_step(self, idx: Tensor, targets: Tensor, scale: float, sync: bool = True,
