@@ -173,6 +173,14 @@ class NeuralNetworkModel(nn.Module):
         return m._progress_doc()
 
     @classmethod
+    def mark_status(cls, model_id: str, code: str, message: str):
+        """Rewrite a stored model's status (e.g. ``Error`` after a worker crash)."""
+        model = cls.deserialize(model_id)
+        model.status = _status(code, message)
+        model.serialize()
+        ckpt.wait_flushes()
+
+    @classmethod
     def delete(cls, model_id: str):
         model_path = cls.get_model_path(model_id)
         shm_path = os.path.join(cls.SHM_PATH, model_path)
@@ -296,6 +304,24 @@ class NeuralNetworkModel(nn.Module):
         for i, a in enumerate(attn):
             a.set_kv_cache(cache, i)
         return cache, pos
+
+    def _forward_nocache(self, x: Tensor):
+        """Full-context forward with any attached KV cache temporarily detached (testing aid)."""
+        attn = self._find_attention_layers()
+        pos = self._find_position_embeddings()
+        saved = [(a._kv_cache, a._layer_idx) for a in attn]
+        offs = [p.position_offset for p in pos]
+        for a in attn:
+            a.set_kv_cache(None, 0)
+        for p in pos:
+            p.position_offset = 0
+        try:
+            return self(x, skip_softmax=True)
+        finally:
+            for a, (c, i) in zip(attn, saved):
+                a.set_kv_cache(c, i)
+            for p, o in zip(pos, offs):
+                p.position_offset = o
 
     def _detach_kv_cache(self, pos_embeddings=None):
         for a in self._find_attention_layers():
@@ -584,7 +610,7 @@ class _GenericRunner:
         with self.amp if self.device.type == "cuda" else nullcontext():
             acts, loss = fwd(x, y, skip_softmax=True)
             scaled = loss * scale if scale != 1.0 else loss
-        if capture:
+        if capture and not self._acts:  # stats use the first micro-step's activations
             for a in acts:
                 a.retain_grad()
             self._acts.extend(acts)
@@ -597,7 +623,7 @@ class _GenericRunner:
         self.model.optimizer.step()
 
     def captured(self):
-        return self._algos, [(a, a.grad) for a in self._acts[:len(self._algos)]] if self._acts else []
+        return self._algos, [(a, a.grad) for a in self._acts]
 
     def close(self):
         if self.reducer is not None:

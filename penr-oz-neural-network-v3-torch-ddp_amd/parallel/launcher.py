@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import logging
 import multiprocessing as mp
+from multiprocessing import connection as mp_connection
 import os
 import socket
 import time
@@ -82,18 +83,17 @@ def launch_single_node_ddp(run_id: str, device: str, worker_op: Callable[..., No
         procs.append(p)
 
     failed_rank, failed_code = None, 0
+    alive = {p.sentinel: (rank, p) for rank, p in enumerate(procs)}
     try:
-        while True:
-            alive = False
-            for rank, p in enumerate(procs):
-                code = p.exitcode
-                if code is None:
-                    alive = True
-                elif code != 0 and failed_rank is None:
-                    failed_rank, failed_code = rank, code
-            if failed_rank is not None or not alive:
-                break
-            time.sleep(monitor_interval)
+        # wait on process sentinels: the first process to exit is seen first, so a rank that
+        # dies of a peer's crash ("connection reset") is not blamed for it
+        while alive and failed_rank is None:
+            ready = mp_connection.wait(list(alive), timeout=monitor_interval)
+            for s in sorted(ready, key=lambda x: alive[x][0]):
+                rank, p = alive.pop(s)
+                p.join()
+                if p.exitcode != 0 and failed_rank is None:
+                    failed_rank, failed_code = rank, p.exitcode
     finally:
         if failed_rank is not None:
             log.error(f"Run {run_id}: rank {failed_rank} exited with code {failed_code}; stopping the group")

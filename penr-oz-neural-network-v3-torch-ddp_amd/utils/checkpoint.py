@@ -1,6 +1,6 @@
 """Checkpoint IO: atomic writes, shared-memory cache, background disk flush, progress sidecar.
 
-Format parity with the reference (``neural_net_model.py:98-174``): ``torch.save`` of a dict
+Format parity with the reference (``neural_net_model.py:98-174``): ``torch.save`` (default pickle protocol) of a dict
 with ``layers, state, optim, optim_state, progress, average_cost, average_cost_history,
 stats, status`` at ``models/model_{id}.pth``, cached under ``{SHM}/models/``.
 
@@ -18,6 +18,7 @@ import platform
 import shutil
 import tempfile
 import threading
+import uuid
 
 import torch
 
@@ -27,6 +28,9 @@ MODELS_FOLDER = "models"
 
 
 def detect_shm_path() -> str:
+    override = os.environ.get("PENROZ_SHM_PATH")
+    if override:
+        return override
     system = platform.system()
     if system == "Linux":
         if os.path.isdir("/dev/shm") and os.access("/dev/shm", os.W_OK):
@@ -40,8 +44,7 @@ def detect_shm_path() -> str:
 def _atomic_write(path: str, writer):
     d = os.path.dirname(path) or "."
     os.makedirs(d, exist_ok=True)
-    fd, tmp = tempfile.mkstemp(prefix=".tmp_", dir=d)
-    os.close(fd)
+    tmp = f"{path}.tmp-{os.getpid()}-{threading.get_ident()}-{uuid.uuid4().hex[:8]}"
     try:
         writer(tmp)
         os.replace(tmp, path)
@@ -52,7 +55,9 @@ def _atomic_write(path: str, writer):
 
 
 def atomic_torch_save(obj, path: str):
-    _atomic_write(path, lambda tmp: torch.save(obj, tmp, pickle_protocol=5))
+    # torch's default pickle protocol (2): the only one the weights_only loader accepts (the
+    # reference writes protocol 5, which `torch.load(weights_only=True)` rejects)
+    _atomic_write(path, lambda tmp: torch.save(obj, tmp))
 
 
 def atomic_copy(src: str, dst: str):
@@ -88,4 +93,12 @@ def sidecar_path(pth_path: str) -> str:
 
 
 def load(path: str) -> dict:
-    return torch.load(path, weights_only=True, map_location="cpu")
+    """Safe load (``weights_only=True``). Legacy pickle-5 checkpoints written by the reference can
+    only be read with ``PENROZ_TRUSTED_CHECKPOINTS=1`` (an explicit opt-in to full unpickling)."""
+    try:
+        return torch.load(path, weights_only=True, map_location="cpu")
+    except Exception:
+        if os.environ.get("PENROZ_TRUSTED_CHECKPOINTS") == "1":
+            log.warning(f"loading {path} with full unpickling (PENROZ_TRUSTED_CHECKPOINTS=1)")
+            return torch.load(path, weights_only=False, map_location="cpu")
+        raise

@@ -1,0 +1,40 @@
+"""GPT pattern lowering (CPU): which layer lists the fused executor accepts."""
+import copy
+
+import bench
+from penroz.models.executor import GPTExecutor
+from penroz.models.mapper import Mapper
+from penroz.models.model import NeuralNetworkModel
+
+
+def _model(layers):
+    return NeuralNetworkModel("x", Mapper(layers, {"adamw": {"lr": 1e-3}}))
+
+
+def test_reference_example_layout_matches():
+    spec = GPTExecutor.match(_model(bench.gpt2_layers(V=128, C=128, L=2, H=2, P=64)))
+    assert spec is not None and (spec.C, spec.H, spec.D, spec.F, spec.V, spec.P) == (128, 2, 64, 512, 128, 64)
+    assert len(spec.blocks) == 2 and spec.gelu_approx == "none"
+
+
+def test_hf_style_layouts():
+    from transformers import GPT2Config
+    from penroz.models import hf
+    cfg = GPT2Config(vocab_size=128, n_positions=64, n_embd=128, n_layer=1, n_head=2)
+    assert GPTExecutor.match(_model(hf.gpt2_layers(cfg))) is None  # HF default dropout 0.1 -> generic path
+    cfg = GPT2Config(vocab_size=128, n_positions=64, n_embd=128, n_layer=1, n_head=2, resid_pdrop=0.0,
+                     embd_pdrop=0.0, attn_pdrop=0.1)
+    spec = GPTExecutor.match(_model(hf.gpt2_layers(cfg)))
+    assert spec is not None and spec.gelu_approx == "tanh"  # attention dropout runs in the flash kernel
+
+
+def test_non_matching_layouts():
+    base = bench.gpt2_layers(V=128, C=128, L=1, H=2, P=64)
+    rope = copy.deepcopy(base)
+    rope[2]["residual"][0]["sequential"][2]["attention"]["rope_theta"] = 10000.0
+    assert GPTExecutor.match(_model(rope)) is None
+    odd_head = copy.deepcopy(base)
+    odd_head[2]["residual"][0]["sequential"][2]["attention"]["num_heads"] = 4  # D = 32
+    assert GPTExecutor.match(_model(odd_head)) is None
+    mlp = [{"linear": {"in_features": 4, "out_features": 4}}, {"relu": {}}, {"linear": {"in_features": 4, "out_features": 2}}]
+    assert GPTExecutor.match(_model(mlp)) is None
