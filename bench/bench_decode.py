@@ -1,0 +1,37 @@
+"""KV-cache decode throughput: GPT-2 124M (reference example layout), random weights, one MI355X.
+
+python bench/bench_decode.py [--batch 64] [--prompt 64] [--new 128] [--turbo]
+Prints one JSON line: generated tokens/s over all rows (BASELINE config 4: batch 64 /generate).
+"""
+import argparse, json, os, sys, time
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+import bench
+from penroz.models.mapper import Mapper
+from penroz.models.model import NeuralNetworkModel
+from penroz.models import kv_cache as KV
+import penroz.models.model as M
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--batch", type=int, default=64)
+ap.add_argument("--prompt", type=int, default=64)
+ap.add_argument("--new", type=int, default=128)
+ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+ap.add_argument("--turbo", action="store_true")
+a = ap.parse_args()
+if a.turbo:
+    M.create_kv_cache = lambda n, cap=None: KV.TurboQuantKVCache(n, cap)
+torch.manual_seed(0)
+m = NeuralNetworkModel("dec", Mapper(bench.gpt2_layers(), {"adamw": {"lr": 6e-4}})).to("cuda")
+if a.dtype == "bf16":
+    m.to(dtype=torch.bfloat16)
+ctx = torch.randint(0, 50304, (a.batch, a.prompt)).tolist()
+m.generate_batch(ctx, 1024, 4, temperature=1.0, top_k=50)  # warmup
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+out = m.generate_batch(ctx, 1024, a.new, temperature=1.0, top_k=50)
+torch.cuda.synchronize()
+dt = time.perf_counter() - t0
+print(json.dumps({"metric": "decode tokens/sec (all rows)", "value": a.batch * a.new / dt, "batch": a.batch,
+                  "prompt": a.prompt, "new_tokens": a.new, "ms_per_step": dt / a.new * 1e3, "dtype": a.dtype,
+                  "kv_cache": "int8-turboquant" if a.turbo else a.dtype, "model": "gpt2-124m", "data": "random weights"}))

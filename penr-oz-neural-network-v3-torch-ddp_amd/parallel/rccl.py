@@ -1,0 +1,53 @@
+"""Python side of the native RCCL communicator (``csrc/comm/rccl_comm.cpp``).
+
+Rank 0 creates an RCCL unique id and publishes it through the ``torch.distributed`` TCPStore;
+every rank then builds its own ``ncclComm_t`` bound to its GPU and a high-priority HIP stream.
+Used by :class:`penroz.parallel.reducer.GradReducer` when ``PENROZ_COMM=native``.
+"""
+from __future__ import annotations
+
+import importlib
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+_REPO_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+_BUILD_DIR = os.path.join(_REPO_ROOT, "build_ext")
+
+
+def load_module():
+    if _BUILD_DIR not in sys.path:
+        sys.path.insert(0, _BUILD_DIR)
+    return importlib.import_module("penroz_comm")
+
+
+class NativeComm:
+    _instances: dict = {}
+
+    def __init__(self, group=None, key: str = "penroz_rccl_uid"):
+        mod = load_module()
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        store = dist.distributed_c10d._get_default_store()
+        if rank == 0:
+            store.set(key, mod.RcclComm.unique_id())
+        uid = store.get(key)
+        self.comm = mod.RcclComm(bytes(uid), rank, world, torch.cuda.current_device())
+        self.rank, self.world = rank, world
+
+    @classmethod
+    def get(cls, group=None) -> "NativeComm":
+        k = id(group)
+        if k not in cls._instances:
+            cls._instances[k] = NativeComm(group)
+        return cls._instances[k]
+
+    def all_reduce_avg_async(self, t: torch.Tensor):
+        self.comm.all_reduce_avg_async(t)
+
+    def wait_all(self):
+        self.comm.wait_all()
+
+    def broadcast(self, t: torch.Tensor, root: int = 0):
+        self.comm.broadcast(t, root)

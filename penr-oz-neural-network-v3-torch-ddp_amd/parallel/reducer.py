@@ -110,7 +110,10 @@ class GradReducer:
     def broadcast_params(self, flat_param: torch.Tensor, src: int = 0):
         """Rank-0 parameter broadcast at start (DDP ctor semantics, one collective)."""
         if self.world > 1:
-            dist.broadcast(flat_param, src=src, group=self.group)
+            if self._native is not None:
+                self._native.broadcast(flat_param, src)
+            else:
+                dist.broadcast(flat_param, src=src, group=self.group)
 
 
 class HookedReducer:
