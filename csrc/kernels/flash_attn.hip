@@ -148,21 +148,23 @@ __global__ void __launch_bounds__(256, 2) fa_fwd_kernel(const bf16* __restrict__
   for (int s = 0; s < 4; ++s)
     qf[s] = qrow < T ? *reinterpret_cast<const uint4*>(qbase + (size_t)qrow * RS + 16 * s + 8 * hh) : zero4();
 
-  const int sr = threadIdx.x >> 2, sc = 2 * (threadIdx.x & 3);
+  // staging: thread t -> chunk t&7 of rows (t>>3) + 32i (8 lanes cover one 128-B row:
+  // coalesced, conflict-free ds_write_b128 groups)
+  const int sr = threadIdx.x >> 3, sc = threadIdx.x & 7;
   uint4 kst[2], vst[2];
   auto gload = [&](int kt0) {
-    const int key = kt0 + sr;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      kst[i] = key < T ? *reinterpret_cast<const uint4*>(kbase + (size_t)key * RS + 8 * (sc + i)) : zero4();
-      vst[i] = key < T ? *reinterpret_cast<const uint4*>(vbase + (size_t)key * RS + 8 * (sc + i)) : zero4();
+      const int key = kt0 + sr + 32 * i;
+      kst[i] = key < T ? *reinterpret_cast<const uint4*>(kbase + (size_t)key * RS + 8 * sc) : zero4();
+      vst[i] = key < T ? *reinterpret_cast<const uint4*>(vbase + (size_t)key * RS + 8 * sc) : zero4();
     }
   };
   auto lstore = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      *reinterpret_cast<uint4*>(smem[buf][0] + tile_off(sr, sc + i)) = kst[i];
-      *reinterpret_cast<uint4*>(smem[buf][1] + tile_off(sr, sc + i)) = vst[i];
+      *reinterpret_cast<uint4*>(smem[buf][0] + tile_off(sr + 32 * i, sc)) = kst[i];
+      *reinterpret_cast<uint4*>(smem[buf][1] + tile_off(sr + 32 * i, sc)) = vst[i];
     }
   };
 
@@ -321,9 +323,9 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv_kernel(const bf16* __restr
 #pragma unroll
     for (int i = 0; i < 16; ++i) dk[dh][i] = dv[dh][i] = 0.f;
 
-  // staging: threads 0..127 -> Q slice, 128..255 -> dO slice; each thread 4 chunks of one row
-  // half: row (t>>1)&63, chunks 4(t&1)..+3
-  const int st_tile = threadIdx.x >> 7, sr = (threadIdx.x >> 1) & 63, sc = 4 * (threadIdx.x & 1);
+  // staging: threads 0..127 -> Q slice, 128..255 -> dO slice; thread -> chunk t&7 of rows
+  // ((t>>3)&15) + 16i, i = 0..3 (coalesced, conflict-free ds_write_b128 groups)
+  const int st_tile = threadIdx.x >> 7, sr = (threadIdx.x >> 3) & 15, sc = threadIdx.x & 7;
   const int s_first = (kb * BK) / QS;
   const int nslices = (T + QS - 1) / QS;
   const int per_head = nslices - s_first;
@@ -333,11 +335,14 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv_kernel(const bf16* __restr
   auto gload = [&](int it) {
     const int hq = hk * G + it / per_head;
     const int qs0 = (s_first + it % per_head) * QS;
-    const int q = qs0 + sr;
-    const bf16* src = st_tile == 0 ? qkv + (size_t)b * T * RS + (size_t)hq * kD + (size_t)q * RS
-                                   : dout + (size_t)b * T * ORS + (size_t)hq * kD + (size_t)q * ORS;
+    const bf16* src = st_tile == 0 ? qkv + (size_t)b * T * RS + (size_t)hq * kD
+                                   : dout + (size_t)b * T * ORS + (size_t)hq * kD;
+    const size_t rs = st_tile == 0 ? RS : ORS;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) st[i] = q < T ? *reinterpret_cast<const uint4*>(src + 8 * (sc + i)) : zero4();
+    for (int i = 0; i < 4; ++i) {
+      const int q = qs0 + sr + 16 * i;
+      st[i] = q < T ? *reinterpret_cast<const uint4*>(src + (size_t)q * rs + 8 * sc) : zero4();
+    }
     if (threadIdx.x < 2 * QS) {
       const int qq = qs0 + (threadIdx.x & (QS - 1));
       const size_t r = ((size_t)b * H + hq) * T + qq;
@@ -347,7 +352,7 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv_kernel(const bf16* __restr
   auto lstore = [&](int buf) {
     char* dst = st_tile == 0 ? qt[buf] : dot[buf];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(dst + tile_off(sr, sc + i)) = st[i];
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(dst + tile_off(sr + 16 * i, sc)) = st[i];
     if (threadIdx.x < QS) lse2s[buf][threadIdx.x] = st_scalar;
     else if (threadIdx.x < 2 * QS) dels[buf][threadIdx.x - QS] = st_scalar;
   };
@@ -466,21 +471,23 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dq_kernel(const bf16* __restric
   const float l2 = qok ? lse[rr] * kLog2e : 0.f;
   const float dl = qok ? delta[rr] : 0.f;
 
-  const int sr = threadIdx.x >> 2, sc = 2 * (threadIdx.x & 3);
+  // staging: thread t -> chunk t&7 of rows (t>>3) + 32i (8 lanes cover one 128-B row:
+  // coalesced, conflict-free ds_write_b128 groups)
+  const int sr = threadIdx.x >> 3, sc = threadIdx.x & 7;
   uint4 kst[2], vst[2];
   auto gload = [&](int kt0) {
-    const int k = kt0 + sr;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      kst[i] = k < T ? *reinterpret_cast<const uint4*>(kbase + (size_t)k * RS + 8 * (sc + i)) : zero4();
-      vst[i] = k < T ? *reinterpret_cast<const uint4*>(vbase + (size_t)k * RS + 8 * (sc + i)) : zero4();
+      const int key = kt0 + sr + 32 * i;
+      kst[i] = key < T ? *reinterpret_cast<const uint4*>(kbase + (size_t)key * RS + 8 * sc) : zero4();
+      vst[i] = key < T ? *reinterpret_cast<const uint4*>(vbase + (size_t)key * RS + 8 * sc) : zero4();
     }
   };
   auto lstore = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      *reinterpret_cast<uint4*>(smem[buf][0] + tile_off(sr, sc + i)) = kst[i];
-      *reinterpret_cast<uint4*>(smem[buf][1] + tile_off(sr, sc + i)) = vst[i];
+      *reinterpret_cast<uint4*>(smem[buf][0] + tile_off(sr + 32 * i, sc)) = kst[i];
+      *reinterpret_cast<uint4*>(smem[buf][1] + tile_off(sr + 32 * i, sc)) = vst[i];
     }
   };
   const int kend = min(T, qb * BM + BM);

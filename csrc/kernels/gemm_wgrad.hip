@@ -69,15 +69,17 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(const bf16* __restrict__ 
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), hh = lane >> 5;
   const int wm = w >> 1, wn = w & 1;
 
-  // staging: thread t -> row r = t>>2 of the k-tile, chunks 4(t&3)..+3 (8 bf16 each)
-  const int sr = threadIdx.x >> 2, sc = 4 * (threadIdx.x & 3);
+  // staging: consecutive lanes take consecutive 16-B chunks of a row (coalesced global
+  // loads; every 8-lane ds_write_b128 group covers 8 distinct chunks = all 32 banks):
+  // thread t -> chunk t&15 of rows (t>>4) + 16i, i = 0..3
+  const int sr = threadIdx.x >> 4, sc = threadIdx.x & 15;
   uint4 ast[4], bst[4];
   auto gload = [&](int kk) {
-    const int k = kk + sr;
-    const bool kok = k < k1;
+    const int mc = m0 + 8 * sc, nc = n0 + 8 * sc;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int mc = m0 + 8 * (sc + i), nc = n0 + 8 * (sc + i);
+      const int k = kk + sr + 16 * i;
+      const bool kok = k < k1;
       ast[i] = (kok && mc < M) ? *reinterpret_cast<const uint4*>(A + (size_t)k * lda + mc) : uint4{0, 0, 0, 0};
       bst[i] = (kok && nc < N) ? *reinterpret_cast<const uint4*>(B + (size_t)k * ldb + nc) : uint4{0, 0, 0, 0};
     }
@@ -85,8 +87,8 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(const bf16* __restrict__ 
   auto lstore = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      *reinterpret_cast<uint4*>(smem[buf][0] + off256(sr, sc + i)) = ast[i];
-      *reinterpret_cast<uint4*>(smem[buf][1] + off256(sr, sc + i)) = bst[i];
+      *reinterpret_cast<uint4*>(smem[buf][0] + off256(sr + 16 * i, sc)) = ast[i];
+      *reinterpret_cast<uint4*>(smem[buf][1] + off256(sr + 16 * i, sc)) = bst[i];
     }
   };
 
@@ -143,6 +145,183 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(const bf16* __restrict__ 
     }
 }
 
+
+// ---------------------------------------------------------------------------------------
+// 256×256 tile, 8 waves (2 along M × 4 along N, each wave 128×64 = 4×2 MFMA tiles), BK = 64.
+// Per k-step: 64 KiB of operands for 2·256·256·64 FLOP = 128 FLOP/B (the 128² tile's 64 FLOP/B
+// left it L2-bandwidth-bound at 320–500 TF). LDS rows are 512 B; chunk ch of row r lives at
+// ch ^ ((r&3)<<2), which keeps the 4-row × 4-chunk transposed half-wave reads conflict-free.
+constexpr int BM2 = 256, BN2 = 256, BK2 = 64;
+
+__device__ __forceinline__ int off512(int row, int ch) { return row * 512 + ((ch ^ ((row & 3) << 2)) << 4); }
+
+__device__ __forceinline__ uint2 tr_read512(const char* tile, int row, int col) {
+  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + off512(row, col >> 3) + ((col & 4) << 1)));
+  return __builtin_bit_cast(uint2, v);
+}
+
+__device__ __forceinline__ uint4 tr_frag512(const char* tile, int rbase, int cbase, int lane) {
+  const int hh = lane >> 5, q = (lane & 15) >> 2, p = lane & 3;
+  const int col = cbase + 16 * ((lane >> 4) & 1) + 4 * p;
+  const uint2 a = tr_read512(tile, rbase + 4 * hh + q, col);
+  const uint2 b = tr_read512(tile, rbase + 8 + 4 * hh + q, col);
+  return uint4{a.x, a.y, b.x, b.y};
+}
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void gbl_void_t;
+__device__ uint4 g_zero16[1];  // zero-initialised: source of out-of-range LDS-DMA lanes
+
+// one global_load_lds_dwordx4: 64 lanes x 16 B from per-lane `g` to LDS [lds_addr, +1 KiB).
+// Issued as inline asm so hipcc's waitcnt pass does not serialise it against ds_reads of the
+// other LDS buffer; completion is counted by hand (s_waitcnt vmcnt before the barrier).
+__device__ __forceinline__ void glds16(const void* g, unsigned lds_addr) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(g), "s"(lds_addr)
+               : "memory");
+}
+
+// GLDS: stage tiles with global_load_lds_dwordx4 (LDS-DMA, no VGPR round trip, no ds_write
+// transfer cost). The DMA destination is lane-linear (1 KiB per wave-instruction = two 512-B
+// k-rows), so the XOR swizzle is applied on the per-lane SOURCE address instead.
+template <bool GLDS>
+__global__ void __launch_bounds__(512, 1) wgrad256_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                          float* __restrict__ out, int M, int N, int K, int lda,
+                                                          int ldb, int klen, int tiles_m, int tiles_n, int direct) {
+  extern __shared__ __attribute__((aligned(16))) char smem2[];  // [2 buf][A|B][BK2 * 512]
+  const int nwg = gridDim.x, wg = blockIdx.x;
+  const int xcd = wg & 7, qd = nwg >> 3, rd = nwg & 7;
+  const int id = (xcd < rd ? xcd * (qd + 1) : rd * (qd + 1) + (xcd - rd) * qd) + (wg >> 3);
+  const int ntiles = tiles_m * tiles_n;
+  const int split = id / ntiles, tile = id - split * ntiles;
+  const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+  const int m0 = tm * BM2, n0 = tn * BN2;
+  const int k0 = split * klen, k1 = min(K, k0 + klen);
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), hh = lane >> 5;
+  const int wm = w >> 2, wn = w & 3;
+  constexpr int TILE = BK2 * 512;
+
+  // staging: thread t -> chunk t&31 of rows (t>>5) + 16i, i = 0..3 (a wave covers two whole
+  // 512-B rows: coalesced loads, conflict-free ds_write_b128 groups)
+  const int sr = threadIdx.x >> 5, sc = threadIdx.x & 31;
+  uint4 ast[4], bst[4];
+  auto gload = [&](int kk) {
+    const int mc = m0 + 8 * sc, nc = n0 + 8 * sc;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = kk + sr + 16 * i;
+      const bool kok = k < k1;
+      ast[i] = (kok && mc < M) ? *reinterpret_cast<const uint4*>(A + (size_t)k * lda + mc) : uint4{0, 0, 0, 0};
+      bst[i] = (kok && nc < N) ? *reinterpret_cast<const uint4*>(B + (size_t)k * ldb + nc) : uint4{0, 0, 0, 0};
+    }
+  };
+  auto lstore = [&](int buf) {
+    char* a = smem2 + buf * 2 * TILE;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      *reinterpret_cast<uint4*>(a + off512(sr + 16 * i, sc)) = ast[i];
+      *reinterpret_cast<uint4*>(a + TILE + off512(sr + 16 * i, sc)) = bst[i];
+    }
+  };
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // LDS-DMA staging: wave w fills pieces 4w..4w+3 (rows 2p, 2p+1) of both tiles. Per-lane
+  // source offsets are fixed across k-steps (row-in-tile and swizzled chunk); out-of-range
+  // lanes read the zero page.
+  const int rl = lane >> 5, pc = lane & 31;
+  const bf16* asrc[4];
+  const bf16* bsrc[4];
+  int krow[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 2 * (4 * w + i) + rl;
+    const int ch = pc ^ ((row & 3) << 2);  // off512's swizzle, inverted (an involution)
+    const int mc = m0 + 8 * ch, nc = n0 + 8 * ch;
+    krow[i] = k0 + row;
+    asrc[i] = mc < M ? A + (size_t)krow[i] * lda + mc : nullptr;
+    bsrc[i] = nc < N ? B + (size_t)krow[i] * ldb + nc : nullptr;
+  }
+  const unsigned lds_base = (unsigned)(size_t)(lds_void_t*)smem2;
+  const void* zero = (const void*)g_zero16;
+  auto dma = [&](int st, int buf) {
+    const int dk = st * BK2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bool kok = krow[i] + dk < k1;
+      const void* ga = (kok && asrc[i]) ? (const void*)(asrc[i] + (size_t)dk * lda) : zero;
+      const void* gb = (kok && bsrc[i]) ? (const void*)(bsrc[i] + (size_t)dk * ldb) : zero;
+      const unsigned la = __builtin_amdgcn_readfirstlane(lds_base + buf * 2 * TILE + (4 * w + i) * 1024);
+      glds16(ga, la);
+      glds16(gb, la + TILE);
+    }
+  };
+
+  const int nsteps = (k1 - k0 + BK2 - 1) / BK2;
+  if (nsteps > 0) {
+    if constexpr (GLDS) {
+      dma(0, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      gload(k0);
+      lstore(0);
+    }
+  }
+  __syncthreads();
+  for (int st = 0; st < nsteps; ++st) {
+    if constexpr (GLDS) {
+      if (st + 1 < nsteps) dma(st + 1, (st + 1) & 1);
+    } else {
+      if (st + 1 < nsteps) gload(k0 + (st + 1) * BK2);
+    }
+    const char* At = smem2 + (st & 1) * 2 * TILE;
+    const char* Bt = At + TILE;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      uint4 af[4], bf[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bf[j] = tr_frag512(Bt, 16 * s, 64 * wn + 32 * j, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = tr_frag512(At, 16 * s, 128 * wm + 32 * i, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(af[i], bf[j], acc[i][j]);
+    }
+    if constexpr (GLDS) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      if (st + 1 < nsteps) lstore((st + 1) & 1);
+    }
+    __syncthreads();
+  }
+  float* o = direct ? out : out + (size_t)split * M * N;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + 64 * wn + 32 * j + (lane & 31);
+      if (n >= N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + 128 * wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        if (m < M) {
+          float* p = o + (size_t)m * N + n;
+          if (direct) *p += acc[i][j][r];
+          else *p = acc[i][j][r];
+        }
+      }
+    }
+}
+
 // G[e] += Σ_s slab[s][e]  (vectorised, fixed order)
 __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restrict__ slab, float* __restrict__ g,
                                                           int64_t n4, int splits, int64_t stride4) {
@@ -158,8 +337,9 @@ __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restric
 
 using namespace penroz;
 
-// grad[M][N] += dyᵀ·x with dy [K, M], x [K, N] (bf16, row-major, contiguous rows)
-void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad) {
+// grad[M][N] += dyᵀ·x with dy [K, M], x [K, N] (bf16, row-major, contiguous rows).
+// tile = 256 (default, 8 waves) or 128 (4 waves); glds selects LDS-DMA staging for the 256 tile.
+void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad, int64_t tile, bool glds) {
   TORCH_CHECK(dy.is_cuda() && x.is_cuda() && grad.is_cuda());
   TORCH_CHECK(dy.scalar_type() == torch::kBFloat16 && x.scalar_type() == torch::kBFloat16 &&
               grad.scalar_type() == torch::kFloat32, "wgrad: bf16 operands, fp32 gradient");
@@ -169,24 +349,65 @@ void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad) {
   TORCH_CHECK(grad.size(0) == M && grad.size(1) == N, "wgrad: gradient shape mismatch");
   TORCH_CHECK(M % 8 == 0 && N % 8 == 0 && dy.stride(0) % 8 == 0 && x.stride(0) % 8 == 0,
               "wgrad: widths and row strides must be multiples of 8");
+  TORCH_CHECK(tile == 128 || tile == 256, "wgrad: tile must be 128 or 256");
   if (K == 0) return;
-  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+  const int T = (int)tile;
+  const int tiles_m = (M + T - 1) / T, tiles_n = (N + T - 1) / T;
   const int ntiles = tiles_m * tiles_n;
-  int splits = std::max(1, std::min((512 + ntiles - 1) / ntiles, K / 512));
-  int klen = ((K + splits - 1) / splits + BK - 1) / BK * BK;
+  // Split-K count from a wave-quantisation cost model: the launch runs ceil(ntiles·s / slots)
+  // waves of workgroups, each 1/s of the K loop long, plus the slab round trip (s slabs written
+  // and read once) priced against the per-workgroup MFMA time. slots = resident workgroups:
+  // 1 (256-tile, 128 KiB LDS) or 2 (128-tile) per CU.
+  static int n_cu = 0;
+  if (n_cu == 0) {
+    hipDeviceProp_t prop;
+    n_cu = hipGetDeviceProperties(&prop, grad.get_device()) == hipSuccess ? prop.multiProcessorCount : 256;
+  }
+  const int slots = T == 256 ? n_cu : 2 * n_cu;
+  const double wg_full_k = (double)T * T * 2.0 * K / (T == 256 ? 2.3e12 : 1.1e12);  // seconds, one workgroup
+  int splits = 1;
+  double best = 1e30;
+  for (int s = 1; s <= std::max(1, K / 512) && s <= 64; ++s) {
+    const double waves = (double)((ntiles * (int64_t)s + slots - 1) / slots);
+    const double slab = s > 1 ? (double)s * M * N * 8.0 / 4.0e12 : 0.0;
+    const double cost = waves * wg_full_k / s + slab;
+    if (cost < best * 0.995) best = cost, splits = s;
+  }
+  const int bk = T == 256 ? BK2 : BK;
+  int klen = ((K + splits - 1) / splits + bk - 1) / bk * bk;
   splits = (K + klen - 1) / klen;
   auto stream = at::hip::getCurrentHIPStream();
   const int nwg = ntiles * splits;
   const bf16* a = reinterpret_cast<const bf16*>(dy.data_ptr());
   const bf16* b = reinterpret_cast<const bf16*>(x.data_ptr());
-  if (splits == 1) {
-    hipLaunchKernelGGL(wgrad_kernel, dim3(nwg), dim3(256), 0, stream, a, b, grad.data_ptr<float>(), M, N, K,
-                       (int)dy.stride(0), (int)x.stride(0), klen, tiles_m, tiles_n, 1);
-    return;
+  torch::Tensor slab;
+  float* dst = grad.data_ptr<float>();
+  if (splits > 1) {
+    slab = torch::empty({(int64_t)splits * M * N}, grad.options());
+    dst = slab.data_ptr<float>();
   }
-  auto slab = torch::empty({(int64_t)splits * M * N}, grad.options());
-  hipLaunchKernelGGL(wgrad_kernel, dim3(nwg), dim3(256), 0, stream, a, b, slab.data_ptr<float>(), M, N, K,
-                     (int)dy.stride(0), (int)x.stride(0), klen, tiles_m, tiles_n, 0);
+  const int direct = splits == 1 ? 1 : 0;
+  if (T == 256) {
+    const size_t lds = 2 * 2 * BK2 * 512;
+    static bool attr_set = false;
+    if (!attr_set) {
+      hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad256_kernel<true>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad256_kernel<false>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      attr_set = true;
+    }
+    if (glds)
+      hipLaunchKernelGGL(wgrad256_kernel<true>, dim3(nwg), dim3(512), lds, stream, a, b, dst, M, N, K,
+                         (int)dy.stride(0), (int)x.stride(0), klen, tiles_m, tiles_n, direct);
+    else
+      hipLaunchKernelGGL(wgrad256_kernel<false>, dim3(nwg), dim3(512), lds, stream, a, b, dst, M, N, K,
+                         (int)dy.stride(0), (int)x.stride(0), klen, tiles_m, tiles_n, direct);
+  } else {
+    hipLaunchKernelGGL(wgrad_kernel, dim3(nwg), dim3(256), 0, stream, a, b, dst, M, N, K, (int)dy.stride(0),
+                       (int)x.stride(0), klen, tiles_m, tiles_n, direct);
+  }
+  if (splits == 1) return;
   const int64_t n4 = (int64_t)M * N / 4;
   hipLaunchKernelGGL(slab_reduce_kernel, dim3((int)std::min<int64_t>((n4 + 255) / 256, 2048)), dim3(256), 0, stream,
                      slab.data_ptr<float>(), grad.data_ptr<float>(), n4, splits, n4);

@@ -1,6 +1,8 @@
 """Build the penroz native extensions in-tree for gfx950 with hipcc (no hipify, no CUDA).
 
     python setup.py build_ext        # -> build_ext/penroz_kernels*.so, build_ext/penroz_comm*.so
+    python setup.py isa KERNEL.hip   # -> build_ext/isa/KERNEL.s (gfx950 device assembly, for audits:
+                                     #    VGPR/AGPR counts, spills, s_waitcnt placement)
 
 Each ``csrc/kernels/*.hip`` is compiled with ``hipcc --offload-arch=gfx950`` in parallel and
 linked together with the pybind11 bindings against PyTorch's own libraries (including the
@@ -102,7 +104,24 @@ def build_all(jobs: int | None = None) -> list[str]:
     return built
 
 
+def dump_isa(src_name: str) -> str:
+    """Device assembly of one kernel source (``--cuda-device-only -S``)."""
+    src = os.path.join(CSRC, "kernels", src_name)
+    out_dir = os.path.join(OUT, "isa")
+    os.makedirs(out_dir, exist_ok=True)
+    out = os.path.join(out_dir, os.path.splitext(src_name)[0] + ".s")
+    cmd = [HIPCC] + _flags("penroz_kernels") + ["--cuda-device-only", "-S", src, "-o", out]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"isa dump failed: {src}\n{r.stderr}")
+    return out
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[1] == "isa":
+        for name in sys.argv[2:]:
+            print(dump_isa(name))
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] not in ("build_ext", "build"):
         print(__doc__)
         sys.exit(2)
