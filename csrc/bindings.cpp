@@ -41,7 +41,7 @@ torch::Tensor sample_tokens(torch::Tensor logits, c10::optional<torch::Tensor> u
 torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c10::optional<torch::Tensor> k_scale,
                           c10::optional<torch::Tensor> v_scale, int64_t S, int64_t q_offset, double scale);
 // gemm_wgrad.hip
-void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad, int64_t tile, bool glds);
+void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad, int64_t tile, int64_t variant);
 // flash_attn.hip
 void flash_attn_fwd(torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int64_t H, int64_t Hkv, int64_t D,
                     double scale, double p_drop, int64_t seed);
@@ -72,7 +72,7 @@ PYBIND11_MODULE(penroz_kernels, m) {
   m.def("sample_tokens", &sample_tokens);
   m.def("decode_attn", &decode_attn);
   m.def("wgrad_gemm", &wgrad_gemm, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("grad"),
-        pybind11::arg("tile") = 256, pybind11::arg("glds") = true);
+        pybind11::arg("tile") = 256, pybind11::arg("variant") = 2);
   m.def("flash_attn_fwd", &flash_attn_fwd);
   m.def("flash_attn_bwd", &flash_attn_bwd);
 }

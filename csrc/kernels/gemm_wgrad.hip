@@ -2,20 +2,23 @@
 //
 // For a linear y = x·Wᵀ: A = dY [tokens, out], B = X [tokens, in], G = dW [out, in]. Both
 // operands are row-major in the reduction dimension k (tokens), which is what makes this GEMM
-// awkward for library kernels at GPT-2 shapes (hipBLASLt measured 280–670 TF here: tiny M×N,
-// K = 65 536).  Design:
-//   * 128×128 output tile per 256-thread workgroup (4 waves, 2×2 of 64×64 = 2×2 MFMA
-//     32x32x16 tiles each), k-step 64;
-//   * both operand tiles are staged row-major [64 k][128] in LDS (16-B global loads, issued one
-//     k-step ahead into registers, written after the MFMAs — T14) and consumed column-wise
-//     with ds_read_b64_tr_b16, so no transposes in memory; 256-B rows use the XOR swizzle
-//     ch ^ ((row&3)<<2 | (row>>2)&3), which makes the 4-row × 4-chunk transposed half-wave
-//     reads bank-conflict-free;
-//   * split-K over tokens to put ≥ 512 workgroups on 256 CUs; each split writes an fp32
-//     slab and a deterministic column-ordered reduction adds the slabs into the gradient
-//     buffer (fused accumulate, bitwise reproducible); one split => direct read-add-write;
+// awkward for library kernels at GPT-2 shapes (hipBLASLt measured 270–980 TF here: small M×N,
+// K = 65 536).  Design (default path = wgrad256_ring_kernel<32, 4>):
+//   * 256×256 output tile per 512-thread workgroup (8 waves as 2×4, each 128×64 = 4×2 MFMA
+//     32x32x16 tiles), one workgroup per CU (128 KiB LDS);
+//   * operand tiles arrive by LDS-DMA (global_load_lds_dwordx4, issued in inline asm so the
+//     compiler does not serialise it against ds_reads) into a 4-stage ring of [32 k][256]
+//     tiles; three stages are in flight and the end-of-step wait is a counted vmcnt;
+//   * tiles are consumed column-wise with ds_read_b64_tr_b16 (no transposes in memory); the
+//     512-B rows use the XOR swizzle ch ^ ((row&3)<<2), applied on the DMA SOURCE address
+//     because the DMA destination is lane-linear;
+//   * split-K over tokens chosen by a wave-quantisation cost model; each split writes an fp32
+//     slab and a deterministic fixed-order reduction adds the slabs into the gradient buffer
+//     (bitwise reproducible); one split => direct read-add-write;
 //   * XCD-aware bijective block remap: a contiguous chunk of (split, tile) pairs per XCD so
 //     workgroups sharing a k-range and an operand panel share that XCD's L2.
+// wgrad_kernel (128×128, 4 waves, register staging) and wgrad256_kernel (double-buffered)
+// are kept as selectable variants for A/B measurement.
 #include "common.h"
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
@@ -322,6 +325,110 @@ __global__ void __launch_bounds__(512, 1) wgrad256_kernel(const bf16* __restrict
     }
 }
 
+// LDS-DMA ring: NBUF stages of BKT k-rows; tile t+NBUF-1 is issued while tile t is consumed,
+// and the end-of-step wait is a counted vmcnt that leaves NBUF-2 tiles in flight across the
+// barrier (tiles beyond the split's range DMA the zero page, so the count is uniform).
+template <int BKT, int NBUF>
+__global__ void __launch_bounds__(512, 1) wgrad256_ring_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                               float* __restrict__ out, int M, int N, int K, int lda,
+                                                               int ldb, int klen, int tiles_m, int tiles_n,
+                                                               int direct) {
+  extern __shared__ __attribute__((aligned(16))) char smem2[];  // [NBUF][A|B][BKT * 512]
+  constexpr int TILE = BKT * 512;
+  constexpr int PIECES = BKT / 16;  // 1-KiB pieces per wave per operand per stage
+  constexpr int G = 2 * PIECES;     // DMA instructions per wave per stage
+  static_assert(BKT % 16 == 0 && NBUF >= 3 && (NBUF - 2) * G <= 63, "ring geometry");
+  const int nwg = gridDim.x, wg = blockIdx.x;
+  const int xcd = wg & 7, qd = nwg >> 3, rd = nwg & 7;
+  const int id = (xcd < rd ? xcd * (qd + 1) : rd * (qd + 1) + (xcd - rd) * qd) + (wg >> 3);
+  const int ntiles = tiles_m * tiles_n;
+  const int split = id / ntiles, tile = id - split * ntiles;
+  const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+  const int m0 = tm * BM2, n0 = tn * BN2;
+  const int k0 = split * klen, k1 = min(K, k0 + klen);
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), hh = lane >> 5;
+  const int wm = w >> 2, wn = w & 3;
+
+  const int rl = lane >> 5, pc = lane & 31;
+  const bf16* asrc[PIECES];
+  const bf16* bsrc[PIECES];
+  int krow[PIECES];
+#pragma unroll
+  for (int i = 0; i < PIECES; ++i) {
+    const int row = 2 * (PIECES * w + i) + rl;
+    const int ch = pc ^ ((row & 3) << 2);
+    const int mc = m0 + 8 * ch, nc = n0 + 8 * ch;
+    krow[i] = k0 + row;
+    asrc[i] = mc < M ? A + (size_t)krow[i] * lda + mc : nullptr;
+    bsrc[i] = nc < N ? B + (size_t)krow[i] * ldb + nc : nullptr;
+  }
+  const unsigned lds_base = (unsigned)(size_t)(lds_void_t*)smem2;
+  const void* zero = (const void*)g_zero16;
+  auto dma = [&](int st) {
+    const int dk = st * BKT, buf = st % NBUF;
+#pragma unroll
+    for (int i = 0; i < PIECES; ++i) {
+      const bool kok = krow[i] + dk < k1;
+      const void* ga = (kok && asrc[i]) ? (const void*)(asrc[i] + (size_t)dk * lda) : zero;
+      const void* gb = (kok && bsrc[i]) ? (const void*)(bsrc[i] + (size_t)dk * ldb) : zero;
+      const unsigned la = __builtin_amdgcn_readfirstlane(lds_base + buf * 2 * TILE + (PIECES * w + i) * 1024);
+      glds16(ga, la);
+      glds16(gb, la + TILE);
+    }
+  };
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nsteps = (k1 - k0 + BKT - 1) / BKT;
+#pragma unroll
+  for (int t = 0; t < NBUF - 1; ++t) dma(t);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NBUF - 2) * G) : "memory");
+  __syncthreads();
+  for (int st = 0; st < nsteps; ++st) {
+    dma(st + NBUF - 1);  // into the stage consumed at step st-1 (freed by its barrier)
+    const char* At = smem2 + (st % NBUF) * 2 * TILE;
+    const char* Bt = At + TILE;
+#pragma unroll
+    for (int s = 0; s < BKT / 16; ++s) {
+      uint4 af[4], bf[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bf[j] = tr_frag512(Bt, 16 * s, 64 * wn + 32 * j, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = tr_frag512(At, 16 * s, 128 * wm + 32 * i, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(af[i], bf[j], acc[i][j]);
+    }
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NBUF - 2) * G) : "memory");  // stage st+1 landed
+    __syncthreads();
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the zero-page prefetches
+  float* o = direct ? out : out + (size_t)split * M * N;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + 64 * wn + 32 * j + (lane & 31);
+      if (n >= N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + 128 * wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        if (m < M) {
+          float* p = o + (size_t)m * N + n;
+          if (direct) *p += acc[i][j][r];
+          else *p = acc[i][j][r];
+        }
+      }
+    }
+}
+
 // G[e] += Σ_s slab[s][e]  (vectorised, fixed order)
 __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restrict__ slab, float* __restrict__ g,
                                                           int64_t n4, int splits, int64_t stride4) {
@@ -338,8 +445,8 @@ __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restric
 using namespace penroz;
 
 // grad[M][N] += dyᵀ·x with dy [K, M], x [K, N] (bf16, row-major, contiguous rows).
-// tile = 256 (default, 8 waves) or 128 (4 waves); glds selects LDS-DMA staging for the 256 tile.
-void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad, int64_t tile, bool glds) {
+// tile = 256 (default, 8 waves) or 128 (4 waves); variant selects the 256-tile pipeline (see below).
+void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad, int64_t tile, int64_t variant) {
   TORCH_CHECK(dy.is_cuda() && x.is_cuda() && grad.is_cuda());
   TORCH_CHECK(dy.scalar_type() == torch::kBFloat16 && x.scalar_type() == torch::kBFloat16 &&
               grad.scalar_type() == torch::kFloat32, "wgrad: bf16 operands, fp32 gradient");
@@ -388,21 +495,42 @@ void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad, int64_t t
   }
   const int direct = splits == 1 ? 1 : 0;
   if (T == 256) {
-    const size_t lds = 2 * 2 * BK2 * 512;
+    // variant: 0 = register staging, 1 = LDS-DMA double buffer (BK 64), 2 = LDS-DMA ring
+    // (BK 32 x 4 stages; default, fastest measured), 3 = LDS-DMA ring (BK 32 x 5 stages).
+    // GPT-2 124M, K = 65 536 (TF): qkv 703/809/863/873, proj 683/766/774/766,
+    // fc 792/911/962/956, fc2 829/954/984/960, lm_head 911/1019/1032/1024.
     static bool attr_set = false;
     if (!attr_set) {
+      const int l2 = 2 * 2 * BK2 * 512;
       hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad256_kernel<true>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                          hipFuncAttributeMaxDynamicSharedMemorySize, l2);
       hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad256_kernel<false>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                          hipFuncAttributeMaxDynamicSharedMemorySize, l2);
+      hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad256_ring_kernel<32, 4>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 4 * 2 * 32 * 512);
+      hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad256_ring_kernel<32, 5>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 5 * 2 * 32 * 512);
       attr_set = true;
     }
-    if (glds)
-      hipLaunchKernelGGL(wgrad256_kernel<true>, dim3(nwg), dim3(512), lds, stream, a, b, dst, M, N, K,
-                         (int)dy.stride(0), (int)x.stride(0), klen, tiles_m, tiles_n, direct);
-    else
-      hipLaunchKernelGGL(wgrad256_kernel<false>, dim3(nwg), dim3(512), lds, stream, a, b, dst, M, N, K,
-                         (int)dy.stride(0), (int)x.stride(0), klen, tiles_m, tiles_n, direct);
+    const int lda = (int)dy.stride(0), ldb = (int)x.stride(0);
+    switch (variant) {
+      case 0:
+        hipLaunchKernelGGL(wgrad256_kernel<false>, dim3(nwg), dim3(512), 2 * 2 * BK2 * 512, stream, a, b, dst, M, N,
+                           K, lda, ldb, klen, tiles_m, tiles_n, direct);
+        break;
+      case 1:
+        hipLaunchKernelGGL(wgrad256_kernel<true>, dim3(nwg), dim3(512), 2 * 2 * BK2 * 512, stream, a, b, dst, M, N,
+                           K, lda, ldb, klen, tiles_m, tiles_n, direct);
+        break;
+      case 2:
+        hipLaunchKernelGGL((wgrad256_ring_kernel<32, 4>), dim3(nwg), dim3(512), 4 * 2 * 32 * 512, stream, a, b, dst,
+                           M, N, K, lda, ldb, klen, tiles_m, tiles_n, direct);
+        break;
+      default:
+        hipLaunchKernelGGL((wgrad256_ring_kernel<32, 5>), dim3(nwg), dim3(512), 5 * 2 * 32 * 512, stream, a, b, dst,
+                           M, N, K, lda, ldb, klen, tiles_m, tiles_n, direct);
+        break;
+    }
   } else {
     hipLaunchKernelGGL(wgrad_kernel, dim3(nwg), dim3(256), 0, stream, a, b, dst, M, N, K, (int)dy.stride(0),
                        (int)x.stride(0), klen, tiles_m, tiles_n, direct);

@@ -324,15 +324,15 @@ def test_tensor_stats():
     _close(hist.cpu(), h.hist, 2e-3, 0.01)
 
 
-@pytest.mark.parametrize("tile,glds", [(128, False), (256, False), (256, True)])
+@pytest.mark.parametrize("tile,variant", [(128, 0), (256, 0), (256, 1), (256, 2), (256, 3)])
 @pytest.mark.parametrize("K,M,N", [(65536, 2304, 768), (4096, 768, 768), (1000, 200, 136), (8192, 50304, 768), (3000, 1600, 6400)])
-def test_wgrad_gemm(K, M, N, tile, glds):
+def test_wgrad_gemm(K, M, N, tile, variant):
     from penroz.ops import gemm as G
     torch.manual_seed(0)
     dy = torch.randn(K, M, device=DEV).to(torch.bfloat16)
     x = torch.randn(K, N, device=DEV).to(torch.bfloat16)
     grad = torch.randn(M, N, device=DEV)
     ref = grad + dy.float().t() @ x.float()
-    _ext.kernels().wgrad_gemm(dy, x, grad, tile, glds)
+    _ext.kernels().wgrad_gemm(dy, x, grad, tile, variant)
     rel = (grad - ref).norm() / ref.norm()
     assert rel < 1e-4, rel
