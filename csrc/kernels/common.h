@@ -28,8 +28,12 @@ __device__ __forceinline__ uint16_t f2bf_bits(float f) {
   return *reinterpret_cast<uint16_t*>(&b);
 }
 
+typedef float float2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+
+// two fp32 -> packed bf16x2 (RNE) in ONE v_cvt_pk_bf16_f32 (the scalar form costs 4 VALU ops)
 __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
-  return (uint32_t)f2bf_bits(lo) | ((uint32_t)f2bf_bits(hi) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){lo, hi}, bf16x2_t));
 }
 
 __device__ __forceinline__ float wave_sum(float v) {
@@ -127,5 +131,25 @@ __device__ __forceinline__ uint32_t hash_u32(uint64_t x) {
 __device__ __forceinline__ float uniform01(uint64_t seed, uint64_t counter) {
   return (hash_u32(seed * 0x9E3779B97F4A7C15ULL + counter) >> 8) * (1.0f / 16777216.0f);
 }
+
+
+// ---- LDS-DMA (global_load_lds_dwordx4) ----------------------------------------------------
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void gbl_void_t;
+static __device__ uint4 g_zero16[1];  // zero-initialised: source of out-of-range LDS-DMA lanes
+
+// one global_load_lds_dwordx4: 64 lanes x 16 B from per-lane `g` to LDS [lds_addr, +1 KiB)
+// (lane-linear destination, wave-uniform base). Issued as inline asm so hipcc's waitcnt pass
+// does not serialise it against ds_reads of other LDS buffers; completion is counted by hand
+// (s_waitcnt vmcnt before the barrier that publishes the buffer).
+__device__ __forceinline__ void glds16(const void* g, unsigned lds_addr) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(g), "s"(lds_addr)
+               : "memory");
+}
+
+__device__ __forceinline__ unsigned lds_addr_of(const void* p) { return (unsigned)(size_t)(lds_void_t*)p; }
 
 }  // namespace penroz

@@ -36,6 +36,7 @@
 // the identical mask; the softmax normaliser uses the undropped probabilities (SDPA
 // semantics).
 #include "common.h"
+#include <type_traits>
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 
@@ -122,6 +123,26 @@ __device__ __forceinline__ void store4(bf16* p, float a, float b, float c, float
   *reinterpret_cast<uint2*>(p) = uint2{pack_bf16x2(a, b), pack_bf16x2(c, d)};
 }
 
+// XCD-aware block mapping. Workgroups are dealt to the 8 XCDs round-robin in dispatch order
+// (x fastest), so the plain grid would scatter one head's blocks over all eight L2s. Remap so
+// the gridDim.x blocks of a head share an XCD (its L2 then serves the head's K/V or Q/dO
+// re-reads) with heads dealt to XCDs round-robin; block index order (heaviest first) is kept
+// per XCD. Bijective; a tail of heads that is not a multiple of 8 keeps the plain order.
+__device__ __forceinline__ void xcd_head_block(int& blk, int& head) {
+  const int nblk = gridDim.x, nheads = gridDim.y;
+  const int id = blockIdx.x + nblk * blockIdx.y;
+  const int full = (nheads >> 3) * nblk;  // slots per XCD in the full head groups
+  const int xcd = id & 7, slot = id >> 3;
+  if (slot < full) {
+    head = (slot / nblk) * 8 + xcd;
+    blk = slot - (slot / nblk) * nblk;
+  } else {
+    const int r = id - 8 * full;
+    head = (nheads & ~7) + r / nblk;
+    blk = r - (r / nblk) * nblk;
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // forward
 template <bool DROPOUT>
@@ -131,8 +152,10 @@ __global__ void __launch_bounds__(256, 2) fa_fwd_kernel(const bf16* __restrict__
   constexpr int BM = 128, BN = 64;
   __shared__ __attribute__((aligned(16))) char smem[2][2][BN * 128];
   const int nqb = (T + BM - 1) / BM;
-  const int qb = nqb - 1 - blockIdx.x;
-  const int b = blockIdx.y / H, h = blockIdx.y % H, hk = h / (H / Hkv);
+  int qi, bh;
+  xcd_head_block(qi, bh);
+  const int qb = nqb - 1 - qi;
+  const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
   const int lane = threadIdx.x & 63, w = wave_id(), hh = lane >> 5;
   const size_t RS = (size_t)(H + 2 * Hkv) * kD;
   const bf16* qbase = qkv + (size_t)b * T * RS + (size_t)h * kD;
@@ -194,44 +217,56 @@ __global__ void __launch_bounds__(256, 2) fa_fwd_kernel(const bf16* __restrict__
 #pragma unroll
         for (int st = 0; st < 4; ++st) s[kh] = mfma32(row_frag(Kt, 32 * kh, st, lane), qf[st], s[kh]);
       }
+      // softmax on raw scores: max first (scaling commutes with max, c > 0), then
+      // p = 2^(s·c − m) as one fma + exp. The mask variant is a separate code path so the
+      // common (off-diagonal) tile has no per-element select or branch.
+      auto softmax = [&](auto mask_tag) {
+        constexpr bool MASK = decltype(mask_tag)::value;
+        float tmax = -INFINITY;
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            if constexpr (MASK) {
+              const int key = kt0 + 32 * kh + acc_row(i, lane);
+              s[kh][i] = (key > qrow || key >= T) ? -INFINITY : s[kh][i];
+            }
+            tmax = fmaxf(tmax, s[kh][i]);
+          }
+        tmax = halves_max(tmax) * c;
+        if (!__all(tmax <= m + kRescaleThr)) {  // wave-uniform: rare after the first tiles
+          const float mnew = fmaxf(m, tmax);
+          const float alpha = fexp2(m - mnew);
+          m = mnew;
+          l *= alpha;
+#pragma unroll
+          for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) o[dh][i] *= alpha;
+        }
+        const float negm = -m;
+        float2_t lsum = {0.f, 0.f};
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+          for (int i = 0; i < 16; i += 2) {
+            float2_t p = {fexp2(fmaf(s[kh][i], c, negm)), fexp2(fmaf(s[kh][i + 1], c, negm))};
+            lsum += p;
+            if constexpr (DROPOUT) {
+              const int key = kt0 + 32 * kh + acc_row(i, lane);
+              p[0] = dropout_keep(seed, b, h, H, T, qrow, key, p_drop) ? p[0] * inv_keep : 0.f;
+              p[1] = dropout_keep(seed, b, h, H, T, qrow, key + 1, p_drop) ? p[1] * inv_keep : 0.f;
+            }
+            s[kh][i] = p[0];
+            s[kh][i + 1] = p[1];
+          }
+        l += lsum[0] + lsum[1];
+      };
       const bool need_mask = (kt0 + BN - 1 > q0) || (kt0 + BN > T);
-      float tmax = -INFINITY;
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          float v = s[kh][i] * c;
-          if (need_mask) {
-            const int key = kt0 + 32 * kh + acc_row(i, lane);
-            v = (key > qrow || key >= T) ? -INFINITY : v;
-          }
-          s[kh][i] = v;
-          tmax = fmaxf(tmax, v);
-        }
-      tmax = halves_max(tmax);
-      if (!__all(tmax <= m + kRescaleThr)) {  // wave-uniform: rare after the first tiles
-        const float mnew = fmaxf(m, tmax);
-        const float alpha = fexp2(m - mnew);
-        m = mnew;
-        l *= alpha;
-#pragma unroll
-        for (int dh = 0; dh < 2; ++dh)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) o[dh][i] *= alpha;
-      }
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float p = fexp2(s[kh][i] - m);
-          l += p;
-          if constexpr (DROPOUT) {
-            const int key = kt0 + 32 * kh + acc_row(i, lane);
-            s[kh][i] = dropout_keep(seed, b, h, H, T, qrow, key, p_drop) ? p * inv_keep : 0.f;
-          } else {
-            s[kh][i] = p;
-          }
-        }
+      if (need_mask)
+        softmax(std::true_type{});
+      else
+        softmax(std::false_type{});
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
@@ -255,6 +290,381 @@ __global__ void __launch_bounds__(256, 2) fa_fwd_kernel(const bf16* __restrict__
         store4(orow + 32 * dh + 8 * g + 4 * hh, o[dh][4 * g] * inv, o[dh][4 * g + 1] * inv, o[dh][4 * g + 2] * inv,
                o[dh][4 * g + 3] * inv);
     if (hh == 0) lse[((size_t)b * H + h) * T + qrow] = (m + log2f(l)) * kLn2;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// forward, software-pipelined across key tiles (default): S_{j+1} = K_{j+1}·Qᵀ is issued
+// before tile j's softmax so the matrix cores run it while the SIMD does tile j's VALU work
+// (an MFMA blocks vector issue for only 8 of its 32 cycles); V_j's transposed fragments are
+// read before the softmax so their LDS latency hides behind it too. K/V live in a 3-stage LDS
+// ring (K_{j+1} and V_j are read while tile j+2 is staged), one barrier per tile.
+template <bool DROPOUT>
+__global__ void __launch_bounds__(256, 2) fa_fwd2_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+                                                      float* __restrict__ lse, int T, int H, int Hkv, float scale,
+                                                      float p_drop, uint64_t seed) {
+  constexpr int BM = 128, BN = 64, NST = 3;
+  __shared__ __attribute__((aligned(16))) char smem[NST][2][BN * 128];
+  const int nqb = (T + BM - 1) / BM;
+  int qi, bh;
+  xcd_head_block(qi, bh);
+  const int qb = nqb - 1 - qi;
+  const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
+  const int lane = threadIdx.x & 63, w = wave_id(), hh = lane >> 5;
+  const size_t RS = (size_t)(H + 2 * Hkv) * kD;
+  const bf16* qbase = qkv + (size_t)b * T * RS + (size_t)h * kD;
+  const bf16* kbase = qkv + (size_t)b * T * RS + (size_t)(H + hk) * kD;
+  const bf16* vbase = qkv + (size_t)b * T * RS + (size_t)(H + Hkv + hk) * kD;
+  const int q0 = qb * BM + 32 * w;
+  const int qrow = q0 + (lane & 31);
+  const float c = scale * kLog2e;
+  const float inv_keep = DROPOUT ? 1.f / (1.f - p_drop) : 1.f;
+
+  uint4 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+    qf[s] = qrow < T ? *reinterpret_cast<const uint4*>(qbase + (size_t)qrow * RS + 16 * s + 8 * hh) : zero4();
+
+  const int sr = threadIdx.x >> 3, sc = threadIdx.x & 7;
+  uint4 kst[2], vst[2];
+  auto gload = [&](int kt0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int key = kt0 + sr + 32 * i;
+      kst[i] = key < T ? *reinterpret_cast<const uint4*>(kbase + (size_t)key * RS + 8 * sc) : zero4();
+      vst[i] = key < T ? *reinterpret_cast<const uint4*>(vbase + (size_t)key * RS + 8 * sc) : zero4();
+    }
+  };
+  auto lstore = [&](int stg) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      *reinterpret_cast<uint4*>(smem[stg][0] + tile_off(sr + 32 * i, sc)) = kst[i];
+      *reinterpret_cast<uint4*>(smem[stg][1] + tile_off(sr + 32 * i, sc)) = vst[i];
+    }
+  };
+  auto scores = [&](int stg, f32x16 (&sa)[2]) {
+    const char* Kt = smem[stg][0];
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sa[kh][i] = 0.f;
+#pragma unroll
+      for (int st = 0; st < 4; ++st) sa[kh] = mfma32(row_frag(Kt, 32 * kh, st, lane), qf[st], sa[kh]);
+    }
+  };
+
+  const int kend = min(T, qb * BM + BM);
+  const int ntiles = (kend + BN - 1) / BN;
+  const int jlast = min(ntiles - 1, (q0 + 31) / BN);  // this wave's last tile with a visible key
+  f32x16 o[2];
+#pragma unroll
+  for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[dh][i] = 0.f;
+  float m = -1e30f, l = 0.f;
+
+  // one pipelined step: S of tile j+1 into `sn`, softmax + P·V of tile j from `sc`
+  auto step = [&](int j, f32x16 (&scur)[2], f32x16 (&snext)[2]) {
+    const int kt0 = j * BN;
+    if (j + 2 < ntiles) gload(kt0 + 2 * BN);
+    if (j + 1 <= jlast) scores((j + 1) % NST, snext);
+    __builtin_amdgcn_sched_barrier(0);
+    if (j <= jlast) {
+      const char* Vt = smem[j % NST][1];
+      uint4 vfr[2][2][2];
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+          for (int dh = 0; dh < 2; ++dh) vfr[kh][ss][dh] = tr_frag(Vt, 32 * kh + 16 * ss, 32 * dh, lane);
+      auto softmax = [&](auto mask_tag) {
+        constexpr bool MASK = decltype(mask_tag)::value;
+        float tmax = -INFINITY;
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            if constexpr (MASK) {
+              const int key = kt0 + 32 * kh + acc_row(i, lane);
+              scur[kh][i] = (key > qrow || key >= T) ? -INFINITY : scur[kh][i];
+            }
+            tmax = fmaxf(tmax, scur[kh][i]);
+          }
+        tmax = halves_max(tmax) * c;
+        if (!__all(tmax <= m + kRescaleThr)) {
+          const float mnew = fmaxf(m, tmax);
+          const float alpha = fexp2(m - mnew);
+          m = mnew;
+          l *= alpha;
+#pragma unroll
+          for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) o[dh][i] *= alpha;
+        }
+        const float negm = -m;
+        float2_t lsum = {0.f, 0.f};
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+          for (int i = 0; i < 16; i += 2) {
+            float2_t p = {fexp2(fmaf(scur[kh][i], c, negm)), fexp2(fmaf(scur[kh][i + 1], c, negm))};
+            lsum += p;
+            if constexpr (DROPOUT) {
+              const int key = kt0 + 32 * kh + acc_row(i, lane);
+              p[0] = dropout_keep(seed, b, h, H, T, qrow, key, p_drop) ? p[0] * inv_keep : 0.f;
+              p[1] = dropout_keep(seed, b, h, H, T, qrow, key + 1, p_drop) ? p[1] * inv_keep : 0.f;
+            }
+            scur[kh][i] = p[0];
+            scur[kh][i + 1] = p[1];
+          }
+        l += lsum[0] + lsum[1];
+      };
+      if ((kt0 + BN - 1 > q0) || (kt0 + BN > T))
+        softmax(std::true_type{});
+      else
+        softmax(std::false_type{});
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          const uint4 pf = acc_frag(scur[kh], ss);
+#pragma unroll
+          for (int dh = 0; dh < 2; ++dh) o[dh] = mfma32(vfr[kh][ss][dh], pf, o[dh]);
+        }
+    }
+    if (j + 2 < ntiles) lstore((j + 2) % NST);
+    __syncthreads();
+  };
+
+  gload(0);
+  lstore(0);
+  if (ntiles > 1) {
+    gload(BN);
+    lstore(1);
+  }
+  __syncthreads();
+  f32x16 sA[2], sB[2];
+  scores(0, sA);
+  int j = 0;
+  for (; j + 1 < ntiles; j += 2) {
+    step(j, sA, sB);
+    step(j + 1, sB, sA);
+  }
+  if (j < ntiles) step(j, sA, sB);
+
+  l = halves_sum(l);
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  if (qrow < T) {
+    bf16* orow = out + ((size_t)b * T + qrow) * H * kD + (size_t)h * kD;
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        store4(orow + 32 * dh + 8 * g + 4 * hh, o[dh][4 * g] * inv, o[dh][4 * g + 1] * inv, o[dh][4 * g + 2] * inv,
+               o[dh][4 * g + 3] * inv);
+    if (hh == 0) lse[((size_t)b * H + h) * T + qrow] = (m + log2f(l)) * kLn2;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// forward, two query blocks per wave (default): a 128-thread workgroup = 2 waves × 64 query
+// rows; each wave holds two independent 32-row blocks A and B. Per 64-key tile the K
+// fragments (row reads) and V fragments (transposed reads) are read from LDS ONCE per wave
+// and used by both blocks, halving LDS traffic per MFMA, and the two blocks' dependency
+// chains interleave: S_B's MFMAs run under softmax_A, P_A·V's under softmax_B. Query blocks
+// of 64 rows are aligned to key tiles, so a wave's only masked tile is its diagonal one.
+template <bool DROPOUT>
+__global__ void __launch_bounds__(128, 2) fa_fwd3_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+                                                      float* __restrict__ lse, int T, int H, int Hkv, float scale,
+                                                      float p_drop, uint64_t seed) {
+  constexpr int BM = 128, BN = 64;
+  __shared__ __attribute__((aligned(16))) char smem[2][2][BN * 128];
+  const int nqb = (T + BM - 1) / BM;
+  int qi, bh;
+  xcd_head_block(qi, bh);
+  const int qb = nqb - 1 - qi;
+  const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
+  const int lane = threadIdx.x & 63, w = wave_id(), hh = lane >> 5;
+  const size_t RS = (size_t)(H + 2 * Hkv) * kD;
+  const bf16* qbase = qkv + (size_t)b * T * RS + (size_t)h * kD;
+  const bf16* kbase = qkv + (size_t)b * T * RS + (size_t)(H + hk) * kD;
+  const bf16* vbase = qkv + (size_t)b * T * RS + (size_t)(H + Hkv + hk) * kD;
+  const int q0 = qb * BM + 64 * w;  // block A rows q0..q0+31, block B rows q0+32..q0+63
+  const float c = scale * kLog2e;
+  const float inv_keep = DROPOUT ? 1.f / (1.f - p_drop) : 1.f;
+  int qrow[2];
+  qrow[0] = q0 + (lane & 31);
+  qrow[1] = q0 + 32 + (lane & 31);
+
+  uint4 qf[2][4];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      qf[a][s] = qrow[a] < T ? *reinterpret_cast<const uint4*>(qbase + (size_t)qrow[a] * RS + 16 * s + 8 * hh) : zero4();
+
+  // LDS-DMA staging (no staging registers). K image is chunk-major [8 chunks][64 keys][16 B]:
+  // row-fragment reads (16 lanes on 16 consecutive keys, one chunk) are conflict-free and all
+  // fragment addresses differ by immediates; one DMA piece = one chunk column, so wave 0's
+  // eight pieces share ONE per-lane source pointer. V keeps the swizzled row-major image
+  // (tile_off) for the transposed reads; wave 1 fills it, piece p = keys 8p..8p+7. Keys past
+  // T are clamped to T-1: finite data that the mask (K) or P = 0 (V) cancels.
+  auto dma = [&](int kt0, int buf) {
+    const unsigned dst = __builtin_amdgcn_readfirstlane(lds_addr_of(smem[buf][w]));
+    if (w == 0) {
+      const bf16* g = kbase + (size_t)min(kt0 + lane, T - 1) * RS;
+#pragma unroll
+      for (int p = 0; p < 8; ++p) glds16(g + 8 * p, dst + p * 1024);
+    } else {
+      const int prow = lane >> 3, pch = lane & 7;
+#pragma unroll
+      for (int p = 0; p < 8; ++p) {
+        const int row = 8 * p + prow;
+        const int ch = pch ^ ((((row >> 1) & 1) << 2) | ((row >> 2) & 3));
+        glds16(vbase + (size_t)min(kt0 + row, T - 1) * RS + 8 * ch, dst + p * 1024);
+      }
+    }
+  };
+
+  const int kend = min(T, qb * BM + BM);
+  const int ntiles = (kend + BN - 1) / BN;
+  const int jlast = min(ntiles - 1, q0 / BN);  // the wave's diagonal tile
+  f32x16 o[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) o[a][dh][i] = 0.f;
+  float m[2] = {-1e30f, -1e30f}, l[2] = {0.f, 0.f};
+
+  auto softmax = [&](auto mask_tag, int a, int kt0, f32x16 (&sa)[2]) {
+    constexpr bool MASK = decltype(mask_tag)::value;
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        if constexpr (MASK) {
+          const int key = kt0 + 32 * kh + acc_row(i, lane);
+          sa[kh][i] = (key > qrow[a] || key >= T) ? -INFINITY : sa[kh][i];
+        }
+        tmax = fmaxf(tmax, sa[kh][i]);
+      }
+    tmax = halves_max(tmax) * c;
+    if (!__all(tmax <= m[a] + kRescaleThr)) {
+      const float mnew = fmaxf(m[a], tmax);
+      const float alpha = fexp2(m[a] - mnew);
+      m[a] = mnew;
+      l[a] *= alpha;
+#pragma unroll
+      for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[a][dh][i] *= alpha;
+    }
+    const float negm = -m[a];
+    float2_t lsum = {0.f, 0.f};
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int i = 0; i < 16; i += 2) {
+        float2_t p = {fexp2(fmaf(sa[kh][i], c, negm)), fexp2(fmaf(sa[kh][i + 1], c, negm))};
+        lsum += p;
+        if constexpr (DROPOUT) {
+          const int key = kt0 + 32 * kh + acc_row(i, lane);
+          p[0] = dropout_keep(seed, b, h, H, T, qrow[a], key, p_drop) ? p[0] * inv_keep : 0.f;
+          p[1] = dropout_keep(seed, b, h, H, T, qrow[a], key + 1, p_drop) ? p[1] * inv_keep : 0.f;
+        }
+        sa[kh][i] = p[0];
+        sa[kh][i + 1] = p[1];
+      }
+    l[a] += lsum[0] + lsum[1];
+  };
+
+  // one tile for both blocks; MASK only on the diagonal tile
+  auto tile = [&](auto mask_tag, int j) {
+    const int kt0 = j * BN;
+    const char* Kt = smem[j & 1][0];
+    const char* Vt = smem[j & 1][1];
+    f32x16 sA[2], sB[2];
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {  // K fragments of one 32-key half at a time (16 VGPRs)
+      uint4 kfr[4];
+#pragma unroll
+      for (int st = 0; st < 4; ++st)  // element j = K[32kh + (lane&31)][16st + 8hh + j]
+        kfr[st] = *reinterpret_cast<const uint4*>(Kt + (2 * st + hh) * 1024 + (32 * kh + (lane & 31)) * 16);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sA[kh][i] = sB[kh][i] = 0.f;
+#pragma unroll
+      for (int st = 0; st < 4; ++st) sA[kh] = mfma32(kfr[st], qf[0][st], sA[kh]);
+#pragma unroll
+      for (int st = 0; st < 4; ++st) sB[kh] = mfma32(kfr[st], qf[1][st], sB[kh]);
+    }
+    uint4 vfr[2][2][2];
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+        for (int dh = 0; dh < 2; ++dh) vfr[kh][ss][dh] = tr_frag(Vt, 32 * kh + 16 * ss, 32 * dh, lane);
+    softmax(mask_tag, 0, kt0, sA);
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const uint4 pf = acc_frag(sA[kh], ss);
+#pragma unroll
+        for (int dh = 0; dh < 2; ++dh) o[0][dh] = mfma32(vfr[kh][ss][dh], pf, o[0][dh]);
+      }
+    softmax(mask_tag, 1, kt0, sB);
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const uint4 pf = acc_frag(sB[kh], ss);
+#pragma unroll
+        for (int dh = 0; dh < 2; ++dh) o[1][dh] = mfma32(vfr[kh][ss][dh], pf, o[1][dh]);
+      }
+  };
+
+  dma(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // unmasked tiles, then the peeled diagonal tile (kept out of the loop so its mask
+  // predicates are not hoisted as loop invariants), then barrier-only steps while the other
+  // wave finishes; every wave passes the same ntiles barriers and issues its DMA share
+  int j = 0;
+  for (; j < jlast; ++j) {
+    dma((j + 1) * BN, (j + 1) & 1);  // j < jlast <= ntiles-1: buffer freed by the last barrier
+    tile(std::false_type{}, j);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (j + 1 < ntiles) dma((j + 1) * BN, (j + 1) & 1);
+  tile(std::true_type{}, j);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (++j; j < ntiles; ++j) {
+    if (j + 1 < ntiles) dma((j + 1) * BN, (j + 1) & 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    const float ls = halves_sum(l[a]);
+    const float inv = ls > 0.f ? 1.f / ls : 0.f;
+    if (qrow[a] < T) {
+      bf16* orow = out + ((size_t)b * T + qrow[a]) * H * kD + (size_t)h * kD;
+#pragma unroll
+      for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          store4(orow + 32 * dh + 8 * g + 4 * hh, o[a][dh][4 * g] * inv, o[a][dh][4 * g + 1] * inv,
+                 o[a][dh][4 * g + 2] * inv, o[a][dh][4 * g + 3] * inv);
+      if (hh == 0) lse[((size_t)b * H + h) * T + qrow[a]] = (m[a] + log2f(ls)) * kLn2;
+    }
   }
 }
 
@@ -298,8 +708,9 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv_kernel(const bf16* __restr
   __shared__ __attribute__((aligned(16))) char dot[2][QS * 128];
   __shared__ __attribute__((aligned(16))) float lse2s[2][QS];
   __shared__ __attribute__((aligned(16))) float dels[2][QS];
-  const int kb = blockIdx.x;
-  const int b = blockIdx.y / Hkv, hk = blockIdx.y % Hkv;
+  int kb, bh;
+  xcd_head_block(kb, bh);
+  const int b = bh / Hkv, hk = bh % Hkv;
   const int G = H / Hkv;
   const int lane = threadIdx.x & 63, w = wave_id(), hh = lane >> 5;
   const size_t RS = (size_t)(H + 2 * Hkv) * kD;
@@ -382,28 +793,35 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv_kernel(const bf16* __restr
           dp = mfma32(row_frag(Dt, 0, s, lane), vf[s], dp);
         }
         const bool need_mask = (kw0 + 31 > qh0) || (qh0 + 32 > T) || (kw0 + 32 > T);
+        auto grads = [&](auto mask_tag) {  // P and dS in place; mask path only on diagonal tiles
+          constexpr bool MASK = decltype(mask_tag)::value;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int r0 = 8 * g + 4 * hh;
-          const float4_t l2 = *reinterpret_cast<const float4_t*>(&lse2s[buf][32 * half + r0]);
-          const float4_t dl = *reinterpret_cast<const float4_t*>(&dels[buf][32 * half + r0]);
+          for (int g = 0; g < 4; ++g) {
+            const int r0 = 8 * g + 4 * hh;
+            const float4_t l2 = *reinterpret_cast<const float4_t*>(&lse2s[buf][32 * half + r0]);
+            const float4_t dl = *reinterpret_cast<const float4_t*>(&dels[buf][32 * half + r0]);
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int i = 4 * g + k;
-            const int q = qh0 + r0 + k;
-            float p = fexp2(sp[i] * c - l2[k]);
-            if (need_mask) p = (key > q || q >= T || key >= T) ? 0.f : p;
-            float dpi = dp[i];
-            float pdrop = p;
-            if constexpr (DROPOUT) {
-              const bool keep = dropout_keep(seed, b, hq, H, T, q, key, p_drop);
-              pdrop = keep ? p * inv_keep : 0.f;
-              dpi = keep ? dpi * inv_keep : 0.f;
+            for (int k = 0; k < 4; ++k) {
+              const int i = 4 * g + k;
+              const int q = qh0 + r0 + k;
+              float p = fexp2(fmaf(sp[i], c, -l2[k]));
+              if constexpr (MASK) p = (key > q || q >= T || key >= T) ? 0.f : p;
+              float dpi = dp[i];
+              float pdrop = p;
+              if constexpr (DROPOUT) {
+                const bool keep = dropout_keep(seed, b, hq, H, T, q, key, p_drop);
+                pdrop = keep ? p * inv_keep : 0.f;
+                dpi = keep ? dpi * inv_keep : 0.f;
+              }
+              sp[i] = pdrop;
+              dp[i] = p * (dpi - dl[k]);
             }
-            sp[i] = pdrop;
-            dp[i] = p * (dpi - dl[k]);
           }
-        }
+        };
+        if (need_mask)
+          grads(std::true_type{});
+        else
+          grads(std::false_type{});
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss) {
           const uint4 pf = acc_frag(sp, ss), sf = acc_frag(dp, ss);
@@ -444,8 +862,10 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dq_kernel(const bf16* __restric
   constexpr int BM = 128, BN = 64;
   __shared__ __attribute__((aligned(16))) char smem[2][2][BN * 128];
   const int nqb = (T + BM - 1) / BM;
-  const int qb = nqb - 1 - blockIdx.x;
-  const int b = blockIdx.y / H, h = blockIdx.y % H, hk = h / (H / Hkv);
+  int qi, bh;
+  xcd_head_block(qi, bh);
+  const int qb = nqb - 1 - qi;
+  const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
   const int lane = threadIdx.x & 63, w = wave_id(), hh = lane >> 5;
   const size_t RS = (size_t)(H + 2 * Hkv) * kD;
   const size_t ORS = (size_t)H * kD;
@@ -518,20 +938,27 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dq_kernel(const bf16* __restric
           dp[kh] = mfma32(row_frag(Vt, 32 * kh, st, lane), dof[st], dp[kh]);
         }
       }
+      auto grads = [&](auto mask_tag) {  // dS in place; mask path only on diagonal / ragged tiles
+        constexpr bool MASK = decltype(mask_tag)::value;
 #pragma unroll
-      for (int kh = 0; kh < 2; ++kh)
+        for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int k = kt0 + 32 * kh + acc_row(i, lane);
-          float p = fexp2(s[kh][i] * c - l2);
-          p = (k > qrow || k >= T || !qok) ? 0.f : p;
-          float dpi = dp[kh][i];
-          if constexpr (DROPOUT) {
-            const bool keep = dropout_keep(seed, b, h, H, T, qrow, k, p_drop);
-            dpi = keep ? dpi * inv_keep : 0.f;
+          for (int i = 0; i < 16; ++i) {
+            const int k = kt0 + 32 * kh + acc_row(i, lane);
+            float p = fexp2(fmaf(s[kh][i], c, -l2));
+            if constexpr (MASK) p = (k > qrow || k >= T || !qok) ? 0.f : p;
+            float dpi = dp[kh][i];
+            if constexpr (DROPOUT) {
+              const bool keep = dropout_keep(seed, b, h, H, T, qrow, k, p_drop);
+              dpi = keep ? dpi * inv_keep : 0.f;
+            }
+            s[kh][i] = p * (dpi - dl);
           }
-          s[kh][i] = p * (dpi - dl);
-        }
+      };
+      if ((kt0 + BN - 1 > q0) || (kt0 + BN > T) || (q0 + 32 > T))
+        grads(std::true_type{});
+      else
+        grads(std::false_type{});
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
@@ -567,6 +994,8 @@ static void check_qkv(const torch::Tensor& qkv, int64_t H, int64_t Hkv, int64_t 
   TORCH_CHECK(H % Hkv == 0 && qkv.size(2) == (H + 2 * Hkv) * D, "qkv width must be (H + 2*Hkv)*D");
 }
 
+static int g_fa_fwd_variant = 3;
+
 void flash_attn_fwd(torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int64_t H, int64_t Hkv, int64_t D,
                     double scale, double p_drop, int64_t seed) {
   check_qkv(qkv, H, Hkv, D);
@@ -578,12 +1007,28 @@ void flash_attn_fwd(torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int
   auto stream = at::hip::getCurrentHIPStream();
   const bf16* q = reinterpret_cast<const bf16*>(qkv.data_ptr());
   bf16* o = reinterpret_cast<bf16*>(out.data_ptr());
+  // dropout always takes the single-stage kernel (the pipelined one would spill with the
+  // mask hashing live across the tile loop)
   if (p_drop > 0.0)
     hipLaunchKernelGGL(fa_fwd_kernel<true>, grid, dim3(256), 0, stream, q, o, lse.data_ptr<float>(), T, (int)H,
                        (int)Hkv, (float)scale, (float)p_drop, (uint64_t)seed);
-  else
+  else if (g_fa_fwd_variant == 1)
     hipLaunchKernelGGL(fa_fwd_kernel<false>, grid, dim3(256), 0, stream, q, o, lse.data_ptr<float>(), T, (int)H,
                        (int)Hkv, (float)scale, 0.f, (uint64_t)seed);
+  else if (g_fa_fwd_variant == 2)
+    hipLaunchKernelGGL(fa_fwd2_kernel<false>, grid, dim3(256), 0, stream, q, o, lse.data_ptr<float>(), T, (int)H,
+                       (int)Hkv, (float)scale, 0.f, (uint64_t)seed);
+  else
+    hipLaunchKernelGGL(fa_fwd3_kernel<false>, grid, dim3(128), 0, stream, q, o, lse.data_ptr<float>(), T, (int)H,
+                       (int)Hkv, (float)scale, 0.f, (uint64_t)seed);
+}
+
+// 1 = single-stage forward (fa_fwd_kernel), 2 = tile-pipelined forward (fa_fwd2_kernel),
+// 3 = two query blocks per wave (fa_fwd3_kernel, default)
+int64_t flash_fwd_variant(int64_t v) {
+  const int64_t prev = g_fa_fwd_variant;
+  if (v > 0) g_fa_fwd_variant = (int)v;
+  return prev;
 }
 
 void flash_attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, torch::Tensor dqkv,

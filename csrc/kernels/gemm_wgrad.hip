@@ -171,21 +171,6 @@ __device__ __forceinline__ uint4 tr_frag512(const char* tile, int rbase, int cba
   return uint4{a.x, a.y, b.x, b.y};
 }
 
-typedef __attribute__((address_space(3))) void lds_void_t;
-typedef __attribute__((address_space(1))) void gbl_void_t;
-__device__ uint4 g_zero16[1];  // zero-initialised: source of out-of-range LDS-DMA lanes
-
-// one global_load_lds_dwordx4: 64 lanes x 16 B from per-lane `g` to LDS [lds_addr, +1 KiB).
-// Issued as inline asm so hipcc's waitcnt pass does not serialise it against ds_reads of the
-// other LDS buffer; completion is counted by hand (s_waitcnt vmcnt before the barrier).
-__device__ __forceinline__ void glds16(const void* g, unsigned lds_addr) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(g), "s"(lds_addr)
-               : "memory");
-}
-
 // GLDS: stage tiles with global_load_lds_dwordx4 (LDS-DMA, no VGPR round trip, no ds_write
 // transfer cost). The DMA destination is lane-linear (1 KiB per wave-instruction = two 512-B
 // k-rows), so the XOR swizzle is applied on the per-lane SOURCE address instead.

@@ -14,7 +14,8 @@ import sys
 import torch
 
 _REPO_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-_BUILD_DIR = os.path.join(_REPO_ROOT, "build_ext")
+# PENROZ_EXT_DIR: load the extension from another in-tree build (same-box A/B benchmarking)
+_BUILD_DIR = os.environ.get("PENROZ_EXT_DIR") or os.path.join(_REPO_ROOT, "build_ext")
 
 _mod = None
 _err: Exception | None = None

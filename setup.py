@@ -20,7 +20,7 @@ import sysconfig
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(ROOT, "csrc")
-OUT = os.path.join(ROOT, "build_ext")
+OUT = os.environ.get("PENROZ_BUILD_DIR") or os.path.join(ROOT, "build_ext")  # override: A/B builds
 OBJ = os.path.join(OUT, "obj")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")

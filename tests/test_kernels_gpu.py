@@ -173,11 +173,18 @@ def _qkv(B, T, H, Hkv, D=64, scale=1.0):
     return (torch.randn(B, T, (H + 2 * Hkv) * D, device=DEV) * scale).to(torch.bfloat16)
 
 
-@pytest.mark.parametrize("B,T,H,Hkv", [(2, 1024, 4, 4), (1, 200, 3, 3), (2, 130, 4, 2), (1, 64, 2, 1), (1, 5, 2, 2)])
-def test_flash_fwd(B, T, H, Hkv):
+@pytest.mark.parametrize("variant", [1, 2, 3])
+@pytest.mark.parametrize("B,T,H,Hkv", [(2, 1024, 4, 4), (1, 200, 3, 3), (2, 130, 4, 2), (1, 64, 2, 1), (1, 5, 2, 2),
+                                       (1, 192, 2, 2), (1, 320, 2, 2)])
+def test_flash_fwd(B, T, H, Hkv, variant):
     torch.manual_seed(0)
     qkv = _qkv(B, T, H, Hkv, scale=1.5)
-    out, lse = A.flash_fwd(qkv, H, Hkv, 64)
+    k = _ext.kernels()
+    prev = k.flash_fwd_variant(variant)
+    try:
+        out, lse = A.flash_fwd(qkv, H, Hkv, 64)
+    finally:
+        k.flash_fwd_variant(prev)
     ro, rl = A.reference_attention_lse(qkv, H, Hkv, 64)
     _close(out, ro, 0.02, 0.01, "out")
     _close(lse, rl, 2e-3, 1e-4, "lse")
