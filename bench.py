@@ -73,6 +73,9 @@ def main():
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--engine", default="fused", choices=["fused", "generic", "reference"])
     ap.add_argument("--model", default="gpt2-124m", choices=list(MODELS))
+    ap.add_argument("--profile", default=None, metavar="DIR",
+                    help="after the timed steps, profile 3 more under torch.profiler into DIR "
+                         "(Chrome trace + per-kernel table); set PENROZ_ROCTX=1 for roctx phase ranges")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -142,6 +145,12 @@ def main():
             "config": {"model": args.model, "global_batch": world * B, "seq_len": T, "micro_batch_per_gpu": B,
                        "tokens_per_step": world * B * T, "parallelism": f"dp{world}"},
         }), flush=True)
+    if args.profile:  # outside the timed region
+        from penroz.utils.profiling import profile_steps
+        out = os.path.join(args.profile, f"rank{rank}")
+        table = profile_steps(lambda: step(0), 3, out)
+        if rank == 0:
+            print(table, file=sys.stderr)
     if world > 1:
         dist.destroy_process_group()
 

@@ -152,4 +152,22 @@ __device__ __forceinline__ void glds16(const void* g, unsigned lds_addr) {
 
 __device__ __forceinline__ unsigned lds_addr_of(const void* p) { return (unsigned)(size_t)(lds_void_t*)p; }
 
+
+// ---- debug build (PENROZ_DEBUG=1 python setup.py build_ext -> build_ext/debug) --------------
+// Device-side checks of data-dependent indices (token ids, targets, cache positions). Release
+// builds compile them out (and clamp / skip instead); debug builds print the failing
+// condition with its location and trap, which surfaces as a HIP error on the next sync.
+#ifdef PENROZ_DEBUG
+#define PZ_DEVICE_CHECK(cond)                                                                  \
+  do {                                                                                         \
+    if (!(cond)) {                                                                             \
+      printf("penroz device check failed: %s at %s:%d (block %d, thread %d)\n", #cond, __FILE__, \
+             __LINE__, (int)blockIdx.x, (int)threadIdx.x);                                     \
+      __builtin_trap();                                                                        \
+    }                                                                                          \
+  } while (0)
+#else
+#define PZ_DEVICE_CHECK(cond) ((void)0)
+#endif
+
 }  // namespace penroz

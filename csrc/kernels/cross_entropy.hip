@@ -36,6 +36,7 @@ __global__ void __launch_bounds__(kCEThreads) ce_kernel(T* __restrict__ logits, 
   const int row = blockIdx.x;
   T* rp = logits + (size_t)row * V;
   const int64_t tgt = targets[row];
+  PZ_DEVICE_CHECK(tgt == ignore_index || (tgt >= 0 && tgt < V));
   const int t = threadIdx.x;
   float v[CPT][8];
   float m = -INFINITY;
@@ -87,6 +88,7 @@ __global__ void __launch_bounds__(kCEThreads) ce_loop_kernel(T* __restrict__ log
   const int row = blockIdx.x;
   T* rp = logits + (size_t)row * V;
   const int64_t tgt = targets[row];
+  PZ_DEVICE_CHECK(tgt == ignore_index || (tgt >= 0 && tgt < V));
   float m = -INFINITY;
   for (int c = 8 * threadIdx.x; c < V; c += 8 * kCEThreads) {
     float v[8];

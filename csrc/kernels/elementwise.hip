@@ -155,6 +155,7 @@ __global__ void __launch_bounds__(256) embed_fwd_kernel(const int64_t* __restric
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= N) return;
   int64_t tok = idx[row];
+  PZ_DEVICE_CHECK(tok >= 0 && tok < V);
   tok = tok < 0 ? 0 : (tok >= V ? V - 1 : tok);
   const int pos = off + row % T;
   for (int c = 8 * lane; c < C; c += 512) {
@@ -175,6 +176,7 @@ __global__ void __launch_bounds__(256) embed_bwd_tok_kernel(const float* __restr
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= N) return;
   const int64_t tok = idx[row];
+  PZ_DEVICE_CHECK(tok >= 0 && tok < V);
   if (tok < 0 || tok >= V) return;
   float* dst = dwte + (size_t)tok * C;
   const float* src = dout + (size_t)row * C;

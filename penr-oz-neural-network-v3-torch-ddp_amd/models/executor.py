@@ -38,6 +38,7 @@ from penroz.ops import activations as act_ops
 from penroz.ops import fused as fused_ops
 from penroz.ops import norms as norm_ops
 from penroz.ops import gemm as gemm_ops
+from penroz.utils.profiling import trace_range
 from penroz.ops import _ext
 
 log = logging.getLogger(__name__)
@@ -341,12 +342,15 @@ class GPTExecutor:
         N, C = B * T, s.C
         seed = self._step_seed
         self._step_seed += 1000
-        self._forward(idx, training=True, dropout_seed=seed)
+        with trace_range("forward"):
+            self._forward(idx, training=True, dropout_seed=seed)
         cap = capture and self._captured is None
         if cap:
             acts = [self.resid[0].view(B, T, C).clone()] * 2 + [r.view(B, T, C).clone() for r in self.resid[1:]] + \
                    [self.lnf_out.view(B, T, C).float().clone(), self.logits.view(B, T, -1).clone()]
         # ---- head: CE (in place -> dlogits), lm_head backward, final LN backward
+        head_range = trace_range("backward.head")
+        head_range.__enter__()
         rows = fused_ops.cross_entropy_fwd_bwd(self.logits, targets.reshape(-1), scale / N)
         loss = rows.sum() * (scale / N)
         torch.mm(self.logits, self.bf16(s.head.weight), out=self.d_c)
@@ -360,7 +364,10 @@ class GPTExecutor:
             grads_cap = [self.logits.view(B, T, -1).clone(), self.d_c.view(B, T, C).float().clone(),
                          self.dresid.view(B, T, C).clone()]
         self._segment_done(0, sync)
+        head_range.__exit__(None, None, None)
         for l in range(self.L - 1, -1, -1):
+            layer_range = trace_range(f"backward.block{l}")
+            layer_range.__enter__()
             b = s.blocks[l]
             # ---- MLP branch
             torch.mm(self.dresid_bf, self.bf16(b.fc2.weight), out=self.d_f)
@@ -387,11 +394,13 @@ class GPTExecutor:
             if cap:
                 grads_cap.append(self.dresid.view(B, T, C).clone())
             self._segment_done(self.L - l, sync)
+            layer_range.__exit__(None, None, None)
         fused_ops.embedding_bwd(self.dresid, idx, self.grad(s.wte.weight), self.grad(s.wpe.weight),
                                 s.wpe.position_offset)
         self._segment_done(self.L + 1, sync)
         if sync and self.reducer is not None:
-            self.reducer.finish()
+            with trace_range("grad_allreduce.wait"):
+                self.reducer.finish()
         if cap:
             # grads_cap: [dlogits, d_lnf, d_resid[L], d_resid[L-1], ..., d_resid[0]]
             dlog, dlnf, dres = grads_cap[0], grads_cap[1], grads_cap[2:]
@@ -404,11 +413,10 @@ class GPTExecutor:
 
     def optimizer_step(self):
         opt = self.model.optimizer
-        if self._opt_flat:
+        with trace_range("optimizer"):
             opt.step()
-        else:
-            opt.step()
-            self.refresh_shadow()
+            if not self._opt_flat:
+                self.refresh_shadow()
 
     def captured(self):
         if self._captured is None:

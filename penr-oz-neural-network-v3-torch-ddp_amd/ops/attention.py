@@ -25,7 +25,11 @@ import torch.nn.functional as F
 
 from penroz.ops._ext import use_kernels, kernels
 
-SUPPORTED_HEAD_DIMS = (64, 128)
+# head dims with a native kernel: prefill / training flash attention (csrc/kernels/flash_attn.hip)
+# and decode attention (csrc/kernels/decode_attn.hip). Other head dims (e.g. Gemma's 256) run
+# torch SDPA on the GPU.
+SUPPORTED_HEAD_DIMS = (64,)
+DECODE_HEAD_DIMS = (64, 128)
 
 
 def reference_causal_attention_qkv(qkv: Tensor, H: int, Hkv: int, D: int, dropout_p: float = 0.0) -> Tensor:
@@ -131,7 +135,7 @@ def decode_attention(q: Tensor, k_cache: Tensor, v_cache: Tensor, seq_len: int,
     GPU: split-K decode kernel (``csrc/kernels/decode_attn.hip``).
     """
     Tq = q.shape[1]
-    if use_kernels(q):
+    if use_kernels(q) and q.shape[-1] in DECODE_HEAD_DIMS:
         return kernels().decode_attn(q.contiguous(), k_cache, v_cache, k_scale, v_scale, int(seq_len),
                                      int(seq_len - Tq), 1.0 / math.sqrt(q.shape[-1]))
     k = k_cache[:, :, :seq_len]

@@ -15,7 +15,10 @@ buckets, autograd hooks, all-reduce during backward).  Design for 8×MI355X / xG
   own stream (RCCL), ordered after the producing kernels by a stream event, so it overlaps
   the rest of the backward; ``finish()`` makes the compute stream wait for all of them
   before the optimizer step;
-* ``no_sync`` micro-steps: the caller simply does not call ``bucket_ready`` until the last.
+* ``no_sync`` micro-steps: the caller simply does not call ``bucket_ready`` until the last;
+* optional bf16 wire format (``PENROZ_GRAD_WIRE=bf16``): a bucket is cast to a bf16 staging
+  buffer on the compute stream, all-reduced in bf16 (half the xGMI bytes), and cast back into
+  the fp32 gradient buffer in ``finish()``; accumulation and the optimizer stay fp32.
 
 Transport: ``torch.distributed`` with the ``nccl`` backend (= RCCL on ROCm; the reference's
 ``ProcessGroupNCCL`` call pattern is *not* replicated — one async all-reduce per bucket with
@@ -33,6 +36,7 @@ import torch.distributed as dist
 log = logging.getLogger(__name__)
 
 DEFAULT_BUCKET_MB = float(os.environ.get("PENROZ_BUCKET_MB", "64"))
+WIRE_DTYPES = {"fp32": None, "bf16": torch.bfloat16}
 
 
 def plan_buckets(segments: list[tuple[int, int]], bucket_bytes: float, elem_size: int = 4) -> list[tuple[int, int]]:
@@ -56,7 +60,8 @@ def plan_buckets(segments: list[tuple[int, int]], bucket_bytes: float, elem_size
 
 
 class GradReducer:
-    def __init__(self, flat_grad: torch.Tensor, buckets: list[tuple[int, int]], group=None):
+    def __init__(self, flat_grad: torch.Tensor, buckets: list[tuple[int, int]], group=None,
+                 wire: str | None = None):
         self.flat_grad = flat_grad
         self.buckets = buckets
         self.group = group
@@ -68,8 +73,15 @@ class GradReducer:
         if self.world > 1 and flat_grad.is_cuda and os.environ.get("PENROZ_COMM", "c10d") == "native":
             from penroz.parallel import rccl
             self._native = rccl.NativeComm.get(group)
+        wire = wire or os.environ.get("PENROZ_GRAD_WIRE", "fp32")
+        if wire not in WIRE_DTYPES:
+            raise ValueError(f"PENROZ_GRAD_WIRE must be one of {sorted(WIRE_DTYPES)}, got {wire!r}")
+        wdt = WIRE_DTYPES[wire]
+        self._wire = None
+        if self.world > 1 and wdt is not None and wdt != flat_grad.dtype:
+            self._wire = torch.empty(flat_grad.numel(), dtype=wdt, device=flat_grad.device)
         log.info(f"GradReducer: {len(buckets)} bucket(s) over {flat_grad.numel() * 4 / 2**20:.1f} MiB, "
-                 f"world {self.world}, transport {'native-rccl' if self._native else self.backend}")
+                 f"world {self.world}, transport {'native-rccl' if self._native else self.backend}, wire {wire}")
 
     def bucket_of(self, elem_index: int) -> int:
         for i, (s, e) in enumerate(self.buckets):
@@ -83,6 +95,9 @@ class GradReducer:
             return
         s, e = self.buckets[i]
         view = self.flat_grad[s:e]
+        if self._wire is not None:
+            self._wire[s:e].copy_(view)  # cast on the producing stream, then reduce the copy
+            view = self._wire[s:e]
         self._launched[i] = True
         if self._native is not None:
             self._native.all_reduce_avg_async(view)
@@ -105,6 +120,9 @@ class GradReducer:
             else:
                 w.wait()
         self._works.clear()
+        if self._wire is not None:
+            for s, e in self.buckets:
+                self.flat_grad[s:e].copy_(self._wire[s:e])
         self._launched = [False] * len(self.buckets)
 
     def broadcast_params(self, flat_param: torch.Tensor, src: int = 0):

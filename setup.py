@@ -1,6 +1,8 @@
 """Build the penroz native extensions in-tree for gfx950 with hipcc (no hipify, no CUDA).
 
     python setup.py build_ext        # -> build_ext/penroz_kernels*.so, build_ext/penroz_comm*.so
+    PENROZ_DEBUG=1 python setup.py build_ext   # -> build_ext/debug/ (-O1 -g, device bounds
+                                     #    checks; load with PENROZ_EXT_DIR=build_ext/debug)
     python setup.py isa KERNEL.hip   # -> build_ext/isa/KERNEL.s (gfx950 device assembly, for audits:
                                      #    VGPR/AGPR counts, spills, s_waitcnt placement)
 
@@ -20,7 +22,11 @@ import sysconfig
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(ROOT, "csrc")
-OUT = os.environ.get("PENROZ_BUILD_DIR") or os.path.join(ROOT, "build_ext")  # override: A/B builds
+DEBUG = os.environ.get("PENROZ_DEBUG", "0") == "1"
+# PENROZ_BUILD_DIR overrides (A/B builds); debug builds default to build_ext/debug and are
+# loaded with PENROZ_EXT_DIR=build_ext/debug
+OUT = os.environ.get("PENROZ_BUILD_DIR") or os.path.join(ROOT, "build_ext", "debug" if DEBUG else "")
+OUT = OUT.rstrip(os.sep)
 OBJ = os.path.join(OUT, "obj")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
@@ -36,7 +42,8 @@ def _torch_paths():
 def _flags(name: str):
     incs, _, abi = _torch_paths()
     py_inc = sysconfig.get_paths()["include"]
-    f = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-D__HIP_PLATFORM_AMD__=1",
+    opt = ["-O1", "-g", "-DPENROZ_DEBUG=1"] if DEBUG else ["-O3"]
+    f = opt + ["-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-D__HIP_PLATFORM_AMD__=1",
          "-DUSE_ROCM=1", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", f"-DTORCH_EXTENSION_NAME={name}",
          "-DTORCH_API_INCLUDE_EXTENSION_H", "-Wno-unused-result", "-Wno-unused-variable",
          "-Wno-deprecated-declarations", f"-I{py_inc}", f"-I{CSRC}", f"-I{os.path.join(CSRC, 'kernels')}"]

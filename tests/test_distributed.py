@@ -44,6 +44,35 @@ def test_grad_reducer_averages(tmp_path):
         assert torch.allclose(torch.load(tmp_path / f"g{r}.pt"), want)
 
 
+def _wire_worker(rank, world, port, out):
+    _init(rank, world, port)
+    torch.manual_seed(7)
+    base = torch.randn(1000)
+    g = base * (rank + 1)
+    red = GradReducer(g, plan_buckets([(0, 400), (400, 1000)], 1000), wire="bf16")
+    assert red._wire is not None and red._wire.dtype == torch.bfloat16
+    red.bucket_ready(0)
+    red.finish()  # launches bucket 1, waits, casts back to fp32
+    assert g.dtype == torch.float32
+    torch.save(g, f"{out}/w{rank}.pt")
+    dist.destroy_process_group()
+
+
+def test_grad_reducer_bf16_wire(tmp_path):
+    mp.spawn(_wire_worker, args=(2, _port(), str(tmp_path)), nprocs=2)
+    torch.manual_seed(7)
+    want = torch.randn(1000) * 1.5
+    for r in range(2):
+        got = torch.load(tmp_path / f"w{r}.pt")
+        assert torch.allclose(got, want, rtol=2e-2, atol=2e-2)
+        assert not torch.equal(got, want)  # really went through bf16
+
+
+def test_grad_reducer_rejects_unknown_wire():
+    with pytest.raises(ValueError):
+        GradReducer(torch.zeros(4), [(0, 4)], wire="fp8")
+
+
 def _hooked_worker(rank, world, port, out):
     _init(rank, world, port)
     from penroz.models.mapper import Mapper

@@ -122,3 +122,29 @@ def test_native_rccl_world_size_one():
 def test_graft_smoke():
     import __graft_entry__
     __graft_entry__.smoke()
+
+
+def test_debug_build_training_step():
+    """The PENROZ_DEBUG build (-O1 -g, device bounds checks) runs the flagship smoke step."""
+    import glob
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    dbg = os.path.join(root, "build_ext", "debug")
+    if not glob.glob(os.path.join(dbg, "penroz_kernels*.so")):
+        pytest.skip("debug build not present (PENROZ_DEBUG=1 python setup.py build_ext)")
+    env = dict(os.environ, PENROZ_EXT_DIR=dbg)
+    code = ("import sys; sys.path.insert(0, %r); import __graft_entry__ as g; "
+            "from penroz.ops import _ext; assert _ext._BUILD_DIR == %r; g.smoke()") % (root, dbg)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "smoke ok" in r.stdout
+    assert "device check failed" not in r.stdout + r.stderr
+
+
+def test_roctx_ranges_on_gpu(monkeypatch):
+    from penroz.utils import profiling
+    monkeypatch.setattr(profiling, "ENABLED", True)
+    with profiling.trace_range("test.range"):
+        torch.ones(4, device="cuda").sum().item()
+    profiling.mark("test.mark")
