@@ -49,7 +49,7 @@ def main():
     if "fwd" in a.which:
         from penroz.ops._ext import kernels
         k = kernels()
-        variants = [1, 2, 3] if hasattr(k, "flash_fwd_variant") else [0]
+        variants = [1, 2, 3] + ([99] if os.environ.get('PENROZ_FA_DIAG') else []) if hasattr(k, "flash_fwd_variant") else [0]
         for v in variants:
             if v:
                 prev = k.flash_fwd_variant(v)

@@ -150,6 +150,26 @@ __device__ __forceinline__ void glds16(const void* g, unsigned lds_addr) {
                : "memory");
 }
 
+
+// LDS-DMA with a wave-uniform 64-bit SGPR base and a per-lane 32-bit byte offset: per-piece
+// address updates become scalar adds (no 64-bit VALU address math). No instruction offset:
+// on an LDS-DMA load it would shift the LDS destination as well as the global address.
+__device__ __forceinline__ void glds16_s(const void* sbase, unsigned voff, unsigned lds_addr) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(sbase), "s"(lds_addr)
+               : "memory");
+}
+
+// Make the compiler treat a register value as freshly produced here: it waits for the load
+// that produced it BEFORE this point, so no compiler-tracked load stays outstanding into a
+// loop whose waits are counted by hand (LDS-DMA issued in inline asm is invisible to hipcc's
+// waitcnt pass, and a wait for an old load would also drain the in-flight DMA).
+__device__ __forceinline__ void launder(uint4& v) {
+  asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+}
+
 __device__ __forceinline__ unsigned lds_addr_of(const void* p) { return (unsigned)(size_t)(lds_void_t*)p; }
 
 

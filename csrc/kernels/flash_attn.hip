@@ -474,7 +474,7 @@ __global__ void __launch_bounds__(256, 2) fa_fwd2_kernel(const bf16* __restrict_
 // and used by both blocks, halving LDS traffic per MFMA, and the two blocks' dependency
 // chains interleave: S_B's MFMAs run under softmax_A, P_A·V's under softmax_B. Query blocks
 // of 64 rows are aligned to key tiles, so a wave's only masked tile is its diagonal one.
-template <bool DROPOUT>
+template <bool DROPOUT, bool NOSYNC = false>
 __global__ void __launch_bounds__(128, 2) fa_fwd3_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
                                                       float* __restrict__ lse, int T, int H, int Hkv, float scale,
                                                       float p_drop, uint64_t seed) {
@@ -503,6 +503,10 @@ __global__ void __launch_bounds__(128, 2) fa_fwd3_kernel(const bf16* __restrict_
 #pragma unroll
     for (int s = 0; s < 4; ++s)
       qf[a][s] = qrow[a] < T ? *reinterpret_cast<const uint4*>(qbase + (size_t)qrow[a] * RS + 16 * s + 8 * hh) : zero4();
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) launder(qf[a][s]);  // no compiler-tracked load left for the loop
 
   // LDS-DMA staging (no staging registers). K image is chunk-major [8 chunks][64 keys][16 B]:
   // row-fragment reads (16 lanes on 16 consecutive keys, one chunk) are conflict-free and all
@@ -510,9 +514,32 @@ __global__ void __launch_bounds__(128, 2) fa_fwd3_kernel(const bf16* __restrict_
   // eight pieces share ONE per-lane source pointer. V keeps the swizzled row-major image
   // (tile_off) for the transposed reads; wave 1 fills it, piece p = keys 8p..8p+7. Keys past
   // T are clamped to T-1: finite data that the mask (K) or P = 0 (V) cancels.
+  // fast path (whole tile inside T): SGPR base per piece, per-lane byte offsets fixed
+  const unsigned RSB = (unsigned)RS * 2;  // row stride in bytes
+  const unsigned k_voff = (unsigned)lane * RSB;
+  unsigned v_voff[2];
+#pragma unroll
+  for (int par = 0; par < 2; ++par) {
+    const int row = 8 * par + (lane >> 3);  // rows 8p + (lane>>3): the swizzle depends on p&1 only
+    const int ch = (lane & 7) ^ ((((row >> 1) & 1) << 2) | ((row >> 2) & 3));
+    v_voff[par] = (unsigned)(lane >> 3) * RSB + 16u * ch;
+  }
   auto dma = [&](int kt0, int buf) {
     const unsigned dst = __builtin_amdgcn_readfirstlane(lds_addr_of(smem[buf][w]));
-    if (w == 0) {
+    if (kt0 + BN <= T) {
+      if (w == 0) {
+        const char* sb = reinterpret_cast<const char*>(kbase + (size_t)kt0 * RS);
+        // (the chunk offset goes on the SGPR base: an instruction offset would shift the LDS
+        // destination too)
+#pragma unroll
+        for (int p = 0; p < 8; ++p) glds16_s(sb + 16 * p, k_voff, dst + p * 1024);
+      } else {
+#pragma unroll
+        for (int p = 0; p < 8; ++p)
+          glds16_s(reinterpret_cast<const char*>(vbase + (size_t)(kt0 + 8 * p) * RS), v_voff[p & 1],
+                      dst + p * 1024);
+      }
+    } else if (w == 0) {  // ragged last tile: clamp keys to T-1 per lane
       const bf16* g = kbase + (size_t)min(kt0 + lane, T - 1) * RS;
 #pragma unroll
       for (int p = 0; p < 8; ++p) glds16(g + 8 * p, dst + p * 1024);
@@ -638,17 +665,23 @@ __global__ void __launch_bounds__(128, 2) fa_fwd3_kernel(const bf16* __restrict_
   for (; j < jlast; ++j) {
     dma((j + 1) * BN, (j + 1) & 1);  // j < jlast <= ntiles-1: buffer freed by the last barrier
     tile(std::false_type{}, j);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if constexpr (!NOSYNC) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
   }
   if (j + 1 < ntiles) dma((j + 1) * BN, (j + 1) & 1);
   tile(std::true_type{}, j);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (++j; j < ntiles; ++j) {
-    if (j + 1 < ntiles) dma((j + 1) * BN, (j + 1) & 1);
+  if constexpr (!NOSYNC) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+  }
+  for (++j; j < ntiles; ++j) {
+    if (j + 1 < ntiles) dma((j + 1) * BN, (j + 1) & 1);
+    if constexpr (!NOSYNC) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
   }
 
 #pragma unroll
@@ -778,20 +811,40 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv_kernel(const bf16* __restr
     const int buf = it & 1;
     const int hq = hk * G + it / per_head;
     const int qs0 = (s_first + it % per_head) * QS;
+    // both 32-row halves' S and dP chains are issued before the first half's VALU so the
+    // matrix cores run half 1 under half 0's P / dS math; dP starts from -δ (the row constant
+    // as the initial accumulator), so dS = P·dP' needs no subtraction
+    bool act[2];
+    f32x16 sp[2], dp[2];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int qh0 = qs0 + 32 * half;
+      act[half] = qh0 + 31 >= kw0 && kw0 < T && qh0 < T;
+      if (act[half]) {
+        const char* Qt = qt[buf] + half * 32 * 128;
+        const char* Dt = dot[buf] + half * 32 * 128;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4_t dl = *reinterpret_cast<const float4_t*>(&dels[buf][32 * half + 8 * g + 4 * hh]);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            sp[half][4 * g + k] = 0.f;
+            dp[half][4 * g + k] = DROPOUT ? 0.f : -dl[k];
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          sp[half] = mfma32(row_frag(Qt, 0, s, lane), kf[s], sp[half]);
+          dp[half] = mfma32(row_frag(Dt, 0, s, lane), vf[s], dp[half]);
+        }
+      }
+    }
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
       const int qh0 = qs0 + 32 * half;  // first query row of this 32-row half
-      if (qh0 + 31 >= kw0 && kw0 < T && qh0 < T) {
+      if (act[half]) {
         const char* Qt = qt[buf] + half * 32 * 128;
         const char* Dt = dot[buf] + half * 32 * 128;
-        f32x16 sp, dp;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) sp[i] = dp[i] = 0.f;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          sp = mfma32(row_frag(Qt, 0, s, lane), kf[s], sp);
-          dp = mfma32(row_frag(Dt, 0, s, lane), vf[s], dp);
-        }
         const bool need_mask = (kw0 + 31 > qh0) || (qh0 + 32 > T) || (kw0 + 32 > T);
         auto grads = [&](auto mask_tag) {  // P and dS in place; mask path only on diagonal tiles
           constexpr bool MASK = decltype(mask_tag)::value;
@@ -799,22 +852,22 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv_kernel(const bf16* __restr
           for (int g = 0; g < 4; ++g) {
             const int r0 = 8 * g + 4 * hh;
             const float4_t l2 = *reinterpret_cast<const float4_t*>(&lse2s[buf][32 * half + r0]);
-            const float4_t dl = *reinterpret_cast<const float4_t*>(&dels[buf][32 * half + r0]);
+            float4_t dl = {0.f, 0.f, 0.f, 0.f};
+            if constexpr (DROPOUT) dl = *reinterpret_cast<const float4_t*>(&dels[buf][32 * half + r0]);
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
               const int i = 4 * g + k;
               const int q = qh0 + r0 + k;
-              float p = fexp2(fmaf(sp[i], c, -l2[k]));
+              float p = fexp2(fmaf(sp[half][i], c, -l2[k]));
               if constexpr (MASK) p = (key > q || q >= T || key >= T) ? 0.f : p;
-              float dpi = dp[i];
-              float pdrop = p;
               if constexpr (DROPOUT) {
                 const bool keep = dropout_keep(seed, b, hq, H, T, q, key, p_drop);
-                pdrop = keep ? p * inv_keep : 0.f;
-                dpi = keep ? dpi * inv_keep : 0.f;
+                sp[half][i] = keep ? p * inv_keep : 0.f;
+                dp[half][i] = p * ((keep ? dp[half][i] * inv_keep : 0.f) - dl[k]);
+              } else {
+                sp[half][i] = p;
+                dp[half][i] = p * dp[half][i];
               }
-              sp[i] = pdrop;
-              dp[i] = p * (dpi - dl[k]);
             }
           }
         };
@@ -824,7 +877,7 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv_kernel(const bf16* __restr
           grads(std::false_type{});
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss) {
-          const uint4 pf = acc_frag(sp, ss), sf = acc_frag(dp, ss);
+          const uint4 pf = acc_frag(sp[half], ss), sf = acc_frag(dp[half], ss);
 #pragma unroll
           for (int dh = 0; dh < 2; ++dh) {
             dv[dh] = mfma32(tr_frag(Dt, 16 * ss, 32 * dh, lane), pf, dv[dh]);
@@ -927,46 +980,51 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dq_kernel(const bf16* __restric
     const char* Kt = smem[j & 1][0];
     const char* Vt = smem[j & 1][1];
     if (kt0 <= q0 + 31) {
+      // dP starts from -δ (row constant = this lane's query row); per 32-key half the dS math
+      // is followed by its dQ MFMAs so the second half's VALU overlaps the first half's MFMAs
       f32x16 s[2], dp[2];
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) s[kh][i] = dp[kh][i] = 0.f;
+        for (int i = 0; i < 16; ++i) {
+          s[kh][i] = 0.f;
+          dp[kh][i] = DROPOUT ? 0.f : -dl;
+        }
 #pragma unroll
         for (int st = 0; st < 4; ++st) {
           s[kh] = mfma32(row_frag(Kt, 32 * kh, st, lane), qf[st], s[kh]);
           dp[kh] = mfma32(row_frag(Vt, 32 * kh, st, lane), dof[st], dp[kh]);
         }
       }
-      auto grads = [&](auto mask_tag) {  // dS in place; mask path only on diagonal / ragged tiles
-        constexpr bool MASK = decltype(mask_tag)::value;
+      const bool need_mask = (kt0 + BN - 1 > q0) || (kt0 + BN > T) || (q0 + 32 > T);
 #pragma unroll
-        for (int kh = 0; kh < 2; ++kh)
+      for (int kh = 0; kh < 2; ++kh) {
+        auto grads = [&](auto mask_tag) {
+          constexpr bool MASK = decltype(mask_tag)::value;
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
             const int k = kt0 + 32 * kh + acc_row(i, lane);
             float p = fexp2(fmaf(s[kh][i], c, -l2));
             if constexpr (MASK) p = (k > qrow || k >= T || !qok) ? 0.f : p;
-            float dpi = dp[kh][i];
             if constexpr (DROPOUT) {
               const bool keep = dropout_keep(seed, b, h, H, T, qrow, k, p_drop);
-              dpi = keep ? dpi * inv_keep : 0.f;
+              s[kh][i] = p * ((keep ? dp[kh][i] * inv_keep : 0.f) - dl);
+            } else {
+              s[kh][i] = p * dp[kh][i];
             }
-            s[kh][i] = p * (dpi - dl);
           }
-      };
-      if ((kt0 + BN - 1 > q0) || (kt0 + BN > T) || (q0 + 32 > T))
-        grads(std::true_type{});
-      else
-        grads(std::false_type{});
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh)
+        };
+        if (need_mask)
+          grads(std::true_type{});
+        else
+          grads(std::false_type{});
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss) {
           const uint4 sf = acc_frag(s[kh], ss);
 #pragma unroll
           for (int dh = 0; dh < 2; ++dh) dq[dh] = mfma32(tr_frag(Kt, 32 * kh + 16 * ss, 32 * dh, lane), sf, dq[dh]);
         }
+      }
     }
     if (j + 1 < ntiles) lstore((j + 1) & 1);
     __syncthreads();
@@ -1018,9 +1076,12 @@ void flash_attn_fwd(torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int
   else if (g_fa_fwd_variant == 2)
     hipLaunchKernelGGL(fa_fwd2_kernel<false>, grid, dim3(256), 0, stream, q, o, lse.data_ptr<float>(), T, (int)H,
                        (int)Hkv, (float)scale, 0.f, (uint64_t)seed);
-  else
+  else if (g_fa_fwd_variant == 3)
     hipLaunchKernelGGL(fa_fwd3_kernel<false>, grid, dim3(128), 0, stream, q, o, lse.data_ptr<float>(), T, (int)H,
                        (int)Hkv, (float)scale, 0.f, (uint64_t)seed);
+  else  // 99: timing diagnostic only (no DMA wait / barrier inside the loop: WRONG results)
+    hipLaunchKernelGGL((fa_fwd3_kernel<false, true>), grid, dim3(128), 0, stream, q, o, lse.data_ptr<float>(), T,
+                       (int)H, (int)Hkv, (float)scale, 0.f, (uint64_t)seed);
 }
 
 // 1 = single-stage forward (fa_fwd_kernel), 2 = tile-pipelined forward (fa_fwd2_kernel),

@@ -91,12 +91,14 @@ class KVCache:
     def _alloc(self, like: Tensor, B: int, Hkv: int, cap: int, D: int, dtype=None):
         return torch.empty(B, Hkv, cap, D, dtype=dtype or like.dtype, device=like.device)
 
-    def _ensure(self, layer_idx: int, like: Tensor, B: int, Hkv: int, D: int, needed: int):
+    def _ensure(self, layer_idx: int, like: Tensor, B: int, Hkv: int, D: int, new_tokens: int):
+        """Make room for ``new_tokens`` more (a shape / device change resets the layer first)."""
         k = self._k[layer_idx]
         if k is not None and (k.shape[0] != B or k.shape[1] != Hkv or k.shape[3] != D
                               or k.device != like.device):
             k = None
             self._len[layer_idx] = 0
+        needed = self._len[layer_idx] + new_tokens
         if k is None:
             cap = max(needed, self._capacity_hint or DEFAULT_CAPACITY)
             self._k[layer_idx] = self._alloc(like, B, Hkv, cap, D)
@@ -112,8 +114,8 @@ class KVCache:
     def _write(self, layer_idx: int, k_bthd: Tensor, v_bthd: Tensor) -> int:
         """Store k/v given as [B, T, Hkv, D]; returns the new length."""
         B, T, Hkv, D = k_bthd.shape
+        self._ensure(layer_idx, k_bthd, B, Hkv, D, T)
         pos = self._len[layer_idx]
-        self._ensure(layer_idx, k_bthd, B, Hkv, D, pos + T)
         samp_ops.kv_store_into(k_bthd, self._k[layer_idx], pos)
         samp_ops.kv_store_into(v_bthd, self._v[layer_idx], pos)
         self._len[layer_idx] = pos + T
@@ -162,12 +164,14 @@ class TurboQuantKVCache(KVCache):
     def _dequantize(quantized: Tensor, scale: Tensor) -> Tensor:
         return quantized.float() * scale
 
-    def _ensure(self, layer_idx: int, like: Tensor, B: int, Hkv: int, D: int, needed: int):
+    def _ensure(self, layer_idx: int, like: Tensor, B: int, Hkv: int, D: int, new_tokens: int):
+        """Make room for ``new_tokens`` more (a shape / device change resets the layer first)."""
         k = self._k[layer_idx]
         if k is not None and (k.shape[0] != B or k.shape[1] != Hkv or k.shape[3] != D
                               or k.device != like.device):
             k = None
             self._len[layer_idx] = 0
+        needed = self._len[layer_idx] + new_tokens
         if k is None:
             cap = max(needed, self._capacity_hint or DEFAULT_CAPACITY)
             self._k[layer_idx] = self._alloc(like, B, Hkv, cap, D, torch.int8)
@@ -188,8 +192,8 @@ class TurboQuantKVCache(KVCache):
 
     def _write(self, layer_idx: int, k_bthd: Tensor, v_bthd: Tensor) -> int:
         B, T, Hkv, D = k_bthd.shape
+        self._ensure(layer_idx, k_bthd, B, Hkv, D, T)
         pos = self._len[layer_idx]
-        self._ensure(layer_idx, k_bthd, B, Hkv, D, pos + T)
         samp_ops.kv_quantize_into(k_bthd, self._k[layer_idx], self._sk[layer_idx], pos)
         samp_ops.kv_quantize_into(v_bthd, self._v[layer_idx], self._sv[layer_idx], pos)
         self._dtype[layer_idx] = k_bthd.dtype

@@ -1,7 +1,7 @@
 """Build the penroz native extensions in-tree for gfx950 with hipcc (no hipify, no CUDA).
 
     python setup.py build_ext        # -> build_ext/penroz_kernels*.so, build_ext/penroz_comm*.so
-    PENROZ_DEBUG=1 python setup.py build_ext   # -> build_ext/debug/ (-O1 -g, device bounds
+    PENROZ_DEBUG=1 python setup.py build_ext   # -> build_ext/debug/ (-O1, device bounds
                                      #    checks; load with PENROZ_EXT_DIR=build_ext/debug)
     python setup.py isa KERNEL.hip   # -> build_ext/isa/KERNEL.s (gfx950 device assembly, for audits:
                                      #    VGPR/AGPR counts, spills, s_waitcnt placement)
@@ -42,7 +42,7 @@ def _torch_paths():
 def _flags(name: str):
     incs, _, abi = _torch_paths()
     py_inc = sysconfig.get_paths()["include"]
-    opt = ["-O1", "-g", "-DPENROZ_DEBUG=1"] if DEBUG else ["-O3"]
+    opt = ["-O1", "-DPENROZ_DEBUG=1"] if DEBUG else ["-O3"]
     f = opt + ["-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-D__HIP_PLATFORM_AMD__=1",
          "-DUSE_ROCM=1", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", f"-DTORCH_EXTENSION_NAME={name}",
          "-DTORCH_API_INCLUDE_EXTENSION_H", "-Wno-unused-result", "-Wno-unused-variable",

@@ -1,0 +1,218 @@
+"""Rank/env helpers, collectives and launcher plumbing (reference: test_ddp.py, 24 tests, all
+mocked). Real multi-process behaviour is covered separately in test_distributed.py."""
+import logging
+import os
+from unittest import mock
+
+import pytest
+import torch
+
+from penroz.parallel import dist as D
+from penroz.parallel import launcher as LA
+
+
+@pytest.fixture
+def clean_env(monkeypatch):
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "PENROZ_FAULT_RANK", "PENROZ_FAULT_STEP"):
+        monkeypatch.delenv(k, raising=False)
+    return monkeypatch
+
+
+def test_is_ddp_false_without_rank(clean_env):
+    assert not D.is_ddp()
+
+
+def test_is_ddp_true_with_rank(clean_env):
+    clean_env.setenv("RANK", "0")
+    assert D.is_ddp()
+
+
+@pytest.mark.parametrize("fn,var,default", [(D.ddp_rank, "RANK", 0), (D.ddp_local_rank, "LOCAL_RANK", 0),
+                                            (D.ddp_world_size, "WORLD_SIZE", 1)])
+def test_rank_helpers_default(clean_env, fn, var, default):
+    assert fn() == default
+
+
+@pytest.mark.parametrize("fn,var", [(D.ddp_rank, "RANK"), (D.ddp_local_rank, "LOCAL_RANK"),
+                                    (D.ddp_world_size, "WORLD_SIZE")])
+def test_rank_helpers_set(clean_env, fn, var):
+    clean_env.setenv(var, "3")
+    assert fn() == 3
+
+
+@pytest.mark.parametrize("rank,expected", [(None, True), ("0", True), ("2", False)])
+def test_master_proc(clean_env, rank, expected):
+    if rank is not None:
+        clean_env.setenv("RANK", rank)
+    assert D.master_proc() is expected
+
+
+@pytest.mark.parametrize("device,backend", [("cuda", "nccl"), ("cuda:3", "nccl"), ("cpu", "gloo"), ("mps", "gloo")])
+def test_backend_for(device, backend):
+    assert D.backend_for(device) == backend
+
+
+@pytest.mark.parametrize("rank,world,device,expected", [
+    (None, None, "cuda", False),   # not launched distributed
+    ("0", "2", "cuda", True),
+    ("0", "2", "cpu", True),
+    ("0", "1", "mps", False),      # single-process MPS: no DDP (reference semantics)
+    ("0", "2", "mps", True),
+])
+def test_use_ddp_matrix(clean_env, rank, world, device, expected):
+    if rank is not None:
+        clean_env.setenv("RANK", rank)
+        clean_env.setenv("WORLD_SIZE", world)
+    assert D.use_ddp(device) is expected
+
+
+def test_ddp_all_reduce_nccl_uses_avg(clean_env):
+    t = torch.ones(3)
+    with mock.patch.object(D.dist, "get_backend", return_value="nccl"), \
+            mock.patch.object(D.dist, "all_reduce") as ar:
+        D.ddp_all_reduce(t)
+    assert ar.call_args.kwargs["op"] == D.dist.ReduceOp.AVG
+    assert torch.equal(t, torch.ones(3))
+
+
+def test_ddp_all_reduce_gloo_sums_then_divides(clean_env):
+    clean_env.setenv("WORLD_SIZE", "4")
+    t = torch.full((2,), 8.0)
+    with mock.patch.object(D.dist, "get_backend", return_value="gloo"), \
+            mock.patch.object(D.dist, "all_reduce") as ar:
+        D.ddp_all_reduce(t)
+    assert ar.call_args.kwargs["op"] == D.dist.ReduceOp.SUM
+    assert torch.equal(t, torch.full((2,), 2.0))
+
+
+def test_max_over_ranks_without_group_is_identity():
+    assert D.max_over_ranks(1.5, "cpu") == 1.5
+
+
+def test_reconfig_logging_applies_dictconfig(clean_env):
+    with mock.patch.object(D.logging.config, "dictConfig") as dc:
+        D.reconfig_logging()
+    cfg = dc.call_args.args[0]
+    assert cfg["version"] == 1 and "ddp_file" not in cfg["handlers"]
+
+
+def test_reconfig_logging_adds_rank_file_off_linux(clean_env, tmp_path):
+    clean_env.setenv("RANK", "1")
+    clean_env.chdir(tmp_path)
+    with mock.patch.object(D, "running_on_linux", return_value=False), \
+            mock.patch.object(D.logging.config, "dictConfig") as dc:
+        D.reconfig_logging()
+    cfg = dc.call_args.args[0]
+    h = cfg["handlers"]["ddp_file"]
+    assert h["filename"].endswith("ddp_rank01.log") and h["maxBytes"] == 10 * 1024 * 1024
+    assert "ddp_file" in cfg["root"]["handlers"]
+    assert (tmp_path / "logs").is_dir()
+
+
+def test_free_port_is_bindable():
+    import socket
+    p = LA.free_port()
+    s = socket.socket()
+    s.bind(("127.0.0.1", p))
+    s.close()
+
+
+def test_default_nproc_cpu_splits_cores():
+    with mock.patch.object(LA.os, "cpu_count", return_value=16):
+        assert LA.default_nproc("cpu") == 8
+
+
+def test_default_nproc_cuda_counts_devices():
+    with mock.patch.object(LA.torch.cuda, "device_count", return_value=8):
+        assert LA.default_nproc("cuda") == 8
+
+
+class _FakeProc:
+    instances = []
+
+    def __init__(self, target, args, name):
+        self.target, self.args, self.name = target, args, name
+        self.exitcode = 0
+        r, w = os.pipe()
+        os.close(w)  # the read end is immediately "ready" (EOF), like an exited process sentinel
+        self.sentinel = r
+        _FakeProc.instances.append(self)
+
+    def start(self):
+        pass
+
+    def join(self, timeout=None):
+        pass
+
+    def terminate(self):
+        pass
+
+    def kill(self):
+        pass
+
+
+def test_launcher_env_per_rank_and_omp_split():
+    _FakeProc.instances = []
+    ctx = mock.Mock()
+    ctx.Process.side_effect = lambda target, args, name: _FakeProc(target, args, name)
+    with mock.patch.object(LA.mp, "get_context", return_value=ctx), \
+            mock.patch.object(LA.os, "cpu_count", return_value=8):
+        code = LA.launch_single_node_ddp("run42", "cpu", print, nproc=2)
+    assert code == 0
+    envs = [p.args[0] for p in _FakeProc.instances]
+    assert [e["RANK"] for e in envs] == ["0", "1"]
+    assert all(e["WORLD_SIZE"] == "2" and e["MASTER_ADDR"] == "127.0.0.1" for e in envs)
+    assert all(e["OMP_NUM_THREADS"] == "4" and e["PENROZ_RUN_ID"] == "run42" for e in envs)
+    assert envs[0]["MASTER_PORT"] == envs[1]["MASTER_PORT"]
+    for p in _FakeProc.instances:
+        os.close(p.sentinel)
+
+
+def test_launcher_gpu_env_keeps_omp_and_ipc_mode():
+    _FakeProc.instances = []
+    ctx = mock.Mock()
+    ctx.Process.side_effect = lambda target, args, name: _FakeProc(target, args, name)
+    with mock.patch.object(LA.mp, "get_context", return_value=ctx):
+        LA.launch_single_node_ddp("r", "cuda", print, nproc=2)
+    envs = [p.args[0] for p in _FakeProc.instances]
+    assert all("OMP_NUM_THREADS" not in e and e["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" for e in envs)
+    for p in _FakeProc.instances:
+        os.close(p.sentinel)
+
+
+def test_launcher_reports_first_failure():
+    _FakeProc.instances = []
+    ctx = mock.Mock()
+
+    def make(target, args, name):
+        p = _FakeProc(target, args, name)
+        p.exitcode = 13 if name.endswith("rank1") else 0
+        return p
+    ctx.Process.side_effect = make
+    seen = []
+    with mock.patch.object(LA.mp, "get_context", return_value=ctx):
+        code = LA.launch_single_node_ddp("r", "cpu", print, nproc=2, on_failure=lambda r, c: seen.append((r, c)))
+    assert code == 13 and seen == [(1, 13)]
+    for p in _FakeProc.instances:
+        os.close(p.sentinel)
+
+
+def test_fault_injection_only_on_matching_rank_and_step(clean_env):
+    clean_env.setenv("PENROZ_FAULT_RANK", "1")
+    clean_env.setenv("PENROZ_FAULT_STEP", "3")
+    clean_env.setenv("RANK", "1")
+    with mock.patch.object(LA.os, "_exit") as ex:
+        LA.maybe_inject_fault(2)
+        ex.assert_not_called()
+        LA.maybe_inject_fault(3)
+        ex.assert_called_once_with(LA.FAULT_EXIT_CODE)
+    clean_env.setenv("RANK", "0")
+    with mock.patch.object(LA.os, "_exit") as ex:
+        LA.maybe_inject_fault(3)
+        ex.assert_not_called()
+
+
+def test_fault_injection_disabled_by_default(clean_env):
+    with mock.patch.object(LA.os, "_exit") as ex:
+        LA.maybe_inject_fault(0)
+        ex.assert_not_called()
