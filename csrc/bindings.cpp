@@ -73,7 +73,7 @@ PYBIND11_MODULE(penroz_kernels, m) {
   m.def("sample_tokens", &sample_tokens);
   m.def("decode_attn", &decode_attn);
   m.def("wgrad_gemm", &wgrad_gemm, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("grad"),
-        pybind11::arg("tile") = 256, pybind11::arg("variant") = 2);
+        pybind11::arg("tile") = 256, pybind11::arg("variant") = 4);
   m.def("flash_attn_fwd", &flash_attn_fwd);
   m.def("flash_fwd_variant", &flash_fwd_variant, pybind11::arg("variant") = 0,
         "select the forward kernel (1 single-stage, 2 tile-pipelined); returns the previous one");

@@ -414,6 +414,138 @@ __global__ void __launch_bounds__(512, 1) wgrad256_ring_kernel(const bf16* __res
     }
 }
 
+// ---- 16x16x32 MFMA variant ---------------------------------------------------------------
+// Same ring pipeline; each wave's 128×64 output is 8×4 tiles of v_mfma_f32_16x16x32_bf16 (the
+// 16x16 shape holds a higher clock than 32x32x16 on random data at equal cycles per FLOP).
+// Operand fragment (A or B, from a [k][256] tile): lane l holds k = 8·(l>>4) + j, j = 0..7, of
+// column c0 + (l&15) — two ds_read_b64_tr_b16 (rows 8g..8g+3 and 8g+4..8g+7 of its 16-lane
+// group g). One 32-lane read group then covers rows {0-3, 8-11} (or {4-7, 12-15}) × two 16-B
+// chunks; the swizzle ch ^ ((row&3)<<2 | ((row>>3)&1)<<1) puts those 16 pieces on 16 distinct
+// bank slots.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma16(uint4 a, uint4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
+                                                 0, 0, 0);
+}
+
+__device__ __forceinline__ int swz16(int row) { return ((row & 3) << 2) | (((row >> 3) & 1) << 1); }
+
+__device__ __forceinline__ int off512b(int row, int ch) { return row * 512 + ((ch ^ swz16(row)) << 4); }
+
+// element j = tile[kbase + 8·(lane>>4) + j][c0 + (lane&15)]
+__device__ __forceinline__ uint4 tr_frag16(const char* tile, int kbase, int c0, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int col = c0 + 4 * p;
+  const int r0 = kbase + 8 * g + q;
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s16x4*)(tile + off512b(r0, col >> 3) + ((col & 4) << 1)));
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s16x4*)(tile + off512b(r0 + 4, col >> 3) + ((col & 4) << 1)));
+  const uint2 ua = __builtin_bit_cast(uint2, a), ub = __builtin_bit_cast(uint2, b);
+  return uint4{ua.x, ua.y, ub.x, ub.y};
+}
+
+template <int BKT, int NBUF>
+__global__ void __launch_bounds__(512, 1) wgrad256_ring16_kernel(const bf16* __restrict__ A,
+                                                                 const bf16* __restrict__ B, float* __restrict__ out,
+                                                                 int M, int N, int K, int lda, int ldb, int klen,
+                                                                 int tiles_m, int tiles_n, int direct) {
+  extern __shared__ __attribute__((aligned(16))) char smem2[];  // [NBUF][A|B][BKT * 512]
+  constexpr int TILE = BKT * 512;
+  constexpr int PIECES = BKT / 16;
+  constexpr int G = 2 * PIECES;
+  static_assert(BKT % 32 == 0 && NBUF >= 3 && (NBUF - 2) * G <= 63, "ring geometry");
+  const int nwg = gridDim.x, wg = blockIdx.x;
+  const int xcd = wg & 7, qd = nwg >> 3, rd = nwg & 7;
+  const int id = (xcd < rd ? xcd * (qd + 1) : rd * (qd + 1) + (xcd - rd) * qd) + (wg >> 3);
+  const int ntiles = tiles_m * tiles_n;
+  const int split = id / ntiles, tile = id - split * ntiles;
+  const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+  const int m0 = tm * BM2, n0 = tn * BN2;
+  const int k0 = split * klen, k1 = min(K, k0 + klen);
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = w >> 2, wn = w & 3;
+
+  const int rl = lane >> 5, pc = lane & 31;
+  const bf16* asrc[PIECES];
+  const bf16* bsrc[PIECES];
+  int krow[PIECES];
+#pragma unroll
+  for (int i = 0; i < PIECES; ++i) {
+    const int row = 2 * (PIECES * w + i) + rl;
+    const int ch = pc ^ swz16(row);
+    const int mc = m0 + 8 * ch, nc = n0 + 8 * ch;
+    krow[i] = k0 + row;
+    asrc[i] = mc < M ? A + (size_t)krow[i] * lda + mc : nullptr;
+    bsrc[i] = nc < N ? B + (size_t)krow[i] * ldb + nc : nullptr;
+  }
+  const unsigned lds_base = (unsigned)(size_t)(lds_void_t*)smem2;
+  const void* zero = (const void*)g_zero16;
+  auto dma = [&](int st) {
+    const int dk = st * BKT, buf = st % NBUF;
+#pragma unroll
+    for (int i = 0; i < PIECES; ++i) {
+      const bool kok = krow[i] + dk < k1;
+      const void* ga = (kok && asrc[i]) ? (const void*)(asrc[i] + (size_t)dk * lda) : zero;
+      const void* gb = (kok && bsrc[i]) ? (const void*)(bsrc[i] + (size_t)dk * ldb) : zero;
+      const unsigned la = __builtin_amdgcn_readfirstlane(lds_base + buf * 2 * TILE + (PIECES * w + i) * 1024);
+      glds16(ga, la);
+      glds16(gb, la + TILE);
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nsteps = (k1 - k0 + BKT - 1) / BKT;
+#pragma unroll
+  for (int t = 0; t < NBUF - 1; ++t) dma(t);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NBUF - 2) * G) : "memory");
+  __syncthreads();
+  for (int st = 0; st < nsteps; ++st) {
+    dma(st + NBUF - 1);
+    const char* At = smem2 + (st % NBUF) * 2 * TILE;
+    const char* Bt = At + TILE;
+#pragma unroll
+    for (int s = 0; s < BKT / 32; ++s) {
+      uint4 bf[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf[j] = tr_frag16(Bt, 32 * s, 64 * wn + 16 * j, lane);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint4 af = tr_frag16(At, 32 * s, 128 * wm + 16 * i, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af, bf[j], acc[i][j]);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NBUF - 2) * G) : "memory");
+    __syncthreads();
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float* o = direct ? out : out + (size_t)split * M * N;
+  const int g = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + 64 * wn + 16 * j + (lane & 15);
+      if (n >= N) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + 128 * wm + 16 * i + 4 * g + r;
+        if (m < M) {
+          float* p = o + (size_t)m * N + n;
+          if (direct) *p += acc[i][j][r];
+          else *p = acc[i][j][r];
+        }
+      }
+    }
+}
+
 // G[e] += Σ_s slab[s][e]  (vectorised, fixed order)
 __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restrict__ slab, float* __restrict__ g,
                                                           int64_t n4, int splits, int64_t stride4) {
@@ -481,7 +613,8 @@ void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad, int64_t t
   const int direct = splits == 1 ? 1 : 0;
   if (T == 256) {
     // variant: 0 = register staging, 1 = LDS-DMA double buffer (BK 64), 2 = LDS-DMA ring
-    // (BK 32 x 4 stages; default, fastest measured), 3 = LDS-DMA ring (BK 32 x 5 stages).
+    // (BK 32 x 4 stages; default, fastest measured), 3 = LDS-DMA ring (BK 32 x 5 stages),
+    // 4 = ring with 16x16x32 MFMAs (default), 5 = the same with 5 stages.
     // GPT-2 124M, K = 65 536 (TF): qkv 703/809/863/873, proj 683/766/774/766,
     // fc 792/911/962/956, fc2 829/954/984/960, lm_head 911/1019/1032/1024.
     static bool attr_set = false;
@@ -494,6 +627,10 @@ void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad, int64_t t
       hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad256_ring_kernel<32, 4>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, 4 * 2 * 32 * 512);
       hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad256_ring_kernel<32, 5>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 5 * 2 * 32 * 512);
+      hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad256_ring16_kernel<32, 4>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 4 * 2 * 32 * 512);
+      hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad256_ring16_kernel<32, 5>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, 5 * 2 * 32 * 512);
       attr_set = true;
     }
@@ -511,9 +648,17 @@ void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad, int64_t t
         hipLaunchKernelGGL((wgrad256_ring_kernel<32, 4>), dim3(nwg), dim3(512), 4 * 2 * 32 * 512, stream, a, b, dst,
                            M, N, K, lda, ldb, klen, tiles_m, tiles_n, direct);
         break;
-      default:
+      case 3:
         hipLaunchKernelGGL((wgrad256_ring_kernel<32, 5>), dim3(nwg), dim3(512), 5 * 2 * 32 * 512, stream, a, b, dst,
                            M, N, K, lda, ldb, klen, tiles_m, tiles_n, direct);
+        break;
+      case 4:
+        hipLaunchKernelGGL((wgrad256_ring16_kernel<32, 4>), dim3(nwg), dim3(512), 4 * 2 * 32 * 512, stream, a, b,
+                           dst, M, N, K, lda, ldb, klen, tiles_m, tiles_n, direct);
+        break;
+      default:
+        hipLaunchKernelGGL((wgrad256_ring16_kernel<32, 5>), dim3(nwg), dim3(512), 5 * 2 * 32 * 512, stream, a, b,
+                           dst, M, N, K, lda, ldb, klen, tiles_m, tiles_n, direct);
         break;
     }
   } else {

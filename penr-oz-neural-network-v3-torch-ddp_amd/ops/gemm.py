@@ -4,7 +4,7 @@
   accumulate into the flat gradient buffer). GPU: the hand-written MFMA split-K kernel in
   ``csrc/kernels/gemm_wgrad.hip`` (256×256 tile, LDS-DMA staging, transposed LDS reads,
   wave-quantisation-aware split-K, deterministic slab reduction fused with the accumulate).
-  Measured at GPT-2 124M shapes (K = 65 536 tokens, profiles/kernel_bench_r1_wgrad_glds.log): 750–990 TF
+  Measured at GPT-2 124M shapes (K = 65 536 tokens, profiles/kernel_bench_r1_wgrad_ring16.log): 800–1100 TF
   vs hipBLASLt's 270–950 TF on the same calls. Forward / dgrad GEMMs stay on hipBLASLt through
   ``torch.addmm``/``torch.mm`` (measured ≈0.9–1.4 PF at these shapes).
 """
