@@ -59,10 +59,19 @@ def main():
             if v:
                 k.flash_fwd_variant(prev)
     if "bwd" in a.which:
+        from penroz.ops._ext import kernels
+        k = kernels()
         dout = torch.randn_like(out)
         dq = torch.empty_like(qkv)
-        t = timeit(lambda: A.flash_bwd(dout, qkv, out, lse, H, Hkv, D, dqkv=dq), a.iters)
-        res.update(bwd_us=round(t * 1e6, 1), bwd_TF=round(2.5 * fl / t / 1e12, 1))
+        variants = [1, 2] if hasattr(k, "flash_bwd_variant") else [0]
+        for v in variants:
+            if v:
+                prev = k.flash_bwd_variant(v)
+            t = timeit(lambda: A.flash_bwd(dout, qkv, out, lse, H, Hkv, D, dqkv=dq), a.iters)
+            sfx = f"_v{v}" if v else ""
+            res.update({f"bwd{sfx}_us": round(t * 1e6, 1), f"bwd{sfx}_TF": round(2.5 * fl / t / 1e12, 1)})
+            if v:
+                k.flash_bwd_variant(prev)
     if a.sdpa and Hkv == H:
         q, k, v = (x.view(B, T, H, D).transpose(1, 2) for x in qkv.split(H * D, dim=2))
         t = timeit(lambda: F.scaled_dot_product_attention(q, k, v, is_causal=True), a.iters)

@@ -151,6 +151,16 @@ __device__ __forceinline__ void glds16(const void* g, unsigned lds_addr) {
 }
 
 
+
+// 4-byte LDS-DMA (global_load_lds_dword): 64 lanes x 4 B to LDS [lds_addr, +256 B).
+__device__ __forceinline__ void glds4(const void* g, unsigned lds_addr) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(g), "s"(lds_addr)
+               : "memory");
+}
+
 // LDS-DMA with a wave-uniform 64-bit SGPR base and a per-lane 32-bit byte offset: per-piece
 // address updates become scalar adds (no 64-bit VALU address math). No instruction offset:
 // on an LDS-DMA load it would shift the LDS destination as well as the global address.
@@ -168,6 +178,15 @@ __device__ __forceinline__ void glds16_s(const void* sbase, unsigned voff, unsig
 // waitcnt pass, and a wait for an old load would also drain the in-flight DMA).
 __device__ __forceinline__ void launder(uint4& v) {
   asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+}
+
+
+// Lane id the compiler cannot hoist (volatile v_mbcnt): address math derived from it is
+// recomputed where used instead of being precomputed as loop invariants and spilled.
+__device__ __forceinline__ int opaque_lane_id() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
 }
 
 __device__ __forceinline__ unsigned lds_addr_of(const void* p) { return (unsigned)(size_t)(lds_void_t*)p; }

@@ -190,13 +190,20 @@ def test_flash_fwd(B, T, H, Hkv, variant):
     _close(lse, rl, 2e-3, 1e-4, "lse")
 
 
-@pytest.mark.parametrize("B,T,H,Hkv", [(2, 512, 4, 4), (1, 200, 3, 3), (2, 130, 4, 2), (1, 7, 2, 1)])
-def test_flash_bwd(B, T, H, Hkv):
+@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("B,T,H,Hkv", [(2, 512, 4, 4), (1, 200, 3, 3), (2, 130, 4, 2), (1, 7, 2, 1), (1, 1024, 2, 2),
+                                       (1, 320, 4, 1)])
+def test_flash_bwd(B, T, H, Hkv, variant):
     torch.manual_seed(0)
     qkv = _qkv(B, T, H, Hkv)
     out, lse = A.flash_fwd(qkv, H, Hkv, 64)
     dout = torch.randn(B, T, H * 64, device=DEV).to(torch.bfloat16)
-    dq = A.flash_bwd(dout, qkv, out, lse, H, Hkv, 64)
+    k = _ext.kernels()
+    prev = k.flash_bwd_variant(variant)
+    try:
+        dq = A.flash_bwd(dout, qkv, out, lse, H, Hkv, 64)
+    finally:
+        k.flash_bwd_variant(prev)
     x = qkv.float().requires_grad_()
     ro, _ = A.reference_attention_lse(x, H, Hkv, 64)
     (ro * dout.float()).sum().backward()
