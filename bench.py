@@ -134,7 +134,7 @@ def main():
         flops_per_tok = 6 * (sum(p.numel() for p in model.parameters()) - cfg["V"] * cfg["C"] - cfg["P"] * cfg["C"]) \
             + 12 * cfg["L"] * cfg["C"] * T
         print(json.dumps({
-            "metric": "tokens/sec (whole node) GPT-2 124M DDP train" if args.model == "gpt2-124m"
+            "metric": "tokens/sec (whole node) GPT-2 124M DDP train at 1/2/4/8 MI355X" if args.model == "gpt2-124m"
             else f"tokens/sec (whole node) {args.model} DDP train",
             "value": tok_s, "unit": "tokens/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
