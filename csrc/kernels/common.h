@@ -119,6 +119,29 @@ template <> __device__ __forceinline__ float from_f<float>(float v) { return v; 
 template <> __device__ __forceinline__ bf16 from_f<bf16>(float v) { return __float2bfloat16(v); }
 template <> __device__ __forceinline__ __half from_f<__half>(float v) { return __float2half(v); }
 
+// GELU (erf, or tanh when approx) and its derivative, fp32; shared by the elementwise kernels
+// and the GEMM epilogues.
+__device__ __forceinline__ float gelu_f(float x, int approx) {
+  if (approx) {
+    const float k = 0.7978845608028654f;
+    const float t = tanhf(k * (x + 0.044715f * x * x * x));
+    return 0.5f * x * (1.f + t);
+  }
+  return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));
+}
+
+__device__ __forceinline__ float gelu_grad_f(float x, int approx) {
+  if (approx) {
+    const float k = 0.7978845608028654f;
+    const float x2 = x * x;
+    const float t = tanhf(k * (x + 0.044715f * x2 * x));
+    return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k * (1.f + 3.f * 0.044715f * x2);
+  }
+  const float cdf = 0.5f * (1.f + erff(x * 0.7071067811865476f));
+  const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
 // Counter-based RNG (splitmix/murmur finalizer) -> uniform in [0, 1).
 __device__ __forceinline__ uint32_t hash_u32(uint64_t x) {
   x ^= x >> 33;

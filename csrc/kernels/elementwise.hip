@@ -13,28 +13,6 @@
 
 namespace penroz {
 
-// ------------------------------------------------------------------------------ GELU math
-__device__ __forceinline__ float gelu_f(float x, int approx) {
-  if (approx) {
-    const float k = 0.7978845608028654f;
-    const float t = tanhf(k * (x + 0.044715f * x * x * x));
-    return 0.5f * x * (1.f + t);
-  }
-  return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));
-}
-
-__device__ __forceinline__ float gelu_grad_f(float x, int approx) {
-  if (approx) {
-    const float k = 0.7978845608028654f;
-    const float x2 = x * x;
-    const float t = tanhf(k * (x + 0.044715f * x2 * x));
-    return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k * (1.f + 3.f * 0.044715f * x2);
-  }
-  const float cdf = 0.5f * (1.f + erff(x * 0.7071067811865476f));
-  const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
-}
-
 __device__ __forceinline__ float act_f(float x, int kind) {  // 0 gelu, 1 gelu_tanh, 2 silu
   if (kind == 2) return x / (1.f + __expf(-x));
   return gelu_f(x, kind);

@@ -38,3 +38,40 @@ def wgrad(dy: Tensor, x: Tensor, grad: Tensor) -> None:
         grad.add_(torch.mm(dy.t(), x, out_dtype=torch.float32))
     else:
         reference_wgrad(dy, x, grad)
+
+
+# ---- forward / dgrad GEMMs (csrc/kernels/gemm.hip) ------------------------------------------
+# EXPERIMENTAL native path: persistent 256×256-tile MFMA kernel (LDS-DMA double-buffered 64-deep
+# chunks, ping-pong wave groups) with fused bias / bias+GELU epilogues. Measured slower than
+# hipBLASLt on every GPT-2 shape (profiles/gemm_native_r1.log: 0.78-0.92× fwd, 0.85-0.95× dgrad),
+# so it is OFF by default; PENROZ_NATIVE_GEMM=1 routes linear_fwd / linear_dgrad through it.
+NATIVE_GEMM = os.environ.get("PENROZ_NATIVE_GEMM", "0")
+
+
+def _gemm_ok(a: Tensor, b: Tensor, n: int) -> bool:
+    return (NATIVE_GEMM == "1" and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16
+            and a.shape[1] % 32 == 0 and a.shape[1] >= 128 and n % 8 == 0 and a.stride(1) == 1 and b.stride(1) == 1
+            and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0)
+
+
+def linear_fwd(x: Tensor, w: Tensor, bias: Tensor | None, out: Tensor, act: Tensor | None = None,
+               gelu_approx: str = "none") -> Tensor:
+    """out = x·wᵀ (+ bias); with ``act``: out = pre-activation, act = GELU(out) (one pass)."""
+    if use_kernels(x) and _gemm_ok(x, w, w.shape[0]):
+        kernels().gemm_bf16(x, w, False, bias, out, act, 1 if gelu_approx == "tanh" else 0)
+        return out
+    if bias is not None:
+        torch.addmm(bias, x, w.t(), out=out)
+    else:
+        torch.mm(x, w.t(), out=out)
+    if act is not None:
+        act.copy_(torch.nn.functional.gelu(out.float(), approximate=gelu_approx))
+    return out
+
+
+def linear_dgrad(dy: Tensor, w: Tensor, out: Tensor) -> Tensor:
+    """out = dy·w (input gradient of y = x·wᵀ)."""
+    if use_kernels(dy) and _gemm_ok(dy, w, w.shape[1]):
+        kernels().gemm_bf16(dy, w, True, None, out)
+        return out
+    return torch.mm(dy, w, out=out)
