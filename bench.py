@@ -83,10 +83,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and args.gpus != world:
         raise SystemExit(f"--gpus {args.gpus} != WORLD_SIZE {world}")
+    # PENROZ_BENCH_DEVICE / PENROZ_DIST_BACKEND: rehearsal knobs only (e.g. 2 ranks sharing the
+    # one GPU of a test box over gloo); the headline runs use LOCAL_RANK and nccl (= RCCL).
+    local = int(os.environ.get("PENROZ_BENCH_DEVICE", local))
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        backend = os.environ.get("PENROZ_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
     os.environ["PENROZ_ENGINE"] = args.engine
 
     from penroz.models.mapper import Mapper
