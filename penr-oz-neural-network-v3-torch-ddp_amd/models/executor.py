@@ -157,6 +157,7 @@ class GPTExecutor:
         self.reducer = None
         self._captured = None
         self._step_seed = 0
+        self._side_init()
 
     def _param_order(self):
         s = self.spec
@@ -233,15 +234,17 @@ class GPTExecutor:
         self.logits = torch.empty(N, V, dtype=bf, device=dev)
         self.tmp_c = torch.empty(N, C, dtype=bf, device=dev)
         self.dresid = torch.empty(N, C, dtype=f32, device=dev)
-        self.dresid_bf = torch.empty(N, C, dtype=bf, device=dev)
-        self.d_f = torch.empty(N, F, dtype=bf, device=dev)
+        # gradient buffers read by the side-stream weight-gradient GEMMs rotate between two
+        # copies, so the main stream can produce the next one while the side stream still reads
+        self.dresid_bf2 = [torch.empty(N, C, dtype=bf, device=dev) for _ in range(2)]
+        self.d_f2 = [torch.empty(N, F, dtype=bf, device=dev) for _ in range(2)]
+        self.dqkv2 = [torch.empty(N, 3 * C, dtype=bf, device=dev) for _ in range(2)]
         self.d_c = torch.empty(N, C, dtype=bf, device=dev)
-        self.dqkv = torch.empty(N, 3 * C, dtype=bf, device=dev)
         self._acts_shape = (B, T)
 
     def free_buffers(self):
         for name in ("resid", "resid_mid", "ln1", "ln2", "qkv", "fcpre", "fcact", "lnf_out", "logits", "tmp_c",
-                     "dresid", "dresid_bf", "d_f", "d_c", "dqkv", "att", "lse", "stats", "statsf"):
+                     "dresid", "dresid_bf2", "d_f2", "d_c", "dqkv2", "att", "lse", "stats", "statsf"):
             if hasattr(self, name):
                 delattr(self, name)
         self._acts_shape = None
@@ -325,10 +328,59 @@ class GPTExecutor:
             return
         bkt = self._seg_bucket[seg_index]
         if self._bucket_last_seg[bkt] == seg_index:
-            self.reducer.bucket_ready(bkt)
+            if getattr(self, "_side", None) is None:
+                self.reducer.bucket_ready(bkt)
+                return
+            # the bucket's weight gradients come from the side stream, its bias / LayerNorm
+            # gradients from the main stream: launch the collective from the side stream after
+            # it has caught up with the main stream
+            main = torch.cuda.current_stream(self.device)
+            with torch.cuda.stream(self._side):
+                self._side.wait_stream(main)
+                self.reducer.bucket_ready(bkt)
+
+    # ---- weight gradients on a side HIP stream -------------------------------------------------
+    # The weight-gradient GEMMs are off the backward's critical path (nothing in the backward
+    # reads them), so they run on a second stream: MFMA-bound wgrad kernels then overlap the
+    # memory-/latency-bound work of the main stream (LayerNorm / GELU backward, column sums,
+    # flash-attention backward, cross-entropy). Ordering: the side stream waits on an event
+    # recorded after each operand's producer; before the main stream overwrites a rotating
+    # operand buffer it waits on the event recorded after that buffer's last side-stream reader;
+    # gradient buckets are handed to the reducer from the side stream (after it has also waited
+    # for the main stream's bias / LayerNorm gradients), and the main stream joins the side stream
+    # before the step returns. PENROZ_WGRAD_STREAM=0 runs everything on one stream (A/B).
+    def _side_init(self):
+        import os
+        self._side = None
+        if self.device.type == "cuda" and os.environ.get("PENROZ_WGRAD_STREAM", "1") != "0":
+            self._side = torch.cuda.Stream(device=self.device)
+        self._buf_free = {}
 
     def _wgrad(self, dy: Tensor, x: Tensor, p: Tensor):
-        gemm_ops.wgrad(dy, x, self.grad(p))
+        if getattr(self, "_side", None) is None:
+            gemm_ops.wgrad(dy, x, self.grad(p))
+            return
+        main = torch.cuda.current_stream(self.device)
+        ready = torch.cuda.Event()
+        ready.record(main)
+        with torch.cuda.stream(self._side):
+            self._side.wait_event(ready)
+            gemm_ops.wgrad(dy, x, self.grad(p))
+            done = torch.cuda.Event()
+            done.record(self._side)
+        self._buf_free[dy.data_ptr()] = done
+
+    def _reuse(self, buf: Tensor) -> Tensor:
+        """Main stream: wait until the side stream no longer reads ``buf`` (before overwriting)."""
+        ev = self._buf_free.pop(buf.data_ptr(), None) if getattr(self, "_side", None) is not None else None
+        if ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(ev)
+        return buf
+
+    def _join_side(self):
+        if getattr(self, "_side", None) is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self._side)
+            self._buf_free.clear()
 
     @torch.no_grad()
     def train_micro_step(self, idx: Tensor, targets: Tensor, scale: float, sync: bool = True,
@@ -357,8 +409,10 @@ class GPTExecutor:
         self._wgrad(self.logits, self.lnf_out, s.head.weight)
         mean, rstd = self.statsf
         last = s.blocks[-1]
+        rb = 0  # rotating dresid_bf buffer index
         norm_ops.ln_bwd(self.d_c, self.resid[self.L], mean, rstd, s.lnf.weight, self.dresid, False,
-                        self.dresid_bf, self.grad(s.lnf.weight), self.grad(s.lnf.bias), self.grad(last.fc2.bias))
+                        self._reuse(self.dresid_bf2[rb]), self.grad(s.lnf.weight), self.grad(s.lnf.bias),
+                        self.grad(last.fc2.bias))
         grads_cap = []
         if cap:
             grads_cap = [self.logits.view(B, T, -1).clone(), self.d_c.view(B, T, C).float().clone(),
@@ -369,28 +423,33 @@ class GPTExecutor:
             layer_range = trace_range(f"backward.block{l}")
             layer_range.__enter__()
             b = s.blocks[l]
+            d_f, dqkv = self._reuse(self.d_f2[l & 1]), self._reuse(self.dqkv2[l & 1])
+            dres_bf = self.dresid_bf2[rb]
             # ---- MLP branch
-            torch.mm(self.dresid_bf, self.bf16(b.fc2.weight), out=self.d_f)
-            self._wgrad(self.dresid_bf, self.fcact[l], b.fc2.weight)
-            act_ops.gelu_bwd(self.d_f, self.fcpre[l], s.gelu_approx, self.grad(b.fc.bias), out=self.d_f)
-            torch.mm(self.d_f, self.bf16(b.fc.weight), out=self.d_c)
-            self._wgrad(self.d_f, self.ln2[l], b.fc.weight)
+            torch.mm(dres_bf, self.bf16(b.fc2.weight), out=d_f)
+            self._wgrad(dres_bf, self.fcact[l], b.fc2.weight)
+            act_ops.gelu_bwd(d_f, self.fcpre[l], s.gelu_approx, self.grad(b.fc.bias), out=d_f)
+            torch.mm(d_f, self.bf16(b.fc.weight), out=self.d_c)
+            self._wgrad(d_f, self.ln2[l], b.fc.weight)
             _, _, mean, rstd = self.stats[l]
+            rb ^= 1
+            dres_bf = self._reuse(self.dresid_bf2[rb])
             norm_ops.ln_bwd(self.d_c, self.resid_mid[l], mean, rstd, b.ln2.weight, self.dresid, True,
-                            self.dresid_bf, self.grad(b.ln2.weight), self.grad(b.ln2.bias), self.grad(b.proj.bias))
+                            dres_bf, self.grad(b.ln2.weight), self.grad(b.ln2.bias), self.grad(b.proj.bias))
             # ---- attention branch
-            torch.mm(self.dresid_bf, self.bf16(b.proj.weight), out=self.d_c)
-            self._wgrad(self.dresid_bf, self.att[l], b.proj.weight)
+            torch.mm(dres_bf, self.bf16(b.proj.weight), out=self.d_c)
+            self._wgrad(dres_bf, self.att[l], b.proj.weight)
             attn_ops.flash_bwd(self.d_c.view(B, T, C), self.qkv[l].view(B, T, 3 * C), self.att[l].view(B, T, C),
-                               self.lse[l], s.H, s.H, s.D, b.attn.dropout, seed + l, dqkv=self.dqkv.view(B, T, 3 * C))
-            fused_ops.colsum(self.dqkv, self.grad(b.qkv.bias))
-            torch.mm(self.dqkv, self.bf16(b.qkv.weight), out=self.d_c)
-            self._wgrad(self.dqkv, self.ln1[l], b.qkv.weight)
+                               self.lse[l], s.H, s.H, s.D, b.attn.dropout, seed + l, dqkv=dqkv.view(B, T, 3 * C))
+            fused_ops.colsum(dqkv, self.grad(b.qkv.bias))
+            torch.mm(dqkv, self.bf16(b.qkv.weight), out=self.d_c)
+            self._wgrad(dqkv, self.ln1[l], b.qkv.weight)
             mean, rstd, _, _ = self.stats[l]
             prev_bias = self.grad(s.blocks[l - 1].fc2.bias) if l > 0 else None
+            rb ^= 1
             norm_ops.ln_bwd(self.d_c, self.resid[l], mean, rstd, b.ln1.weight, self.dresid, True,
-                            self.dresid_bf if l > 0 else None, self.grad(b.ln1.weight), self.grad(b.ln1.bias),
-                            prev_bias)
+                            self._reuse(self.dresid_bf2[rb]) if l > 0 else None, self.grad(b.ln1.weight),
+                            self.grad(b.ln1.bias), prev_bias)
             if cap:
                 grads_cap.append(self.dresid.view(B, T, C).clone())
             self._segment_done(self.L - l, sync)
@@ -398,6 +457,7 @@ class GPTExecutor:
         fused_ops.embedding_bwd(self.dresid, idx, self.grad(s.wte.weight), self.grad(s.wpe.weight),
                                 s.wpe.position_offset)
         self._segment_done(self.L + 1, sync)
+        self._join_side()
         if sync and self.reducer is not None:
             with trace_range("grad_allreduce.wait"):
                 self.reducer.finish()
