@@ -40,6 +40,8 @@ torch::Tensor sample_tokens(torch::Tensor logits, c10::optional<torch::Tensor> u
 // decode_attn.hip
 torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c10::optional<torch::Tensor> k_scale,
                           c10::optional<torch::Tensor> v_scale, int64_t S, int64_t q_offset, double scale);
+// elementwise.hip (deferred.h)
+void set_deferred_reduce_stream(int64_t stream, int64_t device);
 // gemm.hip
 void gemm_bf16(torch::Tensor a, torch::Tensor b, bool b_kn, c10::optional<torch::Tensor> bias, torch::Tensor out,
                c10::optional<torch::Tensor> act, int64_t gelu_approx, int64_t ablate);
@@ -76,6 +78,7 @@ PYBIND11_MODULE(penroz_kernels, m) {
   m.def("multi_tensor_adam", &multi_tensor_adam);
   m.def("sample_tokens", &sample_tokens);
   m.def("decode_attn", &decode_attn);
+  m.def("set_deferred_reduce_stream", &set_deferred_reduce_stream);
   m.def("gemm_bf16", &gemm_bf16, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("b_kn"),
         pybind11::arg("bias") = pybind11::none(), pybind11::arg("out"), pybind11::arg("act") = pybind11::none(),
         pybind11::arg("gelu_approx") = 0, pybind11::arg("ablate") = 0);

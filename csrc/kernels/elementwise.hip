@@ -7,7 +7,7 @@
 // 8 columns fixed while it walks rows, so the partial sums live in registers; a workgroup
 // reduces its 4 waves in LDS and writes one partial row, finished by a tiny reduction.
 #include "common.h"
-#include "reduce.h"
+#include "deferred.h"
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 
@@ -337,10 +337,8 @@ static void colsum_impl(const torch::Tensor& a, const torch::Tensor* x, torch::T
       hipLaunchKernelGGL((rows_colsum_kernel<1, T>), dim3(ctiles, R), dim3(256), 0, stream, ap, xp, op,
                          part.data_ptr<float>(), N, F, approx);
   })
-  const int S = reduce_slices(R);
-  auto mid = torch::empty({S, F}, a.options().dtype(torch::kFloat32));
   float* outs[1] = {dst.data_ptr<float>()};
-  reduce_partials_add(part.data_ptr<float>(), 1, R, F, outs, mid.data_ptr<float>(), S, stream);
+  reduce_partials_auto(part, 1, R, F, outs, stream);
 }
 
 void gelu_bwd(torch::Tensor dy, torch::Tensor x, int64_t approx, c10::optional<torch::Tensor> dbias,
@@ -490,4 +488,17 @@ std::vector<torch::Tensor> tensor_stats(torch::Tensor x, int64_t bins) {
   auto width = (hi - lo) / (double)bins;
   auto density = hist / ((double)n * width);
   return {mean, stdv, mn, mx, density, edges};
+}
+
+namespace penroz {
+DeferredReduce& deferred_reduce() {
+  static DeferredReduce d;
+  return d;
+}
+}  // namespace penroz
+
+// stream = 0: finish column reductions on the current stream (default)
+void set_deferred_reduce_stream(int64_t stream, int64_t device) {
+  penroz::deferred_reduce().stream = reinterpret_cast<hipStream_t>(stream);
+  penroz::deferred_reduce().device = (int)device;
 }

@@ -13,7 +13,7 @@
 // gradient of the linear that fed this residual — are reduced per workgroup in LDS and
 // finished by a small column-reduction kernel (deterministic, no atomics).
 #include "common.h"
-#include "reduce.h"
+#include "deferred.h"
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 
@@ -371,8 +371,6 @@ void layernorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor mean, torch:
                                          part.data_ptr<float>(), (int)N, (int)C, accumulate ? 1 : 0,
                                          want_bias ? 1 : 0))))
   const int A = want_bias ? 3 : 2;
-  const int S = reduce_slices(grid);
-  auto mid = torch::empty({A, S, C}, x.options().dtype(torch::kFloat32));
   float* outs[3] = {dw.data_ptr<float>(), db.data_ptr<float>(), want_bias ? dbias_prev->data_ptr<float>() : nullptr};
-  reduce_partials_add(part.data_ptr<float>(), A, grid, (int)C, outs, mid.data_ptr<float>(), S, stream);
+  reduce_partials_auto(part, A, grid, (int)C, outs, stream);
 }

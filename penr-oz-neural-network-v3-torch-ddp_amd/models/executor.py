@@ -340,10 +340,10 @@ class GPTExecutor:
                 self.reducer.bucket_ready(bkt)
 
     # ---- weight gradients on a side HIP stream -------------------------------------------------
-    # The weight-gradient GEMMs are off the backward's critical path (nothing in the backward
-    # reads them), so they run on a second stream: MFMA-bound wgrad kernels then overlap the
-    # memory-/latency-bound work of the main stream (LayerNorm / GELU backward, column sums,
-    # flash-attention backward, cross-entropy). Ordering: the side stream waits on an event
+    # The weight-gradient GEMMs, the qkv bias column sum and the finishing kernels of every
+    # dγ / dβ / bias column reduction are off the backward's critical path (nothing in the
+    # backward reads parameter gradients), so they run on a second stream and overlap the
+    # main stream's dgrad GEMMs, LayerNorm / GELU backward, flash-attention backward. Ordering: the side stream waits on an event
     # recorded after each operand's producer; before the main stream overwrites a rotating
     # operand buffer it waits on the event recorded after that buffer's last side-stream reader;
     # gradient buckets are handed to the reducer from the side stream (after it has also waited
@@ -356,19 +356,28 @@ class GPTExecutor:
             self._side = torch.cuda.Stream(device=self.device)
         self._buf_free = {}
 
-    def _wgrad(self, dy: Tensor, x: Tensor, p: Tensor):
+    def _side_call(self, operand: Tensor, fn):
+        """Run ``fn`` (gradient-only work reading ``operand``) on the side stream, or inline."""
         if getattr(self, "_side", None) is None:
-            gemm_ops.wgrad(dy, x, self.grad(p))
+            fn()
             return
         main = torch.cuda.current_stream(self.device)
         ready = torch.cuda.Event()
         ready.record(main)
         with torch.cuda.stream(self._side):
             self._side.wait_event(ready)
-            gemm_ops.wgrad(dy, x, self.grad(p))
+            fn()
             done = torch.cuda.Event()
             done.record(self._side)
-        self._buf_free[dy.data_ptr()] = done
+        self._buf_free[operand.data_ptr()] = done
+
+    def _wgrad(self, dy: Tensor, x: Tensor, p: Tensor):
+        self._side_call(dy, lambda: gemm_ops.wgrad(dy, x, self.grad(p)))
+
+    def _defer_reductions(self, on: bool):
+        """LayerNorm / bias column-reduction finishing kernels go to the side stream (on) or not."""
+        if getattr(self, "_side", None) is not None:
+            _ext.kernels().set_deferred_reduce_stream(self._side.cuda_stream if on else 0, self.device.index or 0)
 
     def _reuse(self, buf: Tensor) -> Tensor:
         """Main stream: wait until the side stream no longer reads ``buf`` (before overwriting)."""
@@ -403,6 +412,7 @@ class GPTExecutor:
         # ---- head: CE (in place -> dlogits), lm_head backward, final LN backward
         head_range = trace_range("backward.head")
         head_range.__enter__()
+        self._defer_reductions(True)
         rows = fused_ops.cross_entropy_fwd_bwd(self.logits, targets.reshape(-1), scale / N)
         loss = rows.sum() * (scale / N)
         torch.mm(self.logits, self.bf16(s.head.weight), out=self.d_c)
@@ -441,7 +451,7 @@ class GPTExecutor:
             self._wgrad(dres_bf, self.att[l], b.proj.weight)
             attn_ops.flash_bwd(self.d_c.view(B, T, C), self.qkv[l].view(B, T, 3 * C), self.att[l].view(B, T, C),
                                self.lse[l], s.H, s.H, s.D, b.attn.dropout, seed + l, dqkv=dqkv.view(B, T, 3 * C))
-            fused_ops.colsum(dqkv, self.grad(b.qkv.bias))
+            self._side_call(dqkv, lambda: fused_ops.colsum(dqkv, self.grad(b.qkv.bias)))
             torch.mm(dqkv, self.bf16(b.qkv.weight), out=self.d_c)
             self._wgrad(dqkv, self.ln1[l], b.qkv.weight)
             mean, rstd, _, _ = self.stats[l]
@@ -457,6 +467,7 @@ class GPTExecutor:
         fused_ops.embedding_bwd(self.dresid, idx, self.grad(s.wte.weight), self.grad(s.wpe.weight),
                                 s.wpe.position_offset)
         self._segment_done(self.L + 1, sync)
+        self._defer_reductions(False)
         self._join_side()
         if sync and self.reducer is not None:
             with trace_range("grad_allreduce.wait"):
