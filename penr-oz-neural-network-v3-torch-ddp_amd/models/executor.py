@@ -157,6 +157,9 @@ class GPTExecutor:
         self.reducer = None
         self._captured = None
         self._step_seed = 0
+        self._reduce_pending = False
+        import os
+        self._overlap_opt = os.environ.get("PENROZ_OVERLAP_OPT", "1") != "0"
         self._side_init()
 
     def _param_order(self):
@@ -317,9 +320,12 @@ class GPTExecutor:
                 self._bucket_last_seg[bkt] = i
 
     def end_training(self):
+        if self.reducer is not None:
+            self.wait_gradients()
         self.reducer = None
 
     def zero_grad(self):
+        self.wait_gradients()
         self.flat_grad.zero_()
         self._captured = None
 
@@ -487,8 +493,16 @@ class GPTExecutor:
         self._defer_reductions(False)
         self._join_side()
         if sync and self.reducer is not None:
-            with trace_range("grad_allreduce.wait"):
-                self.reducer.finish()
+            # Overlap the tail: the last bucket (token embedding, produced by the final kernel of
+            # the backward) is still reducing when the backward ends. If the optimizer step comes
+            # next, it updates each bucket's slice as soon as that bucket's all-reduce has landed
+            # (optimizer_step), instead of waiting for all of them here.
+            self.reducer.launch_remaining()
+            if self._overlap_opt and not cap and self.reducer.per_bucket_waits():
+                self._reduce_pending = True
+            else:
+                with trace_range("grad_allreduce.wait"):
+                    self.reducer.finish()
         if cap:
             # grads_cap: [dlogits, d_lnf, d_resid[L], d_resid[L-1], ..., d_resid[0]]
             dlog, dlnf, dres = grads_cap[0], grads_cap[1], grads_cap[2:]
@@ -499,12 +513,35 @@ class GPTExecutor:
             self._captured = (algos, pairs[:len(algos)])
         return loss
 
+    def wait_gradients(self):
+        """Make the current stream wait for every outstanding gradient all-reduce."""
+        if self._reduce_pending:
+            self._reduce_pending = False
+            self.reducer.finish()
+
     def optimizer_step(self):
         opt = self.model.optimizer
         with trace_range("optimizer"):
+            if self._reduce_pending:
+                self._reduce_pending = False
+                red = self.reducer
+                ranges = [(lambda i=i: red.wait_bucket(i)) for i in range(len(red.buckets))]
+                if self._buckets_tile_flat() and self._opt_flat and opt.flat_step_ranges(ranges):
+                    red.reset()
+                    return
+                red.finish()
             opt.step()
             if not self._opt_flat:
                 self.refresh_shadow()
+
+    def _buckets_tile_flat(self) -> bool:
+        """The ranged optimizer step needs the buckets to cover the flat buffer exactly once."""
+        pos = 0
+        for s, e in sorted(self.reducer.buckets):
+            if s != pos:
+                return False
+            pos = e
+        return pos == self.flat.numel()
 
     def captured(self):
         if self._captured is None:

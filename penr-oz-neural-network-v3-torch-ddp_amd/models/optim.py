@@ -112,7 +112,7 @@ class _FusedMixin:
         return lr, float(b1), float(b2), float(group["eps"]), float(group["weight_decay"]), \
             bool(group.get("maximize", False))
 
-    def _step_flat(self, group, grad_scale):
+    def _step_flat(self, group, grad_scale, ranges=None):
         f = self._flat
         lr, b1, b2, eps, wd, maximize = self._hyper(group)
         step = None
@@ -121,7 +121,23 @@ class _FusedMixin:
             st["step"] += 1
             step = int(st["step"].item()) if step is None else step
         fn = fused_ops.adamw_step if self._decoupled else fused_ops.adam_step
-        fn(f["param"], f["grad"], f["m"], f["v"], f["shadow"], lr, b1, b2, eps, wd, step, grad_scale, maximize)
+        if ranges is None:
+            fn(f["param"], f["grad"], f["m"], f["v"], f["shadow"], lr, b1, b2, eps, wd, step, grad_scale, maximize)
+            return
+        sh = f["shadow"]
+        for r in ranges:  # (s, e) pairs, or a callable returning one (it may wait for the range first)
+            s, e = r() if callable(r) else r
+            fn(f["param"][s:e], f["grad"][s:e], f["m"][s:e], f["v"][s:e], sh[s:e] if sh is not None else None,
+               lr, b1, b2, eps, wd, step, grad_scale, maximize)
+
+    def flat_step_ranges(self, ranges, grad_scale: float = 1.0) -> bool:
+        """Flat step applied range by range (``ranges`` must cover the flat buffer exactly once);
+        False (nothing done) when the flat path does not apply."""
+        if not (len(self.param_groups) == 1 and self._flat is not None
+                and {id(p) for p in self.param_groups[0]["params"]} == self._flat["ids"]):
+            return False
+        self._step_flat(self.param_groups[0], grad_scale, ranges)
+        return True
 
     def _step_list(self, group, grad_scale):
         lr, b1, b2, eps, wd, maximize = self._hyper(group)

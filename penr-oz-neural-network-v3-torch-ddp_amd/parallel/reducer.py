@@ -106,6 +106,34 @@ class GradReducer:
         else:
             self._works.append((dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group, async_op=True), view))
 
+    def launch_remaining(self):
+        """Launch every bucket not yet launched (no wait)."""
+        for i in range(len(self.buckets)):
+            if not self._launched[i]:
+                self.bucket_ready(i)
+
+    def per_bucket_waits(self) -> bool:
+        """True when :meth:`wait_bucket` can wait for one bucket at a time (c10d transport)."""
+        return self._native is None and len(self._works) == len(self.buckets)
+
+    def wait_bucket(self, i: int) -> tuple[int, int]:
+        """Current stream waits for bucket ``i``'s all-reduce (launch order = bucket order);
+        returns its element range, now holding the averaged gradient."""
+        w = self._works[i]
+        if isinstance(w, tuple):
+            w[0].wait()
+            w[1].div_(self.world)
+        else:
+            w.wait()
+        s, e = self.buckets[i]
+        if self._wire is not None:
+            self.flat_grad[s:e].copy_(self._wire[s:e])
+        return s, e
+
+    def reset(self):
+        self._works.clear()
+        self._launched = [False] * len(self.buckets)
+
     def finish(self):
         """Launch any bucket not yet launched, then wait for all of them."""
         for i in range(len(self.buckets)):
