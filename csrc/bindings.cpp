@@ -39,7 +39,8 @@ torch::Tensor sample_tokens(torch::Tensor logits, c10::optional<torch::Tensor> u
                             int64_t top_k);
 // decode_attn.hip
 torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c10::optional<torch::Tensor> k_scale,
-                          c10::optional<torch::Tensor> v_scale, int64_t S, int64_t q_offset, double scale);
+                          c10::optional<torch::Tensor> v_scale, int64_t S, int64_t q_offset, double scale,
+                          c10::optional<torch::Tensor> seq_len_dev);
 // elementwise.hip (deferred.h)
 void set_deferred_reduce_stream(int64_t stream, int64_t device);
 // gemm.hip
@@ -77,7 +78,9 @@ PYBIND11_MODULE(penroz_kernels, m) {
   m.def("adam_step", &adam_step);
   m.def("multi_tensor_adam", &multi_tensor_adam);
   m.def("sample_tokens", &sample_tokens);
-  m.def("decode_attn", &decode_attn);
+  m.def("decode_attn", &decode_attn, pybind11::arg("q"), pybind11::arg("kc"), pybind11::arg("vc"), pybind11::arg("k_scale"),
+        pybind11::arg("v_scale"), pybind11::arg("S"), pybind11::arg("q_offset"), pybind11::arg("scale"),
+        pybind11::arg("seq_len_dev") = pybind11::none());
   m.def("set_deferred_reduce_stream", &set_deferred_reduce_stream);
   m.def("gemm_bf16", &gemm_bf16, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("b_kn"),
         pybind11::arg("bias") = pybind11::none(), pybind11::arg("out"), pybind11::arg("act") = pybind11::none(),

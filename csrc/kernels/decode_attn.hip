@@ -38,13 +38,39 @@ template <> struct KRow<int8_t> {
   __device__ __forceinline__ static float at(const int8_t* p, int d) { return (float)p[d]; }
 };
 
+// 8 consecutive cache elements -> fp32 (one 16-B load for bf16/fp16, 8 B for int8, 32 B for fp32)
+template <typename TK> struct Row8;
+template <> struct Row8<bf16> {
+  __device__ __forceinline__ static void load(const bf16* p, float (&v)[8]) { Vec8<bf16>::load(p, v); }
+};
+template <> struct Row8<__half> {
+  __device__ __forceinline__ static void load(const __half* p, float (&v)[8]) { Vec8<__half>::load(p, v); }
+};
+template <> struct Row8<float> {
+  __device__ __forceinline__ static void load(const float* p, float (&v)[8]) { Vec8<float>::load(p, v); }
+};
+template <> struct Row8<int8_t> {
+  __device__ __forceinline__ static void load(const int8_t* p, float (&v)[8]) {
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[i] = (float)(int8_t)((u.x >> (8 * i)) & 0xff);
+      v[4 + i] = (float)(int8_t)((u.y >> (8 * i)) & 0xff);
+    }
+  }
+};
+
 template <int D, typename TQ, typename TK>
 __global__ void __launch_bounds__(256) decode_kernel(const TQ* __restrict__ q, const TK* __restrict__ kc,
                                                      const TK* __restrict__ vc, const float* __restrict__ ks,
                                                      const float* __restrict__ vs, TQ* __restrict__ out,
                                                      float* __restrict__ ws_o, float* __restrict__ ws_ml, int B,
                                                      int Tq, int H, int Hkv, int cap, int S, int q_offset,
-                                                     int splits, float scale) {
+                                                     int splits, float scale, const int64_t* __restrict__ S_dev) {
+  if (S_dev != nullptr) {  // graph-replayed decode: the cache length lives on the device
+    S = (int)min<int64_t>(*S_dev, (int64_t)cap);
+    q_offset = S - Tq;
+  }
   constexpr int DL = D / 64;  // output columns per lane
   const int G = H / Hkv;
   int wid_lin = blockIdx.x;
@@ -86,7 +112,12 @@ __global__ void __launch_bounds__(256) decode_kernel(const TQ* __restrict__ q, c
     float kv[D];
     const TK* krow = kc + (head_base + (valid ? key : k0)) * D;
 #pragma unroll
-    for (int d = 0; d < D; ++d) kv[d] = KRow<TK>::at(krow, d);
+    for (int c = 0; c < D / 8; ++c) {  // whole K row in flight: D/8 vector loads
+      float t[8];
+      Row8<TK>::load(krow + 8 * c, t);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) kv[8 * c + e] = t[e];
+    }
     const float kscale = ks ? ks[head_base + (valid ? key : k0)] : 1.f;
     float p[kMaxGroup];
 #pragma unroll
@@ -104,19 +135,29 @@ __global__ void __launch_bounds__(256) decode_kernel(const TQ* __restrict__ q, c
 #pragma unroll
       for (int j = 0; j < DL; ++j) o[i][j] *= alpha;
     }
+    // P·V: lane d owns output column(s) d; V rows are read coalesced, 16 rows in flight per
+    // batch (a one-row-at-a-time loop serialises on the load latency: ~70 µs per call at S=128)
     const int nk = min(64, k1 - blk);
-    for (int j = 0; j < nk; ++j) {
-      const TK* vrow = vc + (head_base + blk + j) * D;
-      const float vsc = vs ? vs[head_base + blk + j] : 1.f;
-      float vv[DL];
+    for (int j0 = 0; j0 < nk; j0 += 16) {
+      float vv[16][DL];
 #pragma unroll
-      for (int jj = 0; jj < DL; ++jj) vv[jj] = KRow<TK>::at(vrow, lane + 64 * jj) * vsc;
+      for (int r = 0; r < 16; ++r) {
+        const int j = min(j0 + r, nk - 1);
+        const TK* vrow = vc + (head_base + blk + j) * D;
+        const float vsc = vs ? vs[head_base + blk + j] : 1.f;
 #pragma unroll
-      for (int i = 0; i < kMaxGroup; ++i) {
-        if (i >= G) break;
-        const float pj = __shfl(p[i], j, 64);
+        for (int jj = 0; jj < DL; ++jj) vv[r][jj] = KRow<TK>::at(vrow, lane + 64 * jj) * vsc;
+      }
 #pragma unroll
-        for (int jj = 0; jj < DL; ++jj) o[i][jj] += pj * vv[jj];
+      for (int r = 0; r < 16; ++r) {
+        if (j0 + r >= nk) break;
+#pragma unroll
+        for (int i = 0; i < kMaxGroup; ++i) {
+          if (i >= G) break;
+          const float pj = __shfl(p[i], j0 + r, 64);
+#pragma unroll
+          for (int jj = 0; jj < DL; ++jj) o[i][jj] += pj * vv[r][jj];
+        }
       }
     }
   }
@@ -177,8 +218,12 @@ __global__ void __launch_bounds__(256) decode_combine_kernel(const float* __rest
 
 using namespace penroz;
 
+// seq_len_dev (optional int64 [1] on the device): the cache length is read by the kernel at run
+// time (S / q_offset are then only upper bounds used to size the launch) — lets a captured HIP
+// graph replay the same decode step at every position.
 torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c10::optional<torch::Tensor> k_scale,
-                          c10::optional<torch::Tensor> v_scale, int64_t S, int64_t q_offset, double scale) {
+                          c10::optional<torch::Tensor> v_scale, int64_t S, int64_t q_offset, double scale,
+                          c10::optional<torch::Tensor> seq_len_dev) {
   TORCH_CHECK(q.is_cuda() && q.is_contiguous() && q.dim() == 4, "q must be [B, Tq, H, D]");
   TORCH_CHECK(kc.is_contiguous() && vc.is_contiguous() && kc.dim() == 4 && kc.sizes() == vc.sizes());
   const int B = q.size(0), Tq = q.size(1), H = q.size(2), D = q.size(3);
@@ -201,6 +246,12 @@ torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c
     wo = ws_o.data_ptr<float>();
     wm = ws_ml.data_ptr<float>();
   }
+  const int64_t* sdev = nullptr;
+  if (seq_len_dev.has_value() && seq_len_dev->defined()) {
+    TORCH_CHECK(seq_len_dev->is_cuda() && seq_len_dev->scalar_type() == torch::kInt64 && seq_len_dev->numel() == 1,
+                "seq_len_dev must be a device int64 [1]");
+    sdev = seq_len_dev->data_ptr<int64_t>();
+  }
   const float* ksp = quant ? k_scale->data_ptr<float>() : nullptr;
   const float* vsp = quant ? v_scale->data_ptr<float>() : nullptr;
   auto stream = at::hip::getCurrentHIPStream();
@@ -214,10 +265,10 @@ torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c
     TQ* op = reinterpret_cast<TQ*>(out.data_ptr());
     if (D == 64)
       hipLaunchKernelGGL((decode_kernel<64, TQ, TK>), grid, dim3(256), 0, stream, qp, kp, vp, ksp, vsp, op, wo, wm, B,
-                         Tq, H, Hkv, cap, (int)S, (int)q_offset, splits, (float)scale);
+                         Tq, H, Hkv, cap, (int)S, (int)q_offset, splits, (float)scale, sdev);
     else
       hipLaunchKernelGGL((decode_kernel<128, TQ, TK>), grid, dim3(256), 0, stream, qp, kp, vp, ksp, vsp, op, wo, wm, B,
-                         Tq, H, Hkv, cap, (int)S, (int)q_offset, splits, (float)scale);
+                         Tq, H, Hkv, cap, (int)S, (int)q_offset, splits, (float)scale, sdev);
     if (splits > 1) {
       const int rows = B * Tq * H;
       hipLaunchKernelGGL(decode_combine_kernel<TQ>, dim3(std::min(2048, (rows * D + 255) / 256)), dim3(256), 0, stream,

@@ -1,0 +1,193 @@
+"""Graph-captured incremental decoding: one HIP graph replays a whole decode step.
+
+The reference decodes one token per Python iteration through every layer module
+(``neural_net_model.py:360-406, 457-514``) and grows its KV cache with ``torch.cat``. At
+batch 64 on MI355X that per-token path is launch-bound: ~150 kernel launches plus Python
+dispatch per token cost ~2.9 ms while the actual work (weights + cache read once) is ~0.2 ms.
+
+Here the decode step — the model's own module forward (so numerics are the eager path's:
+same LayerNorm / GELU / decode-attention kernels, same GEMMs), KV append, sampling, and the
+feedback of the sampled token into the next step's input — is captured ONCE per
+(rows, block size, sampling settings) into a ``torch.cuda.CUDAGraph`` (a hipGraph on ROCm) and
+replayed. Everything that changes between steps lives on the device:
+
+* ``StaticKVCache.pos_t`` / ``len_t``: the slot this step writes and the cache length after it;
+  the append is an ``index_copy_`` at ``pos_t`` and the decode-attention kernel reads ``len_t``
+  at run time (``csrc/kernels/decode_attn.hip``, ``seq_len_dev``);
+* ``PositionEmbedding.position_offset_tensor``: the learned position gathered at ``pos_t``;
+* the uniforms of temperature / top-k sampling are drawn on the device (graph-safe Philox);
+* the sampled token is copied into the step's input buffer and into a burst output buffer.
+
+The host only tracks the cache length (one per replay) to switch to the reference's
+sliding-window re-prefill when the window is full, and copies each burst of tokens back once
+(stop-token checks per burst). Prefill and re-prefill run eagerly. Models with RoPE (Gemma)
+keep the eager path: their rotary offset is a host integer per layer.
+"""
+from __future__ import annotations
+
+import logging
+import os
+
+import torch
+from torch import Tensor
+
+from penroz.models import kv_cache as kvc
+from penroz.ops import attention as attn_ops
+from penroz.ops import sampling as samp_ops
+
+log = logging.getLogger(__name__)
+
+GRAPH_DECODE = os.environ.get("PENROZ_GRAPH_DECODE", "1") != "0"
+
+
+class _GraphMode:
+    """Mixin: ``attend`` switches to device-positioned append + attention while capturing."""
+
+    graph_mode = False
+
+    def init_graph_state(self, device):
+        self.pos_t = torch.zeros(1, dtype=torch.long, device=device)  # slot written by the step
+        self.len_t = torch.ones(1, dtype=torch.long, device=device)   # cache length after it
+
+    def attend(self, layer_idx: int, q: Tensor, k: Tensor, v: Tensor) -> Tensor:
+        if not self.graph_mode:
+            return super().attend(layer_idx, q, k, v)
+        return self._attend_graph(layer_idx, q, k, v)
+
+
+class StaticKVCache(_GraphMode, kvc.KVCache):
+    def _attend_graph(self, l: int, q: Tensor, k: Tensor, v: Tensor) -> Tensor:
+        kc, vc = self._k[l], self._v[l]
+        kc.index_copy_(2, self.pos_t, k.transpose(1, 2).to(kc.dtype))
+        vc.index_copy_(2, self.pos_t, v.transpose(1, 2).to(vc.dtype))
+        return attn_ops.decode_attention(q, kc, vc, kc.shape[2], seq_len_dev=self.len_t)
+
+
+class StaticTurboKVCache(_GraphMode, kvc.TurboQuantKVCache):
+    def _attend_graph(self, l: int, q: Tensor, k: Tensor, v: Tensor) -> Tensor:
+        for x, store, scales in ((k, self._k, self._sk), (v, self._v, self._sv)):
+            qx, sx = samp_ops.reference_quantize(x.float().transpose(1, 2))  # [B,Hkv,1,D], [B,Hkv,1,1]
+            store[l].index_copy_(2, self.pos_t, qx)
+            scales[l].index_copy_(2, self.pos_t, sx.squeeze(-1))
+        self._dtype[l] = k.dtype
+        return attn_ops.decode_attention(q, self._k[l], self._v[l], self._k[l].shape[2], self._sk[l], self._sv[l],
+                                         seq_len_dev=self.len_t)
+
+
+def applicable(model) -> bool:
+    if not GRAPH_DECODE or not torch.cuda.is_available():
+        return False
+    p = next(model.parameters(), None)
+    if p is None or not p.is_cuda:
+        return False
+    attn = model._find_attention_layers()
+    return bool(attn) and all(a.rope_theta is None for a in attn)
+
+
+class GraphDecoder:
+    """Static decode state + the captured step graph for ``rows`` sequences."""
+
+    def __init__(self, model, rows: int, capacity: int, temperature: float, top_k: int | None):
+        self.model = model
+        self.device = next(model.parameters()).device
+        self.attn = model._find_attention_layers()
+        self.pos_layers = model._find_position_embeddings()
+        cls = StaticTurboKVCache if kvc.TURBO_QUANT_ENABLED else StaticKVCache
+        self.cache = cls(len(self.attn), capacity)
+        self.cache.init_graph_state(self.device)
+        self.rows, self.capacity = rows, capacity
+        self.temperature, self.top_k = float(temperature), top_k
+        self.idx = torch.zeros(rows, 1, dtype=torch.long, device=self.device)
+        self.out = torch.zeros(rows, capacity, dtype=torch.long, device=self.device)
+        self.step_t = torch.zeros(1, dtype=torch.long, device=self.device)
+        self.graph: torch.cuda.CUDAGraph | None = None
+
+    # ------------------------------------------------------------------ cache attachment
+    def attach(self):
+        for i, a in enumerate(self.attn):
+            a.set_kv_cache(self.cache, i)
+
+    def detach(self):
+        for a in self.attn:
+            a.set_kv_cache(None, 0)
+        for p in self.pos_layers:
+            p.position_offset = 0
+            p.position_offset_tensor = None
+
+    # ------------------------------------------------------------------ the step
+    def _step(self):
+        for p in self.pos_layers:
+            p.position_offset_tensor = self.cache.pos_t
+        self.cache.graph_mode = True
+        try:
+            acts, _ = self.model(self.idx, skip_softmax=True)
+            logits = acts[-1]
+            last = logits[:, -1, :] if logits.ndim == 3 else logits
+            nxt = samp_ops.sample(last, self.temperature, self.top_k, device_rng=True)
+            torch.add(nxt, 0, out=self.idx)  # a kernel, not a memcpy node
+            self.out.index_copy_(1, self.step_t, nxt)
+            self.cache.pos_t.add_(1)
+            self.cache.len_t.add_(1)
+            self.step_t.add_(1)
+        finally:
+            self.cache.graph_mode = False
+            for p in self.pos_layers:
+                p.position_offset_tensor = None
+
+    def _set_state(self, last_tok: Tensor, cache_len: int):
+        self.idx.copy_(last_tok)
+        self.cache.pos_t.fill_(cache_len)
+        self.cache.len_t.fill_(cache_len + 1)
+        self.step_t.zero_()
+
+    def _capture(self, last_tok: Tensor, cache_len: int):
+        # warm-up run on a side stream (lazy allocations, kernel loading), then capture. The
+        # warm-up really executes a step, so it must start from the true state: it then writes
+        # exactly the cache slot the first real step rewrites.
+        self._set_state(last_tok, cache_len)
+        side = torch.cuda.Stream(device=self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            self._step()
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        self._set_state(last_tok, cache_len)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._step()
+        self.graph = g
+        self._set_state(last_tok, cache_len)  # capture does not execute; state is as before
+        log.info(f"captured decode graph: rows={self.rows} block={self.capacity} "
+                 f"temperature={self.temperature} top_k={self.top_k}")
+
+    @torch.inference_mode()
+    def run(self, last_tok: Tensor, n_steps: int) -> Tensor:
+        """Decode ``n_steps`` tokens after ``last_tok`` [rows, 1] from the current cache; returns
+        the [rows, n_steps] new tokens (device). The cache must have room for n_steps more."""
+        cache_len = self.cache.seq_len()
+        assert 0 < cache_len and cache_len + n_steps <= self.capacity, (cache_len, n_steps, self.capacity)
+        if self.graph is None:
+            self._capture(last_tok, cache_len)
+        else:
+            self._set_state(last_tok, cache_len)
+        for _ in range(n_steps):
+            self.graph.replay()
+        self.cache._len = [cache_len + n_steps] * self.cache.num_layers
+        return self.out[:, :n_steps]
+
+
+def get_decoder(model, rows: int, block_size: int, temperature: float, top_k: int | None) -> GraphDecoder | None:
+    """Cached per model and (rows, block size, sampling settings, weights identity); None when the
+    model does not qualify (CPU, no attention, RoPE) or ``PENROZ_GRAPH_DECODE=0``."""
+    if not applicable(model):
+        return None
+    p = next(model.parameters())
+    key = (rows, block_size, float(temperature), top_k if temperature else None, kvc.TURBO_QUANT_ENABLED,
+           p.data_ptr(), p.dtype)
+    cache = model.__dict__.setdefault("_graph_decoders", {})
+    dec = cache.get(key)
+    if dec is None:
+        while len(cache) >= 2:  # bounded: each holds a KV cache and a graph memory pool
+            cache.pop(next(iter(cache)))
+        dec = GraphDecoder(model, rows, block_size, temperature, top_k)
+        cache[key] = dec
+    return dec

@@ -96,6 +96,7 @@ class PositionEmbedding(nn.Embedding):
     def __init__(self, *args, **kwargs):
         super().__init__(*args, **kwargs)
         self._position_offset = 0
+        self.position_offset_tensor: Tensor | None = None  # device int64 [1] (graph-replayed decode)
 
     @property
     def position_offset(self) -> int:
@@ -107,6 +108,10 @@ class PositionEmbedding(nn.Embedding):
 
     def forward(self, input_data: Tensor) -> Tensor:
         _, num_positions = input_data.shape
+        if self.position_offset_tensor is not None:  # offset read on the device (caller bounds it)
+            positions = self.position_offset_tensor + torch.arange(num_positions, dtype=torch.long,
+                                                                   device=input_data.device)
+            return super().forward(positions)
         if self._position_offset + num_positions > self.num_embeddings:
             raise ValueError(f"positions {self._position_offset}..{self._position_offset + num_positions} "
                              f"exceed the position table ({self.num_embeddings})")

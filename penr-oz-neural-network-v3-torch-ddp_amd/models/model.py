@@ -378,7 +378,75 @@ class NeuralNetworkModel(nn.Module):
             yield tok
         log.info("Streaming token generation completed")
 
+    def _token_bursts(self, context: Tensor, block_size: int, max_new_tokens: int, temperature, top_k,
+                      softmax_layer, burst: int):
+        """Yield [rows, k] blocks of new tokens (device). On the GPU the decode steps replay a
+        captured HIP graph (``graph_decode.py``); prefill and the sliding-window re-prefill
+        (cache full) run eagerly, exactly as the per-token path."""
+        from penroz.models import graph_decode
+        rows = context.shape[0]
+        dec = graph_decode.get_decoder(self, rows, block_size, temperature, top_k)
+        if dec is None:
+            cache, pos = self._attach_kv_cache(capacity=block_size)
+        else:
+            dec.attach()
+            cache, pos = dec.cache, dec.pos_layers
+            cache.clear()
+        try:
+            remaining = max_new_tokens
+            last = None
+            while remaining > 0:
+                n = cache.seq_len() if cache is not None else 0
+                if dec is None or n == 0 or n >= block_size:
+                    new = self._generate_next_token(context, block_size, temperature, top_k, softmax_layer, cache,
+                                                    pos)
+                    for p in pos:
+                        p.position_offset = 0
+                else:
+                    k = min(remaining, block_size - n, burst)
+                    new = dec.run(last, k)
+                context = torch.cat((context, new.to(context.device)), dim=1)
+                last = context[:, -1:]
+                remaining -= new.shape[1]
+                yield new
+        finally:
+            if cache is not None:
+                cache.log_metrics()
+            if dec is None:
+                self._detach_kv_cache(pos)
+            else:
+                dec.detach()
+
     def _generate(self, input_context, block_size, max_new_tokens, temperature, top_k, stop_token, full_context):
+        context, softmax_layer = self._prepare_generation(input_context, max_new_tokens, temperature, top_k)
+        rows = context.shape[0]
+        generated = []
+        done = torch.zeros(rows, dtype=torch.bool)
+        burst = 1 if (not full_context or stop_token is not None) else max_new_tokens
+        stopped = False
+        with torch.inference_mode():
+            for new in self._token_bursts(context, block_size, max_new_tokens, temperature, top_k, softmax_layer,
+                                          burst):
+                toks = new.tolist()
+                for j in range(new.shape[1]):
+                    col = [r[j] for r in toks]
+                    context = torch.cat((context, new[:, j:j + 1].to(context.device)), dim=1)
+                    generated.append(col[0])
+                    if not full_context:
+                        yield col[0]
+                    if stop_token is not None:
+                        done |= torch.tensor([t == stop_token for t in col])
+                        if bool(done[0]) and (rows == 1 or bool(done.all())):
+                            stopped = True
+                            break
+                if stopped:
+                    break
+        if full_context:
+            yield context[0].tolist()
+
+    def _generate_eager(self, input_context, block_size, max_new_tokens, temperature, top_k, stop_token,
+                        full_context):
+        """Per-token path (kept for A/B and as the reference-shaped loop)."""
         context, softmax_layer = self._prepare_generation(input_context, max_new_tokens, temperature, top_k)
         cache, pos = self._attach_kv_cache(capacity=block_size)
         rows = context.shape[0]
@@ -409,15 +477,14 @@ class NeuralNetworkModel(nn.Module):
                        top_k: int | None = None, stop_token: int | None = None) -> list[list[int]]:
         """All rows' contexts (the reference returns row 0 only — bug 5)."""
         context, sm = self._prepare_generation(input_context, max_new_tokens, temperature, top_k)
-        cache, pos = self._attach_kv_cache(capacity=block_size)
-        try:
-            for _ in range(max_new_tokens):
-                nxt = self._generate_next_token(context, block_size, temperature, top_k, sm, cache, pos)
-                context = torch.cat((context, nxt.to(context.device)), dim=1)
-                if stop_token is not None and bool((nxt == stop_token).all()):
+        burst = 32 if stop_token is not None else max_new_tokens
+        for new in self._token_bursts(context, block_size, max_new_tokens, temperature, top_k, sm, burst):
+            if stop_token is not None:
+                hit = (new == stop_token).all(dim=0).nonzero()
+                if hit.numel():
+                    context = torch.cat((context, new[:, :int(hit[0]) + 1].to(context.device)), dim=1)
                     break
-        finally:
-            self._detach_kv_cache(pos)
+            context = torch.cat((context, new.to(context.device)), dim=1)
         return context.tolist()
 
     # ------------------------------------------------------------------ training

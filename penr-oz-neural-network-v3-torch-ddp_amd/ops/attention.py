@@ -127,17 +127,22 @@ def reference_cache_attention(q: Tensor, k: Tensor, v: Tensor, q_offset: int) ->
 
 
 def decode_attention(q: Tensor, k_cache: Tensor, v_cache: Tensor, seq_len: int,
-                     k_scale: Tensor | None = None, v_scale: Tensor | None = None) -> Tensor:
+                     k_scale: Tensor | None = None, v_scale: Tensor | None = None,
+                     seq_len_dev: Tensor | None = None) -> Tensor:
     """Attention of ``q [B, Tq, H, D]`` against the first ``seq_len`` cache slots.
 
     Cache layout ``[B, Hkv, cap, D]`` (bf16/fp16/fp32, or int8 with per-token fp32 scales
     ``[B, Hkv, cap]`` — TurboQuant; dequantisation fused into the kernel).
-    GPU: split-K decode kernel (``csrc/kernels/decode_attn.hip``).
+    GPU: split-K decode kernel (``csrc/kernels/decode_attn.hip``). ``seq_len_dev`` (device int64
+    [1], GPU only): the kernel reads the cache length at run time (``seq_len`` is then the
+    capacity bound) — the form a captured HIP graph replays at every position.
     """
     Tq = q.shape[1]
     if use_kernels(q) and q.shape[-1] in DECODE_HEAD_DIMS:
         return kernels().decode_attn(q.contiguous(), k_cache, v_cache, k_scale, v_scale, int(seq_len),
-                                     int(seq_len - Tq), 1.0 / math.sqrt(q.shape[-1]))
+                                     int(seq_len - Tq), 1.0 / math.sqrt(q.shape[-1]), seq_len_dev)
+    if seq_len_dev is not None:
+        seq_len = int(seq_len_dev.item())
     k = k_cache[:, :, :seq_len]
     v = v_cache[:, :, :seq_len]
     if k_scale is not None:

@@ -36,14 +36,19 @@ def reference_sample(logits: Tensor, temperature: float, top_k: int | None, unif
     return idx.gather(1, choice)
 
 
-def sample(logits: Tensor, temperature: float, top_k: int | None, generator: torch.Generator | None = None) -> Tensor:
-    """logits [B, V] -> [B, 1] int64 next-token ids."""
+def sample(logits: Tensor, temperature: float, top_k: int | None, generator: torch.Generator | None = None,
+           device_rng: bool = False) -> Tensor:
+    """logits [B, V] -> [B, 1] int64 next-token ids. ``device_rng``: draw the uniforms on the
+    device (required inside a captured HIP graph; the host-drawn default matches CPU runs)."""
     B = logits.shape[0]
     if temperature == 0.0:
         if use_kernels(logits):
             return kernels().sample_tokens(logits.contiguous(), None, 0.0, 0)
         return logits.argmax(dim=-1, keepdim=True)
-    uniform = torch.rand(B, generator=generator, device="cpu").to(logits.device)
+    if device_rng:
+        uniform = torch.rand(B, device=logits.device)
+    else:
+        uniform = torch.rand(B, generator=generator, device="cpu").to(logits.device)
     if use_kernels(logits):
         k = 0 if top_k is None or top_k >= logits.shape[-1] else int(top_k)
         return kernels().sample_tokens(logits.contiguous(), uniform, float(temperature), k)
