@@ -43,6 +43,9 @@ torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c
                           c10::optional<torch::Tensor> seq_len_dev);
 // elementwise.hip (deferred.h)
 void set_deferred_reduce_stream(int64_t stream, int64_t device);
+// decode_attn.hip
+void kv_append(torch::Tensor k, torch::Tensor v, torch::Tensor kc, torch::Tensor vc, c10::optional<torch::Tensor> ks,
+               c10::optional<torch::Tensor> vs, c10::optional<torch::Tensor> pos_dev, int64_t pos);
 // gemm.hip
 void gemm_bf16(torch::Tensor a, torch::Tensor b, bool b_kn, c10::optional<torch::Tensor> bias, torch::Tensor out,
                c10::optional<torch::Tensor> act, int64_t gelu_approx, int64_t ablate);
@@ -82,6 +85,9 @@ PYBIND11_MODULE(penroz_kernels, m) {
         pybind11::arg("v_scale"), pybind11::arg("S"), pybind11::arg("q_offset"), pybind11::arg("scale"),
         pybind11::arg("seq_len_dev") = pybind11::none());
   m.def("set_deferred_reduce_stream", &set_deferred_reduce_stream);
+  m.def("kv_append", &kv_append, pybind11::arg("k"), pybind11::arg("v"), pybind11::arg("kc"), pybind11::arg("vc"),
+        pybind11::arg("ks") = pybind11::none(), pybind11::arg("vs") = pybind11::none(),
+        pybind11::arg("pos_dev") = pybind11::none(), pybind11::arg("pos") = 0);
   m.def("gemm_bf16", &gemm_bf16, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("b_kn"),
         pybind11::arg("bias") = pybind11::none(), pybind11::arg("out"), pybind11::arg("act") = pybind11::none(),
         pybind11::arg("gelu_approx") = 0, pybind11::arg("ablate") = 0);

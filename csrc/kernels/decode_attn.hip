@@ -17,6 +17,7 @@
 // and a second kernel combines them. Enough splits are used to put ≥ 512 workgroups in
 // flight (256 CUs) even at batch 1.
 #include "common.h"
+#include <type_traits>
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 
@@ -66,7 +67,8 @@ __global__ void __launch_bounds__(256) decode_kernel(const TQ* __restrict__ q, c
                                                      const float* __restrict__ vs, TQ* __restrict__ out,
                                                      float* __restrict__ ws_o, float* __restrict__ ws_ml, int B,
                                                      int Tq, int H, int Hkv, int cap, int S, int q_offset,
-                                                     int splits, float scale, const int64_t* __restrict__ S_dev) {
+                                                     int splits, float scale, const int64_t* __restrict__ S_dev,
+                                                     int64_t q_rs) {
   if (S_dev != nullptr) {  // graph-replayed decode: the cache length lives on the device
     S = (int)min<int64_t>(*S_dev, (int64_t)cap);
     q_offset = S - Tq;
@@ -88,7 +90,7 @@ __global__ void __launch_bounds__(256) decode_kernel(const TQ* __restrict__ q, c
 
   for (int i = threadIdx.x; i < G * D; i += 256) {
     const int h = g * G + i / D, d = i % D;
-    qs[i / D][d] = to_f(q[(((size_t)b * Tq + tq) * H + h) * D + d]) * scale;
+    qs[i / D][d] = to_f(q[((size_t)b * Tq + tq) * q_rs + (size_t)h * D + d]) * scale;
   }
   __syncthreads();
 
@@ -214,6 +216,41 @@ __global__ void __launch_bounds__(256) decode_combine_kernel(const float* __rest
   }
 }
 
+// Append one token's K and V rows (read straight from the fused QKV projection) into the cache
+// slot `pos` — taken from device memory when pos_dev is given (graph-replayed decode). One wave
+// per (batch, KV head, K|V) row; int8 caches quantise per token (absmax / 127, round to nearest
+// even) exactly like kv_quant_kernel.
+template <typename T, typename TK>
+__global__ void __launch_bounds__(256) kv_append_kernel(const T* __restrict__ k, const T* __restrict__ v,
+                                                        int64_t k_rs, int64_t v_rs, TK* __restrict__ kc,
+                                                        TK* __restrict__ vc, float* __restrict__ ks,
+                                                        float* __restrict__ vs, int B, int Hkv, int D, int cap,
+                                                        const int64_t* __restrict__ pos_dev, int pos_host) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);  // over B*Hkv*2
+  if (row >= B * Hkv * 2) return;
+  const int which = row & 1, bg = row >> 1;
+  const int g = bg % Hkv, b = bg / Hkv;
+  const T* src = (which ? v + (size_t)b * v_rs : k + (size_t)b * k_rs) + (size_t)g * D;
+  const int pos = pos_dev ? (int)*pos_dev : pos_host;
+  const size_t slot = ((size_t)b * Hkv + g) * cap + pos;
+  TK* dst = (which ? vc : kc) + slot * D;
+  if constexpr (std::is_same<TK, int8_t>::value) {
+    float m = 0.f;
+    for (int d = lane; d < D; d += 64) m = fmaxf(m, fabsf(to_f(src[d])));
+    m = wave_max(m);
+    float sc = m / 127.f;
+    if (sc == 0.f) sc = 1.f;
+    for (int d = lane; d < D; d += 64) {
+      float x = rintf(to_f(src[d]) / sc);
+      dst[d] = (int8_t)fminf(fmaxf(x, -128.f), 127.f);
+    }
+    if (lane == 0) (which ? vs : ks)[slot] = sc;
+  } else {
+    for (int d = lane; d < D; d += 64) dst[d] = src[d];
+  }
+}
+
 }  // namespace penroz
 
 using namespace penroz;
@@ -224,7 +261,10 @@ using namespace penroz;
 torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c10::optional<torch::Tensor> k_scale,
                           c10::optional<torch::Tensor> v_scale, int64_t S, int64_t q_offset, double scale,
                           c10::optional<torch::Tensor> seq_len_dev) {
-  TORCH_CHECK(q.is_cuda() && q.is_contiguous() && q.dim() == 4, "q must be [B, Tq, H, D]");
+  TORCH_CHECK(q.is_cuda() && q.dim() == 4, "q must be [B, Tq, H, D]");
+  // q may be a view into the fused QKV rows: unit dim stride, packed heads, uniform row stride
+  TORCH_CHECK(q.stride(3) == 1 && q.stride(2) == q.size(3) && q.stride(0) == q.size(1) * q.stride(1),
+              "q must have packed heads and a uniform row stride");
   TORCH_CHECK(kc.is_contiguous() && vc.is_contiguous() && kc.dim() == 4 && kc.sizes() == vc.sizes());
   const int B = q.size(0), Tq = q.size(1), H = q.size(2), D = q.size(3);
   const int Hkv = kc.size(1), cap = kc.size(2);
@@ -235,6 +275,7 @@ torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c
   TORCH_CHECK(!quant || (k_scale.has_value() && v_scale.has_value()), "int8 cache needs scales");
   TORCH_CHECK(quant || kc.scalar_type() == q.scalar_type(), "cache dtype must match q");
   auto out = torch::empty({B, Tq, H * D}, q.options());
+  const int64_t q_rs = q.stride(1);
   const int items = B * Hkv * Tq;
   int splits = std::max(1, std::min<int>((512 + items - 1) / items, (int)((S + 255) / 256)));
   torch::Tensor ws_o, ws_ml;
@@ -265,10 +306,10 @@ torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c
     TQ* op = reinterpret_cast<TQ*>(out.data_ptr());
     if (D == 64)
       hipLaunchKernelGGL((decode_kernel<64, TQ, TK>), grid, dim3(256), 0, stream, qp, kp, vp, ksp, vsp, op, wo, wm, B,
-                         Tq, H, Hkv, cap, (int)S, (int)q_offset, splits, (float)scale, sdev);
+                         Tq, H, Hkv, cap, (int)S, (int)q_offset, splits, (float)scale, sdev, q_rs);
     else
       hipLaunchKernelGGL((decode_kernel<128, TQ, TK>), grid, dim3(256), 0, stream, qp, kp, vp, ksp, vsp, op, wo, wm, B,
-                         Tq, H, Hkv, cap, (int)S, (int)q_offset, splits, (float)scale, sdev);
+                         Tq, H, Hkv, cap, (int)S, (int)q_offset, splits, (float)scale, sdev, q_rs);
     if (splits > 1) {
       const int rows = B * Tq * H;
       hipLaunchKernelGGL(decode_combine_kernel<TQ>, dim3(std::min(2048, (rows * D + 255) / 256)), dim3(256), 0, stream,
@@ -284,4 +325,45 @@ torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c
   else if (q.scalar_type() == torch::kFloat16) with_k(__half{});
   else TORCH_CHECK(false, "unsupported q dtype");
   return out;
+}
+
+// k, v: [B, 1, Hkv, D] (views into the fused QKV rows allowed); caches [B, Hkv, cap, D]
+void kv_append(torch::Tensor k, torch::Tensor v, torch::Tensor kc, torch::Tensor vc, c10::optional<torch::Tensor> ks,
+               c10::optional<torch::Tensor> vs, c10::optional<torch::Tensor> pos_dev, int64_t pos) {
+  TORCH_CHECK(k.is_cuda() && k.dim() == 4 && k.sizes() == v.sizes() && k.size(1) == 1, "k/v must be [B, 1, Hkv, D]");
+  TORCH_CHECK(k.stride(3) == 1 && k.stride(2) == k.size(3) && v.stride(3) == 1 && v.stride(2) == v.size(3),
+              "k/v rows must be packed");
+  const int B = k.size(0), Hkv = k.size(2), D = k.size(3);
+  TORCH_CHECK(kc.is_contiguous() && vc.is_contiguous() && kc.sizes() == vc.sizes() && kc.size(0) == B &&
+              kc.size(1) == Hkv && kc.size(3) == D, "cache shape");
+  const int cap = kc.size(2);
+  const int64_t* pd = nullptr;
+  if (pos_dev.has_value() && pos_dev->defined()) {
+    TORCH_CHECK(pos_dev->is_cuda() && pos_dev->scalar_type() == torch::kInt64 && pos_dev->numel() == 1);
+    pd = pos_dev->data_ptr<int64_t>();
+  } else {
+    TORCH_CHECK(pos >= 0 && pos < cap, "cache overflow");
+  }
+  const bool quant = kc.scalar_type() == torch::kInt8;
+  TORCH_CHECK(!quant || (ks.has_value() && vs.has_value()), "int8 cache needs scales");
+  TORCH_CHECK(quant || kc.scalar_type() == k.scalar_type(), "cache dtype must match k/v");
+  const int rows = B * Hkv * 2;
+  auto stream = at::hip::getCurrentHIPStream();
+  auto launch = [&](auto ttag, auto ktag) {
+    using T = decltype(ttag);
+    using TK = decltype(ktag);
+    hipLaunchKernelGGL((kv_append_kernel<T, TK>), dim3((rows + 3) / 4), dim3(256), 0, stream,
+                       reinterpret_cast<const T*>(k.data_ptr()), reinterpret_cast<const T*>(v.data_ptr()), k.stride(0),
+                       v.stride(0), reinterpret_cast<TK*>(kc.data_ptr()), reinterpret_cast<TK*>(vc.data_ptr()),
+                       quant ? ks->data_ptr<float>() : nullptr, quant ? vs->data_ptr<float>() : nullptr, B, Hkv, D,
+                       cap, pd, (int)pos);
+  };
+  auto with_k = [&](auto ttag) {
+    if (quant) launch(ttag, int8_t{});
+    else launch(ttag, ttag);
+  };
+  if (k.scalar_type() == torch::kBFloat16) with_k(bf16{});
+  else if (k.scalar_type() == torch::kFloat32) with_k(float{});
+  else if (k.scalar_type() == torch::kFloat16) with_k(__half{});
+  else TORCH_CHECK(false, "unsupported k dtype");
 }

@@ -12,8 +12,9 @@ feedback of the sampled token into the next step's input — is captured ONCE pe
 replayed. Everything that changes between steps lives on the device:
 
 * ``StaticKVCache.pos_t`` / ``len_t``: the slot this step writes and the cache length after it;
-  the append is an ``index_copy_`` at ``pos_t`` and the decode-attention kernel reads ``len_t``
-  at run time (``csrc/kernels/decode_attn.hip``, ``seq_len_dev``);
+  one kernel appends K/V (read in place from the fused QKV rows, int8-quantised for TurboQuant)
+  at ``pos_t`` and the decode-attention kernel reads q in place and ``len_t`` at run time
+  (``csrc/kernels/decode_attn.hip``: ``kv_append``, ``seq_len_dev``);
 * ``PositionEmbedding.position_offset_tensor``: the learned position gathered at ``pos_t``;
 * the uniforms of temperature / top-k sampling are drawn on the device (graph-safe Philox);
 * the sampled token is copied into the step's input buffer and into a burst output buffer.
@@ -32,6 +33,7 @@ import torch
 from torch import Tensor
 
 from penroz.models import kv_cache as kvc
+from penroz.ops import _ext
 from penroz.ops import attention as attn_ops
 from penroz.ops import sampling as samp_ops
 
@@ -57,18 +59,17 @@ class _GraphMode:
 
 class StaticKVCache(_GraphMode, kvc.KVCache):
     def _attend_graph(self, l: int, q: Tensor, k: Tensor, v: Tensor) -> Tensor:
+        # k, v, q are views into this layer's fused QKV rows: one kernel appends K/V at pos_t,
+        # the decode kernel reads q in place and the cache length from len_t
         kc, vc = self._k[l], self._v[l]
-        kc.index_copy_(2, self.pos_t, k.transpose(1, 2).to(kc.dtype))
-        vc.index_copy_(2, self.pos_t, v.transpose(1, 2).to(vc.dtype))
+        _ext.kernels().kv_append(k, v, kc, vc, None, None, self.pos_t, 0)
         return attn_ops.decode_attention(q, kc, vc, kc.shape[2], seq_len_dev=self.len_t)
 
 
 class StaticTurboKVCache(_GraphMode, kvc.TurboQuantKVCache):
     def _attend_graph(self, l: int, q: Tensor, k: Tensor, v: Tensor) -> Tensor:
-        for x, store, scales in ((k, self._k, self._sk), (v, self._v, self._sv)):
-            qx, sx = samp_ops.reference_quantize(x.float().transpose(1, 2))  # [B,Hkv,1,D], [B,Hkv,1,1]
-            store[l].index_copy_(2, self.pos_t, qx)
-            scales[l].index_copy_(2, self.pos_t, sx.squeeze(-1))
+        # same per-token int8 quantiser as the eager append (kv_quantize)
+        _ext.kernels().kv_append(k, v, self._k[l], self._v[l], self._sk[l], self._sv[l], self.pos_t, 0)
         self._dtype[l] = k.dtype
         return attn_ops.decode_attention(q, self._k[l], self._v[l], self._k[l].shape[2], self._sk[l], self._sv[l],
                                          seq_len_dev=self.len_t)
@@ -181,8 +182,11 @@ def get_decoder(model, rows: int, block_size: int, temperature: float, top_k: in
     if not applicable(model):
         return None
     p = next(model.parameters())
+    # weights identity AND version: in-place updates (training) re-capture, so nothing captured
+    # (e.g. LayerNorm's cached fp32 weight copies for bf16 models) can go stale
+    version = sum(q._version for q in model.parameters())
     key = (rows, block_size, float(temperature), top_k if temperature else None, kvc.TURBO_QUANT_ENABLED,
-           p.data_ptr(), p.dtype)
+           p.data_ptr(), p.dtype, version)
     cache = model.__dict__.setdefault("_graph_decoders", {})
     dec = cache.get(key)
     if dec is None:

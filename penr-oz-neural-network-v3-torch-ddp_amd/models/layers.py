@@ -154,8 +154,21 @@ class LayerNorm(nn.LayerNorm):
 
     def forward(self, x: Tensor) -> Tensor:
         if len(self.normalized_shape) == 1 and self.elementwise_affine:
-            return norm_ops.layer_norm(x, self.weight, self.bias, self.eps)
+            w, b = self.weight, self.bias
+            if w.dtype != torch.float32 and b is not None and not torch.is_grad_enabled():
+                w, b = self._fp32_affine()  # inference on bf16 weights: no per-call casts
+            return norm_ops.layer_norm(x, w, b, self.eps)
         return super().forward(x)
+
+    def _fp32_affine(self):
+        """fp32 copies of (weight, bias) — the kernel's parameter dtype — cached until the
+        parameters change (storage or in-place version)."""
+        key = (self.weight.data_ptr(), self.weight._version, self.bias.data_ptr(), self.bias._version)
+        c = self.__dict__.get("_fp32_cache")
+        if c is None or c[0] != key:
+            c = (key, self.weight.detach().float(), self.bias.detach().float())
+            self.__dict__["_fp32_cache"] = c
+        return c[1], c[2]
 
 
 class GELU(nn.GELU):
