@@ -3,17 +3,17 @@
 //
 // Work item = (batch b, KV head g, query row tq, split s). One 256-thread workgroup owns all
 // H/Hkv query heads that share KV head g (GQA by index math — the cache is never expanded),
-// so each K/V row is loaded once for the whole group. The keys of a split are dealt to the
-// 4 waves in 64-key blocks:
-//   scores : lane j holds key (blk + j); its K row is read as 16-B vectors and dotted with the
-//            group's query vectors (staged in LDS, fp32);
-//   softmax: running (m, l) per query head, wave-wide max/sum, causal mask by absolute
-//            position (query tq sits at q_offset + tq);
-//   PV     : lane d owns output column d (and d+64 for D=128); V row j is read coalesced and
-//            p_j is broadcast with a lane shuffle.
+// so each K/V row is loaded once for the whole group. Keys go in chunks of up to 256 (one key
+// per thread, or 1/2, 1/4 of one for wide rows), so a whole chunk's K and V reads are in
+// flight together — a decode step's cache is short (S ~ 100s) and the kernel is latency-bound:
+//   scores : thread = key; its K row is read as 16-B vectors and dotted with the group's query
+//            vectors (LDS, fp32); V row pieces go raw to an XOR-swizzled LDS tile;
+//   softmax: online (m, l) per query head across chunks, block max/sum through LDS, causal
+//            mask by absolute position (query tq sits at q_offset + tq);
+//   PV     : thread = 2 output columns × every NG-th key of the chunk, from LDS.
 // int8 caches (TurboQuant) carry per-token fp32 scales that are folded into the score and
 // the P·V weight, so the int8 cache is never dequantised to memory.
-// The 4 waves merge through LDS; with several splits the partial (m, l, O) go to a workspace
+// The key groups merge through LDS; with several splits the partial (m, l, O) go to a workspace
 // and a second kernel combines them. Enough splits are used to put ≥ 512 workgroups in
 // flight (256 CUs) even at batch 1.
 #include "common.h"
@@ -61,7 +61,35 @@ template <> struct Row8<int8_t> {
   }
 };
 
-template <int D, typename TQ, typename TK>
+// raw 16-B pieces live in ext-vector registers (HIP's uint4 struct defeats register promotion
+// of an array that is carried across the chunk loop: it went to scratch)
+typedef uint32_t dec_u32x4 __attribute__((ext_vector_type(4)));
+
+// 16 raw cache bytes -> fp32 (8 bf16/fp16, 4 fp32 or 16 int8 values)
+template <typename TK> struct Piece {
+  static constexpr int N = 16 / (int)sizeof(TK);
+  __device__ __forceinline__ static void cvt(const dec_u32x4 u, float (&v)[N]) {
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if constexpr (std::is_same<TK, bf16>::value) {
+        v[2 * i] = __uint_as_float(w[i] << 16);
+        v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+      } else if constexpr (std::is_same<TK, __half>::value) {
+        v[2 * i] = __half2float(__ushort_as_half((unsigned short)(w[i] & 0xffff)));
+        v[2 * i + 1] = __half2float(__ushort_as_half((unsigned short)(w[i] >> 16)));
+      } else if constexpr (std::is_same<TK, float>::value) {
+        v[i] = __uint_as_float(w[i]);
+      } else {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) v[4 * i + b] = (float)(int8_t)((w[i] >> (8 * b)) & 0xff);
+      }
+    }
+  }
+};
+
+// GC: the exact query-group size H/Hkv (1, 4, 8: branch-free loops), or 0 = any size <= 16
+template <int D, int GC, typename TQ, typename TK>
 __global__ void __launch_bounds__(256) decode_kernel(const TQ* __restrict__ q, const TK* __restrict__ kc,
                                                      const TK* __restrict__ vc, const float* __restrict__ ks,
                                                      const float* __restrict__ vs, TQ* __restrict__ out,
@@ -69,12 +97,20 @@ __global__ void __launch_bounds__(256) decode_kernel(const TQ* __restrict__ q, c
                                                      int Tq, int H, int Hkv, int cap, int S, int q_offset,
                                                      int splits, float scale, const int64_t* __restrict__ S_dev,
                                                      int64_t q_rs) {
-  if (S_dev != nullptr) {  // graph-replayed decode: the cache length lives on the device
-    S = (int)min<int64_t>(*S_dev, (int64_t)cap);
-    q_offset = S - Tq;
-  }
-  constexpr int DL = D / 64;  // output columns per lane
-  const int G = H / Hkv;
+  constexpr int GMAX = GC ? GC : kMaxGroup;
+  constexpr int RB = D * (int)sizeof(TK);                 // cache row bytes
+  constexpr int KC = RB * 256 <= 32768 ? 256 : 32768 / RB;  // keys per chunk (V chunk <= 32 KB of LDS)
+  constexpr int TPK = 256 / KC;                           // threads per key in the score phase
+  constexpr int CR = RB / 16;                             // 16-B pieces per row
+  constexpr int CPT = CR / TPK;                           // 16-B pieces of K (and of V) per thread
+  constexpr int PN = Piece<TK>::N;                        // values per piece
+  constexpr int SW = (CR < 8 ? CR : 8) - 1;               // LDS row swizzle mask (pieces)
+  constexpr int NP = D / 2, NG = 256 / NP;                // P·V: column pairs × key groups
+  constexpr int VBUF = KC * RB > NG * GMAX * D * 4 ? KC * RB : NG * GMAX * D * 4;
+  constexpr int QPT = (GMAX * D + 255) / 256;             // query values staged per thread
+  static_assert(CPT >= 1 && NG * NP == 256, "decode tiling");
+
+  const int G = GC ? GC : H / Hkv;
   int wid_lin = blockIdx.x;
   const int split = wid_lin % splits;
   wid_lin /= splits;
@@ -82,113 +118,177 @@ __global__ void __launch_bounds__(256) decode_kernel(const TQ* __restrict__ q, c
   wid_lin /= Tq;
   const int g = wid_lin % Hkv;
   const int b = wid_lin / Hkv;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
 
-  __shared__ float qs[kMaxGroup][D];
-  __shared__ float red_m[4][kMaxGroup], red_l[4][kMaxGroup];
-  __shared__ float red_o[4][kMaxGroup][D];
+  __shared__ __attribute__((aligned(16))) char vbuf[VBUF];  // V chunk, later the P·V partials
+  __shared__ float qs[GMAX][D];
+  __shared__ float pl[GMAX][KC];
+  __shared__ float red_m[4][GMAX], red_l[4][GMAX];
+  __shared__ float fin[GMAX][2];
 
-  for (int i = threadIdx.x; i < G * D; i += 256) {
-    const int h = g * G + i / D, d = i % D;
-    qs[i / D][d] = to_f(q[((size_t)b * Tq + tq) * q_rs + (size_t)h * D + d]) * scale;
+  // the query group's reads go out first (the LDS write below then waits for them only)
+  float qv[QPT];
+#pragma unroll
+  for (int r = 0; r < QPT; ++r) {
+    const int i = t + 256 * r;
+    qv[r] = i < G * D ? to_f(q[((size_t)b * Tq + tq) * q_rs + (size_t)(g * G + i / D) * D + i % D]) : 0.f;
   }
-  __syncthreads();
-
+  if (S_dev != nullptr) {  // graph-replayed decode: the cache length lives on the device
+    S = (int)min<int64_t>(*S_dev, (int64_t)cap);
+    q_offset = S - Tq;
+  }
   const int kend_causal = min(S, q_offset + tq + 1);
   const int per_split = (kend_causal + splits - 1) / splits;
   const int k0 = split * per_split, k1 = min(kend_causal, k0 + per_split);
   const size_t head_base = ((size_t)b * Hkv + g) * cap;
+  const int kk = t / TPK, part = t % TPK;     // score phase: key kk of the chunk, pieces part*CPT..
+  const int kg = t / NP, d0 = 2 * (t % NP);   // P·V phase: columns d0, d0+1 over keys kg, kg+NG, ..
 
-  float m[kMaxGroup], l[kMaxGroup], o[kMaxGroup][DL];
+  // one key (or 1/TPK of it) per thread: a whole chunk's K and V reads are in flight at once
+  // (kept raw in registers, converted at use), and the next chunk's are issued before this
+  // chunk's P·V. V goes raw to LDS (16-B pieces XOR-swizzled by row: conflict-free both ways).
+  dec_u32x4 kr[CPT], vr[CPT];
+  float ksc = 1.f, vsc = 1.f;
+  auto load_chunk = [&](int c0) {
+    const int key = c0 + kk;
+    const size_t row = head_base + (key < k1 ? key : c0);
+    const char* ksrc = reinterpret_cast<const char*>(kc + row * D) + part * CPT * 16;
+    const char* vsrc = reinterpret_cast<const char*>(vc + row * D) + part * CPT * 16;
 #pragma unroll
-  for (int i = 0; i < kMaxGroup; ++i) {
-    m[i] = -INFINITY;
-    l[i] = 0.f;
+    for (int c = 0; c < CPT; ++c) kr[c] = *reinterpret_cast<const dec_u32x4*>(ksrc + 16 * c);
 #pragma unroll
-    for (int j = 0; j < DL; ++j) o[i][j] = 0.f;
-  }
-
-  for (int blk = k0 + 64 * wid; blk < k1; blk += 256) {
-    const int key = blk + lane;
-    const bool valid = key < k1;
-    float kv[D];
-    const TK* krow = kc + (head_base + (valid ? key : k0)) * D;
+    for (int c = 0; c < CPT; ++c) vr[c] = *reinterpret_cast<const dec_u32x4*>(vsrc + 16 * c);
+    if (ks) ksc = ks[row];
+    if (vs) vsc = vs[row];
+  };
+  if (k0 < k1) load_chunk(k0);
 #pragma unroll
-    for (int c = 0; c < D / 8; ++c) {  // whole K row in flight: D/8 vector loads
-      float t[8];
-      Row8<TK>::load(krow + 8 * c, t);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) kv[8 * c + e] = t[e];
-    }
-    const float kscale = ks ? ks[head_base + (valid ? key : k0)] : 1.f;
-    float p[kMaxGroup];
-#pragma unroll
-    for (int i = 0; i < kMaxGroup; ++i) {
-      if (i >= G) break;
-      float s = 0.f;
-#pragma unroll
-      for (int d = 0; d < D; ++d) s += qs[i][d] * kv[d];
-      s = valid ? s * kscale : -INFINITY;
-      const float mn = fmaxf(m[i], wave_max(s));
-      const float alpha = __expf(m[i] - mn);
-      p[i] = valid ? __expf(s - mn) : 0.f;
-      l[i] = l[i] * alpha + wave_sum(p[i]);
-      m[i] = mn;
-#pragma unroll
-      for (int j = 0; j < DL; ++j) o[i][j] *= alpha;
-    }
-    // P·V: lane d owns output column(s) d; V rows are read coalesced, 16 rows in flight per
-    // batch (a one-row-at-a-time loop serialises on the load latency: ~70 µs per call at S=128)
-    const int nk = min(64, k1 - blk);
-    for (int j0 = 0; j0 < nk; j0 += 16) {
-      float vv[16][DL];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int j = min(j0 + r, nk - 1);
-        const TK* vrow = vc + (head_base + blk + j) * D;
-        const float vsc = vs ? vs[head_base + blk + j] : 1.f;
-#pragma unroll
-        for (int jj = 0; jj < DL; ++jj) vv[r][jj] = KRow<TK>::at(vrow, lane + 64 * jj) * vsc;
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        if (j0 + r >= nk) break;
-#pragma unroll
-        for (int i = 0; i < kMaxGroup; ++i) {
-          if (i >= G) break;
-          const float pj = __shfl(p[i], j0 + r, 64);
-#pragma unroll
-          for (int jj = 0; jj < DL; ++jj) o[i][jj] += pj * vv[r][jj];
-        }
-      }
-    }
-  }
-  // merge the 4 waves
-  for (int i = 0; i < G; ++i) {
-    if (lane == 0) { red_m[wid][i] = m[i]; red_l[wid][i] = l[i]; }
-#pragma unroll
-    for (int jj = 0; jj < DL; ++jj) red_o[wid][i][lane + 64 * jj] = o[i][jj];
+  for (int r = 0; r < QPT; ++r) {
+    const int i = t + 256 * r;
+    if (i < G * D) qs[i / D][i % D] = qv[r] * scale;
   }
   __syncthreads();
-  for (int idx = threadIdx.x; idx < G * D; idx += 256) {
-    const int i = idx / D, d = idx % D;
-    float M = -INFINITY;
-    for (int w = 0; w < 4; ++w) M = fmaxf(M, red_m[w][i]);
-    float L = 0.f, O = 0.f;
-    for (int w = 0; w < 4; ++w) {
-      const float f = red_m[w][i] == -INFINITY ? 0.f : __expf(red_m[w][i] - M);
-      L += red_l[w][i] * f;
-      O += red_o[w][i][d] * f;
+
+  float M[GMAX], L[GMAX], o[GMAX][2], s[GMAX];
+#pragma unroll
+  for (int i = 0; i < GMAX; ++i) {
+    M[i] = -INFINITY;
+    L[i] = 0.f;
+    o[i][0] = o[i][1] = 0.f;
+  }
+
+  for (int c0 = k0; c0 < k1; c0 += KC) {
+    const bool valid = c0 + kk < k1;
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      const int pc = part * CPT + c;
+      *reinterpret_cast<dec_u32x4*>(vbuf + kk * RB + ((pc ^ (kk & SW)) << 4)) = vr[c];
     }
+    // scores and the chunk max per query head
+#pragma unroll
+    for (int i = 0; i < GMAX; ++i) {
+      if (!GC && i >= G) break;
+      float a = 0.f;
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) {
+        float kv[PN];
+        Piece<TK>::cvt(kr[c], kv);
+#pragma unroll
+        for (int e = 0; e < PN; ++e) a += qs[i][(part * CPT + c) * PN + e] * kv[e];
+      }
+#pragma unroll
+      for (int x = 1; x < TPK; x <<= 1) a += __shfl_xor(a, x, 64);
+      s[i] = valid ? a * ksc : -INFINITY;
+      const float wm = wave_max(s[i]);
+      if (lane == 0) red_m[wid][i] = wm;
+    }
+    const float vsc_c = vsc;
+    __syncthreads();
+    // online softmax: p (with the V scale folded in) to LDS, chunk sums
+#pragma unroll
+    for (int i = 0; i < GMAX; ++i) {
+      if (!GC && i >= G) break;
+      const float cm = fmaxf(fmaxf(red_m[0][i], red_m[1][i]), fmaxf(red_m[2][i], red_m[3][i]));
+      const float mn = fmaxf(M[i], cm);
+      const float alpha = M[i] == -INFINITY ? 0.f : __expf(M[i] - mn);
+      const float p = valid ? __expf(s[i] - mn) : 0.f;
+      if (part == 0) pl[i][kk] = p * vsc_c;
+      const float ws = wave_sum(part == 0 ? p : 0.f);
+      if (lane == 0) red_l[wid][i] = ws;
+      M[i] = mn;
+      s[i] = alpha;
+    }
+    if (c0 + KC < k1) load_chunk(c0 + KC);  // prefetch: lands while this chunk's P·V runs
+    __syncthreads();
+    const int nv = min(KC, k1 - c0);
+#pragma unroll
+    for (int i = 0; i < GMAX; ++i) {
+      if (!GC && i >= G) break;
+      L[i] = L[i] * s[i] + (red_l[0][i] + red_l[1][i]) + (red_l[2][i] + red_l[3][i]);
+      o[i][0] *= s[i];
+      o[i][1] *= s[i];
+    }
+    // P·V from LDS: thread owns columns d0, d0+1 and keys kg, kg+NG, ...
+    constexpr int ES = (int)sizeof(TK);
+    const int bo = d0 * ES;
+#pragma unroll 8
+    for (int j = kg; j < nv; j += NG) {
+      const char* vp = vbuf + j * RB + ((((bo >> 4) ^ (j & SW))) << 4) + (bo & 15);
+      float v0, v1;
+      if constexpr (std::is_same<TK, bf16>::value) {
+        const uint32_t w = *reinterpret_cast<const uint32_t*>(vp);
+        v0 = __uint_as_float(w << 16);
+        v1 = __uint_as_float(w & 0xffff0000u);
+      } else if constexpr (std::is_same<TK, __half>::value) {
+        const __half2 h2 = *reinterpret_cast<const __half2*>(vp);
+        v0 = __low2float(h2);
+        v1 = __high2float(h2);
+      } else if constexpr (std::is_same<TK, float>::value) {
+        const float2 f2 = *reinterpret_cast<const float2*>(vp);
+        v0 = f2.x;
+        v1 = f2.y;
+      } else {
+        const uint16_t w = *reinterpret_cast<const uint16_t*>(vp);
+        v0 = (float)(int8_t)(w & 0xff);
+        v1 = (float)(int8_t)(w >> 8);
+      }
+#pragma unroll
+      for (int i = 0; i < GMAX; ++i) {
+        if (!GC && i >= G) break;
+        const float pw = pl[i][j];
+        o[i][0] += pw * v0;
+        o[i][1] += pw * v1;
+      }
+    }
+    __syncthreads();
+  }
+  // merge the NG key groups (partials reuse the V buffer)
+  float* ro = reinterpret_cast<float*>(vbuf);
+#pragma unroll
+  for (int i = 0; i < GMAX; ++i) {
+    if (!GC && i >= G) break;
+    *reinterpret_cast<float2*>(ro + (kg * GMAX + i) * D + d0) = make_float2(o[i][0], o[i][1]);
+    if (t == 0) {
+      fin[i][0] = M[i];
+      fin[i][1] = L[i];
+    }
+  }
+  __syncthreads();
+  for (int idx = t; idx < G * D; idx += 256) {
+    const int i = idx / D, d = idx % D;
+    float O = 0.f;
+#pragma unroll
+    for (int x = 0; x < NG; ++x) O += ro[(x * GMAX + i) * D + d];
+    const float Mi = fin[i][0], Li = fin[i][1];
     const int h = g * G + i;
     if (splits == 1) {
-      out[(((size_t)b * Tq + tq) * H + h) * D + d] = from_f<TQ>(L > 0.f ? O / L : 0.f);
+      out[(((size_t)b * Tq + tq) * H + h) * D + d] = from_f<TQ>(Li > 0.f ? O / Li : 0.f);
     } else {
       const size_t r = (((size_t)split * B + b) * Tq + tq) * H + h;
       ws_o[r * D + d] = O;
       if (d == 0) {
-        ws_ml[2 * r] = M;
-        ws_ml[2 * r + 1] = L;
+        ws_ml[2 * r] = Mi;
+        ws_ml[2 * r + 1] = Li;
       }
     }
   }
@@ -304,12 +404,21 @@ torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c
     const TK* kp = reinterpret_cast<const TK*>(kc.data_ptr());
     const TK* vp = reinterpret_cast<const TK*>(vc.data_ptr());
     TQ* op = reinterpret_cast<TQ*>(out.data_ptr());
-    if (D == 64)
-      hipLaunchKernelGGL((decode_kernel<64, TQ, TK>), grid, dim3(256), 0, stream, qp, kp, vp, ksp, vsp, op, wo, wm, B,
-                         Tq, H, Hkv, cap, (int)S, (int)q_offset, splits, (float)scale, sdev, q_rs);
-    else
-      hipLaunchKernelGGL((decode_kernel<128, TQ, TK>), grid, dim3(256), 0, stream, qp, kp, vp, ksp, vsp, op, wo, wm, B,
-                         Tq, H, Hkv, cap, (int)S, (int)q_offset, splits, (float)scale, sdev, q_rs);
+    const int G = H / Hkv;
+#define PENROZ_DECODE(DD, GC)                                                                                   \
+  hipLaunchKernelGGL((decode_kernel<DD, GC, TQ, TK>), grid, dim3(256), 0, stream, qp, kp, vp, ksp, vsp, op, wo, wm, \
+                     B, Tq, H, Hkv, cap, (int)S, (int)q_offset, splits, (float)scale, sdev, q_rs)
+#define PENROZ_DECODE_G(DD)              \
+  switch (G) {                           \
+    case 1: PENROZ_DECODE(DD, 1); break; \
+    case 4: PENROZ_DECODE(DD, 4); break; \
+    case 8: PENROZ_DECODE(DD, 8); break; \
+    default: PENROZ_DECODE(DD, 0);       \
+  }
+    if (D == 64) PENROZ_DECODE_G(64)
+    else PENROZ_DECODE_G(128)
+#undef PENROZ_DECODE_G
+#undef PENROZ_DECODE
     if (splits > 1) {
       const int rows = B * Tq * H;
       hipLaunchKernelGGL(decode_combine_kernel<TQ>, dim3(std::min(2048, (rows * D + 255) / 256)), dim3(256), 0, stream,

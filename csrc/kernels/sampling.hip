@@ -6,6 +6,7 @@
 //   uniform u: thread-major order (thread t owns elements t, t+1024, …), one block scan of
 //   the per-thread sums finds the owning thread, which walks its own elements.
 // The whole decision stays on the device (no sort, no host round trip per token).
+// sample_reg_kernel (default for V % 8 == 0, V <= 64 Ki) keeps the row in registers.
 #include "common.h"
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
@@ -19,12 +20,46 @@ __device__ __forceinline__ uint32_t order_key(float f) {
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
+// Radix-select digit pick over a 256-bin histogram, in parallel (a serial scan of the bins by
+// one thread costs ~10 µs per pass in LDS latency): threads t < 256 scan the bins from the top
+// (d = 255 - t) and the one bin d with S(d+1) < kk <= S(d), S(d) = Σ_{b≥d} bins[b], records the
+// digit (d = 0 when fewer than kk keys remain). Every thread of the block must call it; the
+// caller synchronises before (bins complete) and after (selection visible).
+__device__ __forceinline__ void pick_digit(const uint32_t* bins, uint32_t* wtot, int shift, uint32_t pre,
+                                           uint32_t msk, int kk, uint32_t* sel_prefix, uint32_t* sel_mask,
+                                           int* sel_k) {
+  const int t = threadIdx.x, lane = t & 63;
+  uint32_t c = 0, incl = 0;
+  if (t < 256) {
+    c = bins[255 - t];
+    incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t n = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += n;
+    }
+    if (lane == 63) wtot[t >> 6] = incl;
+  }
+  __syncthreads();
+  if (t < 256) {
+    for (int i = 0; i < (t >> 6); ++i) incl += wtot[i];
+    const int d = 255 - t;
+    const uint32_t above = incl - c;
+    if ((int)above < kk && ((int)incl >= kk || d == 0)) {
+      *sel_k = kk - (int)above;
+      *sel_prefix = pre | ((uint32_t)d << shift);
+      *sel_mask = msk | (255u << shift);
+    }
+  }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(kST) sample_kernel(const T* __restrict__ logits, const float* __restrict__ uni,
                                                      int64_t* __restrict__ out, int V, float temperature, int top_k) {
   __shared__ float fred[kST / 64];
   __shared__ int ired[kST / 64];
   __shared__ uint32_t hist[256];
+  __shared__ uint32_t wtot[4];
   __shared__ float scan[kST];
   __shared__ uint32_t sel_prefix, sel_mask;
   __shared__ int sel_k;
@@ -70,22 +105,13 @@ __global__ void __launch_bounds__(kST) sample_kernel(const T* __restrict__ logit
       for (int b = t; b < 256; b += kST) hist[b] = 0;
       __syncthreads();
       const uint32_t pre = sel_prefix, msk = sel_mask;
+      const int kk = sel_k;
       for (int i = t; i < V; i += kST) {
         const uint32_t k = order_key(to_f(lp[i]));
         if ((k & msk) == pre) atomicAdd(&hist[(k >> shift) & 255u], 1u);
       }
       __syncthreads();
-      if (t == 0) {
-        int kk = sel_k;
-        int d = 255;
-        for (; d > 0; --d) {
-          if ((int)hist[d] >= kk) break;
-          kk -= hist[d];
-        }
-        sel_k = kk;
-        sel_prefix = pre | ((uint32_t)d << shift);
-        sel_mask = msk | (255u << shift);
-      }
+      pick_digit(hist, wtot, shift, pre, msk, kk, &sel_prefix, &sel_mask, &sel_k);
       __syncthreads();
     }
     thr = sel_prefix;
@@ -127,6 +153,193 @@ __global__ void __launch_bounds__(kST) sample_kernel(const T* __restrict__ logit
   if (t == 0) out[row] = result;
 }
 
+// Register-resident variant (V % 8 == 0, V <= 8·1024·CPT): the row is read from memory ONCE
+// (8 elements per 16-B chunk, chunk k of thread t covers elements 8·(t + 512·k)), then argmax,
+// the four radix passes, the softmax sums and the draw all run on registers. The radix
+// histograms are lane-private ([bin][32] copies, lanes l and l+32 share one): the first pass
+// puts almost every logit into one or two bins (sign + exponent bits), and a single shared
+// histogram then serialises tens of thousands of LDS atomics on one address.
+constexpr int kRT = 512;  // 256 VGPRs per thread: room for a 104-logit slice
+
+template <int CPT, typename T>
+__global__ void __launch_bounds__(kRT) sample_reg_kernel(const T* __restrict__ logits, const float* __restrict__ uni,
+                                                         int64_t* __restrict__ out, int V, float temperature,
+                                                         int top_k) {
+  __shared__ uint32_t hist[256 * 32];
+  __shared__ uint32_t bins[256];
+  __shared__ uint32_t wtot[4];
+  __shared__ float fred[kRT / 64];
+  __shared__ int ired[kRT / 64];
+  __shared__ float wsum[kRT / 64];
+  __shared__ uint32_t sel_prefix, sel_mask;
+  __shared__ int sel_k;
+  __shared__ float total_s;
+  __shared__ int64_t result;
+  const int row = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const T* lp = logits + (size_t)row * V;
+  // the 16-B chunks stay packed (bf16: 4 VGPRs per 8 logits) and are widened on use, so a
+  // 104-logit slice per thread (GPT-2's padded 50304 vocab) fits next to the histogram / scan state without spilling
+  constexpr int H = (int)sizeof(T) / 2;
+  uint4 raw[CPT][H];
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    const int c = 8 * (t + kRT * k);
+#pragma unroll
+    for (int h = 0; h < H; ++h)
+      raw[k][h] = c < V ? *reinterpret_cast<const uint4*>(lp + c + 4 * h)
+                        : make_uint4(0xff80ff80u, 0xff80ff80u, 0xff80ff80u, 0xff80ff80u);  // masked by i < V
+  }
+  auto val = [&](int k, int j) -> float {
+    if constexpr (H == 1) {
+      const uint4 r = raw[k][0];
+      const int q = j >> 1;
+      const uint32_t x = q == 0 ? r.x : q == 1 ? r.y : q == 2 ? r.z : r.w;
+      return __uint_as_float((j & 1) ? (x & 0xffff0000u) : (x << 16));
+    } else {
+      const uint4 r = raw[k][j >> 2];
+      const int q = j & 3;
+      const uint32_t x = q == 0 ? r.x : q == 1 ? r.y : q == 2 ? r.z : r.w;
+      return __uint_as_float(x);
+    }
+  };
+  // each pass re-widens from the packed registers: without this barrier the compiler hoists the
+  // widened values / order keys out of the radix loop and keeps them all live (spills)
+  auto opaque = [&]() {
+#pragma unroll
+    for (int k = 0; k < CPT; ++k)
+#pragma unroll
+      for (int h = 0; h < H; ++h) asm volatile("" : "+v"(raw[k][h].x), "+v"(raw[k][h].y), "+v"(raw[k][h].z), "+v"(raw[k][h].w));
+  };
+  // ---- argmax (first index on ties, like torch.argmax)
+  float bm = -INFINITY;
+  int bi = 0x7fffffff;
+#pragma unroll
+  for (int k = 0; k < CPT; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = 8 * (t + kRT * k) + j;
+      const float x = val(k, j);
+      if (i < V && x > bm) { bm = x; bi = i; }
+    }
+  const uint32_t tkey = order_key(bm);  // this thread's max (order key of -inf when empty)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(bm, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (om > bm || (om == bm && oi < bi)) { bm = om; bi = oi; }
+  }
+  if (lane == 0) { fred[w] = bm; ired[w] = bi; }
+  __syncthreads();
+  if (t == 0) {
+    float m = fred[0];
+    int ix = ired[0];
+    for (int i = 1; i < kRT / 64; ++i)
+      if (fred[i] > m || (fred[i] == m && ired[i] < ix)) { m = fred[i]; ix = ired[i]; }
+    result = ix;
+    fred[0] = m;
+  }
+  __syncthreads();
+  const float gmax = fred[0];
+  if (temperature == 0.f) {
+    if (t == 0) out[row] = result;
+    return;
+  }
+  // ---- top-k threshold: radix select over order-preserving keys (4 × 8-bit digits). Counting
+  // every logit costs 4·V LDS atomics, and those that hit one bin serialise (~80 µs per 50 K
+  // row), so the select runs twice over small sets instead: (1) over the 512 per-thread maxima,
+  // whose k-th largest L is a lower bound of the row's k-th largest (k maxima, k elements ≥ L),
+  // then (2) over the elements ≥ L only — typically barely more than k of them.
+  auto radix_select = [&](auto&& visit, int kk0) -> uint32_t {
+    if (t == 0) { sel_prefix = 0; sel_mask = 0; sel_k = kk0; }
+    for (int shift = 24; shift >= 0; shift -= 8) {
+      for (int i = t; i < 256 * 32; i += kRT) hist[i] = 0;
+      __syncthreads();
+      const uint32_t pre = sel_prefix, msk = sel_mask;
+      const int kk = sel_k;
+      opaque();
+      visit([&](uint32_t key) {
+        if ((key & msk) == pre) atomicAdd(&hist[((key >> shift) & 255u) * 32 + (lane & 31)], 1u);
+      });
+      __syncthreads();
+      if (t < 256) {  // rotated reads: the 32 copies of bin t sit on 32 banks
+        uint32_t c = 0;
+        for (int i = 0; i < 32; ++i) c += hist[t * 32 + ((i + t) & 31)];
+        bins[t] = c;
+      }
+      __syncthreads();
+      pick_digit(bins, wtot, shift, pre, msk, kk, &sel_prefix, &sel_mask, &sel_k);
+      __syncthreads();
+    }
+    return sel_prefix;
+  };
+  uint32_t thr = 0;
+  if (top_k > 0 && top_k < V) {
+    uint32_t lo = 0;
+    if (top_k <= kRT) lo = radix_select([&](auto&& add) { add(tkey); }, top_k);
+    thr = radix_select([&](auto&& add) {
+#pragma unroll
+      for (int k = 0; k < CPT; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t key = order_key(val(k, j));
+          if (8 * (t + kRT * k) + j < V && key >= lo) add(key);
+        }
+    }, top_k);
+  }
+  // ---- unnormalised softmax weights of the kept set; block scan of per-thread sums
+  const float invT = 1.f / temperature;
+  const float m = gmax * invT;
+  float s = 0.f;
+  opaque();
+#pragma unroll
+  for (int k = 0; k < CPT; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float x = val(k, j);
+      if (8 * (t + kRT * k) + j < V && (thr == 0 || order_key(x) >= thr)) s += __expf(x * invT - m);
+    }
+  float incl = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float n = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += n;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  if (t == 0) {
+    float run = 0.f;
+    for (int i = 0; i < kRT / 64; ++i) {
+      const float x = wsum[i];
+      wsum[i] = run;
+      run += x;
+    }
+    total_s = run;
+  }
+  __syncthreads();
+  const float before = wsum[w] + incl - s;
+  const float target = uni[row] * total_s;
+  if (s > 0.f && target >= before && target < before + s) {
+    float acc = before;
+    int pick = -1;
+    bool done = false;
+    opaque();
+#pragma unroll
+    for (int k = 0; k < CPT; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = 8 * (t + kRT * k) + j;
+        const float x = val(k, j);
+        if (done || i >= V || (thr != 0 && order_key(x) < thr)) continue;
+        acc += __expf(x * invT - m);
+        pick = i;
+        if (acc > target) done = true;
+      }
+    if (pick >= 0) result = pick;
+  }
+  __syncthreads();
+  if (t == 0) out[row] = result;
+}
+
 }  // namespace penroz
 
 using namespace penroz;
@@ -141,6 +354,34 @@ torch::Tensor sample_tokens(torch::Tensor logits, c10::optional<torch::Tensor> u
   else u = torch::zeros({B}, logits.options().dtype(torch::kFloat32));
   TORCH_CHECK(u.numel() == B && u.is_cuda());
   auto stream = at::hip::getCurrentHIPStream();
+  int chunks = (V / 8 + kRT - 1) / kRT;
+  for (int c : {1, 2, 3, 4, 6, 8, 10, 13, 16})  // instantiated slice sizes
+    if (chunks <= c) { chunks = c; break; }
+  const bool fits = chunks <= (logits.scalar_type() == torch::kBFloat16 ? 16 : 8);
+  if (V % 8 == 0 && fits && logits.scalar_type() != torch::kFloat16) {
+    auto launch = [&](auto tag) {
+      using T = decltype(tag);
+      const T* lp = reinterpret_cast<const T*>(logits.data_ptr());
+      float* up = u.data_ptr<float>();
+      int64_t* op = out.data_ptr<int64_t>();
+      const float tt = (float)temperature;
+      const int kk = (int)top_k;
+#define PENROZ_SAMPLE_REG(C) \
+  case C: hipLaunchKernelGGL((sample_reg_kernel<C, T>), dim3(B), dim3(kRT), 0, stream, lp, up, op, V, tt, kk); break;
+      switch (chunks) {
+        PENROZ_SAMPLE_REG(1) PENROZ_SAMPLE_REG(2) PENROZ_SAMPLE_REG(3) PENROZ_SAMPLE_REG(4) PENROZ_SAMPLE_REG(6)
+        PENROZ_SAMPLE_REG(8)
+        default:
+          if constexpr (sizeof(T) == 2) {
+            switch (chunks) { PENROZ_SAMPLE_REG(10) PENROZ_SAMPLE_REG(13) PENROZ_SAMPLE_REG(16) }
+          }
+      }
+#undef PENROZ_SAMPLE_REG
+    };
+    if (logits.scalar_type() == torch::kBFloat16) launch(bf16{});
+    else launch(float{});
+    return out;
+  }
   if (logits.scalar_type() == torch::kBFloat16)
     hipLaunchKernelGGL(sample_kernel<bf16>, dim3(B), dim3(kST), 0, stream,
                        reinterpret_cast<const bf16*>(logits.data_ptr()), u.data_ptr<float>(), out.data_ptr<int64_t>(),
