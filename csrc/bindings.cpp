@@ -5,7 +5,8 @@
 void layernorm_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor b, double eps, torch::Tensor y, torch::Tensor mean,
                    torch::Tensor rstd);
 void add_layernorm_fwd(torch::Tensor resid_in, torch::Tensor delta, torch::Tensor resid_out, torch::Tensor w,
-                       torch::Tensor b, double eps, torch::Tensor y, torch::Tensor mean, torch::Tensor rstd);
+                       torch::Tensor b, double eps, torch::Tensor y, torch::Tensor mean, torch::Tensor rstd,
+                       c10::optional<torch::Tensor> delta_bias);
 void layernorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor mean, torch::Tensor rstd, torch::Tensor w,
                    torch::Tensor dresid, bool accumulate, c10::optional<torch::Tensor> dresid_bf, torch::Tensor dw,
                    torch::Tensor db, c10::optional<torch::Tensor> dbias_prev);
@@ -18,7 +19,8 @@ void gelu_bwd(torch::Tensor dy, torch::Tensor x, int64_t approx, c10::optional<t
 void colsum(torch::Tensor x, torch::Tensor out);
 torch::Tensor gated_act_fwd(torch::Tensor g, torch::Tensor u, int64_t kind);
 std::vector<torch::Tensor> gated_act_bwd(torch::Tensor dy, torch::Tensor g, torch::Tensor u, int64_t kind);
-void embedding_fwd(torch::Tensor idx, torch::Tensor wte, torch::Tensor wpe, int64_t off, torch::Tensor out);
+void embedding_fwd(torch::Tensor idx, torch::Tensor wte, torch::Tensor wpe, int64_t off, torch::Tensor out,
+                   c10::optional<torch::Tensor> off_dev);
 void embedding_bwd(torch::Tensor dout, torch::Tensor idx, torch::Tensor dwte, torch::Tensor dwpe, int64_t off);
 torch::Tensor rope_qkv(torch::Tensor qkv, torch::Tensor cosv, torch::Tensor sinv, int64_t H, int64_t Hkv, int64_t D,
                        bool inverse);
@@ -49,6 +51,9 @@ void kv_append(torch::Tensor k, torch::Tensor v, torch::Tensor kc, torch::Tensor
 // gemm.hip
 void gemm_bf16(torch::Tensor a, torch::Tensor b, bool b_kn, c10::optional<torch::Tensor> bias, torch::Tensor out,
                c10::optional<torch::Tensor> act, int64_t gelu_approx, int64_t ablate);
+// skinny_gemm.hip
+int64_t skinny_gemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> bias, torch::Tensor out,
+                    torch::Tensor ws, torch::Tensor cnt, int64_t splitk);
 // gemm_wgrad.hip
 void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad, int64_t tile, int64_t variant);
 // flash_attn.hip
@@ -62,7 +67,9 @@ void flash_attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, to
 PYBIND11_MODULE(penroz_kernels, m) {
   m.doc() = "penroz hand-written HIP kernels for MI355X (gfx950)";
   m.def("layernorm_fwd", &layernorm_fwd);
-  m.def("add_layernorm_fwd", &add_layernorm_fwd);
+  m.def("add_layernorm_fwd", &add_layernorm_fwd, pybind11::arg("resid_in"), pybind11::arg("delta"),
+        pybind11::arg("resid_out"), pybind11::arg("w"), pybind11::arg("b"), pybind11::arg("eps"), pybind11::arg("y"),
+        pybind11::arg("mean"), pybind11::arg("rstd"), pybind11::arg("delta_bias") = pybind11::none());
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
   m.def("rmsnorm_bwd", &rmsnorm_bwd);
@@ -71,7 +78,8 @@ PYBIND11_MODULE(penroz_kernels, m) {
   m.def("colsum", &colsum);
   m.def("gated_act_fwd", &gated_act_fwd);
   m.def("gated_act_bwd", &gated_act_bwd);
-  m.def("embedding_fwd", &embedding_fwd);
+  m.def("embedding_fwd", &embedding_fwd, pybind11::arg("idx"), pybind11::arg("wte"), pybind11::arg("wpe"),
+        pybind11::arg("off"), pybind11::arg("out"), pybind11::arg("off_dev") = pybind11::none());
   m.def("embedding_bwd", &embedding_bwd);
   m.def("rope_qkv", &rope_qkv);
   m.def("kv_quantize", &kv_quantize);
@@ -91,6 +99,9 @@ PYBIND11_MODULE(penroz_kernels, m) {
   m.def("gemm_bf16", &gemm_bf16, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("b_kn"),
         pybind11::arg("bias") = pybind11::none(), pybind11::arg("out"), pybind11::arg("act") = pybind11::none(),
         pybind11::arg("gelu_approx") = 0, pybind11::arg("ablate") = 0);
+  m.def("skinny_gemm", &skinny_gemm, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("bias"),
+        pybind11::arg("out"), pybind11::arg("ws"), pybind11::arg("cnt"), pybind11::arg("splitk") = 0,
+        "decode-shaped out[M<=64, N] = x·wᵀ (+bias), bf16; returns the split-K factor used");
   m.def("wgrad_gemm", &wgrad_gemm, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("grad"),
         pybind11::arg("tile") = 256, pybind11::arg("variant") = 4);
   m.def("flash_attn_fwd", &flash_attn_fwd);

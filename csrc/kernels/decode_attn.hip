@@ -363,7 +363,8 @@ torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c
                           c10::optional<torch::Tensor> seq_len_dev) {
   TORCH_CHECK(q.is_cuda() && q.dim() == 4, "q must be [B, Tq, H, D]");
   // q may be a view into the fused QKV rows: unit dim stride, packed heads, uniform row stride
-  TORCH_CHECK(q.stride(3) == 1 && q.stride(2) == q.size(3) && q.stride(0) == q.size(1) * q.stride(1),
+  // (a size-1 Tq dim may carry any stride: the row stride is then stride(0))
+  TORCH_CHECK(q.stride(3) == 1 && q.stride(2) == q.size(3) && (q.size(1) == 1 || q.stride(0) == q.size(1) * q.stride(1)),
               "q must have packed heads and a uniform row stride");
   TORCH_CHECK(kc.is_contiguous() && vc.is_contiguous() && kc.dim() == 4 && kc.sizes() == vc.sizes());
   const int B = q.size(0), Tq = q.size(1), H = q.size(2), D = q.size(3);
@@ -375,7 +376,7 @@ torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c
   TORCH_CHECK(!quant || (k_scale.has_value() && v_scale.has_value()), "int8 cache needs scales");
   TORCH_CHECK(quant || kc.scalar_type() == q.scalar_type(), "cache dtype must match q");
   auto out = torch::empty({B, Tq, H * D}, q.options());
-  const int64_t q_rs = q.stride(1);
+  const int64_t q_rs = Tq == 1 ? q.stride(0) : q.stride(1);
   const int items = B * Hkv * Tq;
   int splits = std::max(1, std::min<int>((512 + items - 1) / items, (int)((S + 255) / 256)));
   torch::Tensor ws_o, ws_ml;

@@ -128,14 +128,16 @@ __global__ void __launch_bounds__(256) gated_bwd_kernel(const T* __restrict__ dy
 template <typename TW>
 __global__ void __launch_bounds__(256) embed_fwd_kernel(const int64_t* __restrict__ idx, const TW* __restrict__ wte,
                                                         const TW* __restrict__ wpe, float* __restrict__ out, int N,
-                                                        int T, int C, int off, int V) {
+                                                        int T, int C, int off, int V, const int64_t* __restrict__ off_dev,
+                                                        int P) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= N) return;
   int64_t tok = idx[row];
   PZ_DEVICE_CHECK(tok >= 0 && tok < V);
   tok = tok < 0 ? 0 : (tok >= V ? V - 1 : tok);
-  const int pos = off + row % T;
+  if (off_dev != nullptr) off = (int)*off_dev;  // graph-replayed decode: position on the device
+  const int pos = min(off + row % T, P - 1);
   for (int c = 8 * lane; c < C; c += 512) {
     float a[8], b[8];
     Vec8<TW>::load(wte + (size_t)tok * C + c, a);
@@ -394,11 +396,18 @@ std::vector<torch::Tensor> gated_act_bwd(torch::Tensor dy, torch::Tensor g, torc
   return {dg, du};
 }
 
-void embedding_fwd(torch::Tensor idx, torch::Tensor wte, torch::Tensor wpe, int64_t off, torch::Tensor out) {
+void embedding_fwd(torch::Tensor idx, torch::Tensor wte, torch::Tensor wpe, int64_t off, torch::Tensor out,
+                   c10::optional<torch::Tensor> off_dev) {
   TORCH_CHECK(idx.is_cuda() && idx.scalar_type() == torch::kInt64 && idx.dim() == 2);
   const int B = idx.size(0), T = idx.size(1), C = wte.size(1), V = wte.size(0);
   TORCH_CHECK(C % 8 == 0 && wpe.size(1) == C && wte.scalar_type() == wpe.scalar_type());
-  TORCH_CHECK(off + T <= wpe.size(0), "positions exceed the position table");
+  const int64_t* od = nullptr;
+  if (off_dev.has_value() && off_dev->defined()) {  // device offset: the caller bounds it (clamped here)
+    TORCH_CHECK(off_dev->is_cuda() && off_dev->scalar_type() == torch::kInt64 && off_dev->numel() == 1);
+    od = off_dev->data_ptr<int64_t>();
+  } else {
+    TORCH_CHECK(off + T <= wpe.size(0), "positions exceed the position table");
+  }
   TORCH_CHECK(out.scalar_type() == torch::kFloat32 && out.numel() == (int64_t)B * T * C && out.is_contiguous());
   auto idxc = idx.contiguous();
   const int N = B * T;
@@ -406,7 +415,7 @@ void embedding_fwd(torch::Tensor idx, torch::Tensor wte, torch::Tensor wpe, int6
   FOR_FLOAT_TYPES(wte.scalar_type(), TW,
     hipLaunchKernelGGL(embed_fwd_kernel<TW>, dim3((N + 3) / 4), dim3(256), 0, stream, idxc.data_ptr<int64_t>(),
                        reinterpret_cast<const TW*>(wte.data_ptr()), reinterpret_cast<const TW*>(wpe.data_ptr()),
-                       out.data_ptr<float>(), N, T, C, (int)off, V))
+                       out.data_ptr<float>(), N, T, C, (int)off, V, od, (int)wpe.size(0)))
 }
 
 void embedding_bwd(torch::Tensor dout, torch::Tensor idx, torch::Tensor dwte, torch::Tensor dwpe, int64_t off) {

@@ -63,7 +63,7 @@ constexpr int kRowsPerBlock = 4;
 // ------------------------------------------------------------------------------------------
 // forward: y = LN(x [+ delta]); optional resid_out = x + delta (fp32)
 template <int NCH, typename TX, typename TD, typename TY, bool ADD>
-__global__ void __launch_bounds__(256) ln_fwd_kernel(const TX* __restrict__ x, const TD* __restrict__ delta,
+__global__ void __launch_bounds__(256) ln_fwd_kernel(const TX* __restrict__ x, const TD* __restrict__ delta, const float* __restrict__ dbias,
                                                      float* __restrict__ resid_out, const float* __restrict__ w,
                                                      const float* __restrict__ b, TY* __restrict__ y,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
@@ -82,6 +82,12 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const TX* __restrict__ x, c
     if constexpr (ADD) {
       float d[4];
       V4<TD>::ld(delta + base + c, d);
+      if (dbias) {  // the producing linear's bias, folded in here (decode program)
+        float e[4];
+        V4<float>::ld(dbias + c, e);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d[k] += e[k];
+      }
 #pragma unroll
       for (int k = 0; k < 4; ++k) v[j][k] += d[k];
       V4<float>::st(resid_out + base + c, v[j]);
@@ -117,7 +123,7 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const TX* __restrict__ x, c
 
 // Generic-width fallback (C % 4 == 0): loops over the row twice through L2.
 template <typename TX, typename TD, typename TY, bool ADD>
-__global__ void __launch_bounds__(256) ln_fwd_loop_kernel(const TX* __restrict__ x, const TD* __restrict__ delta,
+__global__ void __launch_bounds__(256) ln_fwd_loop_kernel(const TX* __restrict__ x, const TD* __restrict__ delta, const float* __restrict__ dbias,
                                                           float* __restrict__ resid_out, const float* __restrict__ w,
                                                           const float* __restrict__ b, TY* __restrict__ y,
                                                           float* __restrict__ mean_out, float* __restrict__ rstd_out,
@@ -133,6 +139,12 @@ __global__ void __launch_bounds__(256) ln_fwd_loop_kernel(const TX* __restrict__
     if constexpr (ADD) {
       float d[4];
       V4<TD>::ld(delta + base + c, d);
+      if (dbias) {
+        float e[4];
+        V4<float>::ld(dbias + c, e);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d[k] += e[k];
+      }
 #pragma unroll
       for (int k = 0; k < 4; ++k) v[k] += d[k];
       V4<float>::st(resid_out + base + c, v);
@@ -283,7 +295,7 @@ static bool nch_ok(int C) { return nch_pick(C) != 0; }
 template <typename TX, typename TD, typename TY, bool ADD>
 static void launch_fwd(const torch::Tensor& x, const torch::Tensor* delta, torch::Tensor* resid_out,
                        const torch::Tensor& w, const torch::Tensor& b, torch::Tensor& y, torch::Tensor& mean,
-                       torch::Tensor& rstd, double eps) {
+                       torch::Tensor& rstd, double eps, const float* dbias = nullptr) {
   const int N = x.size(0), C = x.size(1);
   if (N == 0) return;
   dim3 grid((N + kRowsPerBlock - 1) / kRowsPerBlock), block(256);
@@ -293,11 +305,11 @@ static void launch_fwd(const torch::Tensor& x, const torch::Tensor* delta, torch
   float* rp = resid_out ? resid_out->data_ptr<float>() : nullptr;
   TY* yp = reinterpret_cast<TY*>(y.data_ptr());
   if (nch_ok(C)) {
-    DISPATCH_NCH(C, hipLaunchKernelGGL((ln_fwd_kernel<NCH, TX, TD, TY, ADD>), grid, block, 0, stream, xp, dp, rp,
+    DISPATCH_NCH(C, hipLaunchKernelGGL((ln_fwd_kernel<NCH, TX, TD, TY, ADD>), grid, block, 0, stream, xp, dp, dbias, rp,
                                        w.data_ptr<float>(), b.data_ptr<float>(), yp, mean.data_ptr<float>(),
                                        rstd.data_ptr<float>(), N, C, (float)eps));
   } else {
-    hipLaunchKernelGGL((ln_fwd_loop_kernel<TX, TD, TY, ADD>), grid, block, 0, stream, xp, dp, rp, w.data_ptr<float>(),
+    hipLaunchKernelGGL((ln_fwd_loop_kernel<TX, TD, TY, ADD>), grid, block, 0, stream, xp, dp, dbias, rp, w.data_ptr<float>(),
                        b.data_ptr<float>(), yp, mean.data_ptr<float>(), rstd.data_ptr<float>(), N, C, (float)eps);
   }
 }
@@ -326,7 +338,8 @@ void layernorm_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor b, double eps
 }
 
 void add_layernorm_fwd(torch::Tensor resid_in, torch::Tensor delta, torch::Tensor resid_out, torch::Tensor w,
-                       torch::Tensor b, double eps, torch::Tensor y, torch::Tensor mean, torch::Tensor rstd) {
+                       torch::Tensor b, double eps, torch::Tensor y, torch::Tensor mean, torch::Tensor rstd,
+                       c10::optional<torch::Tensor> delta_bias) {
   const int64_t N = resid_in.size(0), C = resid_in.size(1);
   check_rows(resid_in, N, C, "resid_in");
   check_rows(delta, N, C, "delta");
@@ -334,10 +347,16 @@ void add_layernorm_fwd(torch::Tensor resid_in, torch::Tensor delta, torch::Tenso
   check_rows(y, N, C, "y");
   TORCH_CHECK(resid_out.scalar_type() == torch::kFloat32, "residual stream must be fp32");
   TORCH_CHECK(w.numel() == C && b.numel() == C && mean.numel() == N && rstd.numel() == N);
+  const float* dbp = nullptr;
+  if (delta_bias.has_value() && delta_bias->defined()) {  // resid_out = resid_in + delta + delta_bias
+    TORCH_CHECK(delta_bias->scalar_type() == torch::kFloat32 && delta_bias->is_contiguous() && delta_bias->numel() == C,
+                "delta_bias must be fp32 [C]");
+    dbp = delta_bias->data_ptr<float>();
+  }
   FOR_FLOAT_TYPES(resid_in.scalar_type(), TX,
     FOR_FLOAT_TYPES(delta.scalar_type(), TD,
       FOR_FLOAT_TYPES(y.scalar_type(), TY,
-        launch_fwd<TX, TD, TY, true>(resid_in, &delta, &resid_out, w, b, y, mean, rstd, eps))))
+        launch_fwd<TX, TD, TY, true>(resid_in, &delta, &resid_out, w, b, y, mean, rstd, eps, dbp))))
 }
 
 void layernorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor mean, torch::Tensor rstd, torch::Tensor w,

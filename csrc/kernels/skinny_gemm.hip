@@ -1,0 +1,183 @@
+// Decode-shaped GEMMs: out[M, N] = x[M, K] · W[N, K]ᵀ (+ bias) for M <= 64 rows (one token per
+// sequence of a decode batch), bf16 operands, fp32 accumulate — nn.Linear's layout.
+//
+// At these shapes a GEMM is latency-bound, not FLOP- or bandwidth-bound: GPT-2's QKV projection
+// at M = 64 reads 3.5 MB of weights (0.7 µs of HBM time) and does 0.2 GFLOP, yet a library tile
+// (hipBLASLt MT32x64x64, 96 workgroups) takes ~10 µs. What matters is how many independent loads
+// are in flight per CU and how many CUs take part. So:
+//   * a workgroup owns a 16-column slice of the output for ALL M rows: one 16x16x32 MFMA
+//     column block, MB = ceil(M/16) row blocks; ceil(N/16) workgroups (144 for N = 2304);
+//   * its 4 waves split the K range four ways (reduced through LDS at the end), and narrow
+//     outputs (N = 768: 48 slices) also split K across workgroups (split-K with an in-launch
+//     slab reduction: agent-scope release, arrival counter, the last arriver sums the slabs —
+//     the counter is reset by that last arriver, so a captured graph can replay the kernel);
+//   * operands go straight from global memory to MFMA fragments (A = W rows, B = x rows, 16 B
+//     per lane per k-step) — every k-step's loads of a wave are issued before its first MFMA;
+//     an LDS round trip would only add latency for operands nobody else in the workgroup reads.
+// C/D layout of mfma_f32_16x16x32_bf16: col = lane & 15 (row m of x), row = 4·(lane >> 4) + r
+// (output column n), so each lane ends with 4 consecutive outputs of one row.
+#include "common.h"
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+
+namespace penroz {
+
+typedef short sk_bf16x8 __attribute__((ext_vector_type(8)));
+typedef float sk_f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t sk_u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kSkU = 8;  // k-steps (of 32) whose loads are issued together
+
+template <int MB>
+__global__ void __launch_bounds__(256) skinny_gemm_kernel(const bf16* __restrict__ x, int64_t x_rs,
+                                                          const bf16* __restrict__ w, const bf16* __restrict__ bias,
+                                                          bf16* __restrict__ out, int64_t o_rs, int M, int N, int K,
+                                                          int splitk, float* __restrict__ ws, int* __restrict__ cnt) {
+  // the 4 waves' partial tiles, then (split-K) the "last arriver" flag: ONE LDS object
+  __shared__ __attribute__((aligned(16))) float red[4 * MB * 64 * 4 + 4];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int ntiles = gridDim.x / splitk;
+  const int tile = blockIdx.x / splitk, split = blockIdx.x % splitk;
+  const int n0 = tile * 16;
+  const int steps = K / 32;
+  const int sb0 = (int)((int64_t)steps * split / splitk), sb1 = (int)((int64_t)steps * (split + 1) / splitk);
+  const int nsb = sb1 - sb0;
+  const int s0 = sb0 + nsb * wid / 4, s1 = sb0 + nsb * (wid + 1) / 4;
+
+  const int r16 = lane & 15, kq = 8 * (lane >> 4);
+  const bf16* wp = w + (size_t)min(n0 + r16, N - 1) * K + kq;  // rows past N: clamped, never stored
+  const bf16* xp[MB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    const int m = mb * 16 + r16;
+    xp[mb] = x + (size_t)(m < M ? m : 0) * x_rs + kq;  // rows past M: only feed unstored outputs
+  }
+  sk_f32x4 acc[MB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) acc[mb] = (sk_f32x4){0.f, 0.f, 0.f, 0.f};
+
+  for (int s = s0; s < s1; s += kSkU) {
+    // all loads of the group first (addresses clamped to the last valid step: no per-load
+    // branches), then the MFMAs of the steps that exist
+    sk_u32x4 wa[kSkU], xb[kSkU][MB];
+#pragma unroll
+    for (int u = 0; u < kSkU; ++u) {
+      const size_t ko = (size_t)min(s + u, s1 - 1) * 32;
+      wa[u] = *reinterpret_cast<const sk_u32x4*>(wp + ko);
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) xb[u][mb] = *reinterpret_cast<const sk_u32x4*>(xp[mb] + ko);
+    }
+#pragma unroll
+    for (int u = 0; u < kSkU; ++u) {
+      if (s + u < s1) {
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb)
+          acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(sk_bf16x8, wa[u]),
+                                                            __builtin_bit_cast(sk_bf16x8, xb[u][mb]), acc[mb], 0, 0, 0);
+      }
+    }
+  }
+
+  sk_f32x4* r4 = reinterpret_cast<sk_f32x4*>(red);
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) r4[(wid * MB + mb) * 64 + lane] = acc[mb];
+  __syncthreads();
+
+  auto epilogue = [&](int it, sk_f32x4 v) {
+    const int ln = it & 63, m = (it >> 6) * 16 + (ln & 15), nb = n0 + 4 * (ln >> 4);
+    if (m >= M) return;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = nb + r;
+      if (n < N) out[(size_t)m * o_rs + n] = from_f<bf16>(v[r] + (bias ? bf2f(bias[n]) : 0.f));
+    }
+  };
+  auto block_sum = [&](int it) {
+    const int mb = it >> 6, ln = it & 63;
+    return r4[mb * 64 + ln] + r4[(MB + mb) * 64 + ln] + r4[(2 * MB + mb) * 64 + ln] + r4[(3 * MB + mb) * 64 + ln];
+  };
+  if (splitk == 1) {
+    for (int it = t; it < MB * 64; it += 256) epilogue(it, block_sum(it));
+    return;
+  }
+  // split-K: slab of this (split, tile), then the counter hand-off (agent-scope release on the
+  // writer, acquire on the last arriver; correct wherever the tile's splits ran)
+  sk_f32x4* slab = reinterpret_cast<sk_f32x4*>(ws);
+  for (int it = t; it < MB * 64; it += 256) slab[((size_t)split * ntiles + tile) * (MB * 64) + it] = block_sum(it);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(red + 4 * MB * 64 * 4);
+  if (t == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int prev = __hip_atomic_fetch_add(&cnt[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = prev == splitk - 1;
+  }
+  __syncthreads();
+  if (!*flag) return;
+  if (t == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(&cnt[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  for (int it = t; it < MB * 64; it += 256) {
+    sk_f32x4 v = slab[(size_t)tile * (MB * 64) + it];
+    for (int sp = 1; sp < splitk; ++sp) v += slab[((size_t)sp * ntiles + tile) * (MB * 64) + it];
+    epilogue(it, v);
+  }
+}
+
+}  // namespace penroz
+
+using namespace penroz;
+
+// splitk <= 0: chosen here (workgroups ~ 192 when the 16-column slices alone are too few).
+// ws: fp32 workspace (>= splitk * ceil(N/16) * MB * 256 floats when splitk > 1); cnt: int32
+// counters (>= ceil(N/16)), zero on entry — every launch leaves them zero again.
+int64_t skinny_gemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> bias, torch::Tensor out,
+                    torch::Tensor ws, torch::Tensor cnt, int64_t splitk) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kBFloat16 && w.scalar_type() == torch::kBFloat16 &&
+                  out.scalar_type() == torch::kBFloat16, "skinny_gemm: bf16 x / w / out");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "skinny_gemm: 2-D operands");
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(M >= 1 && M <= 64 && w.size(1) == K && K % 32 == 0, "skinny_gemm: M <= 64, K % 32 == 0");
+  TORCH_CHECK(x.stride(1) == 1 && x.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "skinny_gemm: x rows 16-B aligned");
+  TORCH_CHECK(w.is_contiguous() && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0, "skinny_gemm: w contiguous");
+  TORCH_CHECK(out.size(0) == M && out.size(1) == N && out.stride(1) == 1, "skinny_gemm: out [M, N]");
+  const bf16* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->scalar_type() == torch::kBFloat16 && bias->is_contiguous() && bias->numel() == N,
+                "skinny_gemm: bf16 bias [N]");
+    bp = reinterpret_cast<const bf16*>(bias->data_ptr());
+  }
+  const int ntiles = (N + 15) / 16, steps = K / 32;
+  const int MB = M <= 16 ? 1 : M <= 32 ? 2 : 4;
+  if (splitk <= 0) {
+    splitk = 1;
+    if (ntiles < 128) splitk = std::max(1, std::min({(192 + ntiles - 1) / ntiles, steps / 4, 16}));
+  }
+  TORCH_CHECK(splitk >= 1 && splitk <= steps, "skinny_gemm: bad split");
+  if (splitk > 1) {
+    TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == torch::kFloat32 &&
+                    ws.numel() >= (int64_t)splitk * ntiles * MB * 256, "skinny_gemm: workspace too small");
+    TORCH_CHECK(cnt.is_cuda() && cnt.scalar_type() == torch::kInt32 && cnt.numel() >= ntiles,
+                "skinny_gemm: counters too small");
+  }
+  auto stream = at::hip::getCurrentHIPStream();
+  const dim3 grid(ntiles * splitk);
+  auto xp = reinterpret_cast<const bf16*>(x.data_ptr());
+  auto wp = reinterpret_cast<const bf16*>(w.data_ptr());
+  auto op = reinterpret_cast<bf16*>(out.data_ptr());
+  float* wsp = splitk > 1 ? ws.data_ptr<float>() : nullptr;
+  int* cp = splitk > 1 ? cnt.data_ptr<int>() : nullptr;
+#define PENROZ_SKINNY(MBV)                                                                                       \
+  hipLaunchKernelGGL(skinny_gemm_kernel<MBV>, grid, dim3(256), 0, stream, xp, (int64_t)x.stride(0), wp, bp, op, \
+                     (int64_t)out.stride(0), M, N, K, (int)splitk, wsp, cp)
+  if (MB == 1) PENROZ_SKINNY(1);
+  else if (MB == 2) PENROZ_SKINNY(2);
+  else PENROZ_SKINNY(4);
+#undef PENROZ_SKINNY
+  return splitk;
+}

@@ -83,7 +83,9 @@ def _dropout_zero(m) -> bool:
 class GPTExecutor:
     # ------------------------------------------------------------------ pattern match
     @staticmethod
-    def match(model) -> GPTSpec | None:
+    def match(model, require_fp32: bool = True) -> GPTSpec | None:
+        """The GPT-2 block structure (``require_fp32``: the training executor's fp32 masters;
+        the decode program of ``graph_decode.py`` also takes bf16 models)."""
         ls = list(model.layers)
         if len(ls) < 5:
             return None
@@ -137,7 +139,7 @@ class GPTExecutor:
             return None
         if tuple(spec.lnf.normalized_shape) != (C,) or spec.head.in_features != C:
             return None
-        if any(p.dtype != torch.float32 for p in model.parameters()):
+        if require_fp32 and any(p.dtype != torch.float32 for p in model.parameters()):
             return None
         spec.gelu_approx = approx
         return spec

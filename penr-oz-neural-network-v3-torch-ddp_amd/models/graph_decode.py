@@ -17,7 +17,9 @@ replayed. Everything that changes between steps lives on the device:
   (``csrc/kernels/decode_attn.hip``: ``kv_append``, ``seq_len_dev``);
 * ``PositionEmbedding.position_offset_tensor``: the learned position gathered at ``pos_t``;
 * the uniforms of temperature / top-k sampling are drawn on the device (graph-safe Philox);
-* the sampled token is copied into the step's input buffer and into a burst output buffer.
+* the sampled token is copied into the step's input buffer and into a burst output buffer;
+* the step's ``nn.Linear`` GEMMs (M = rows ≤ 64) run on the decode-shaped MFMA kernel
+  (``ops/gemm.py: decode_gemms``, ``csrc/kernels/skinny_gemm.hip``).
 
 The host only tracks the cache length (one per replay) to switch to the reference's
 sliding-window re-prefill when the window is full, and copies each burst of tokens back once
@@ -34,12 +36,22 @@ from torch import Tensor
 
 from penroz.models import kv_cache as kvc
 from penroz.ops import _ext
+from penroz.ops import activations as act_ops
 from penroz.ops import attention as attn_ops
+from penroz.ops import fused as fused_ops
+from penroz.ops import gemm as gemm_ops
+from penroz.ops import norms as norm_ops
 from penroz.ops import sampling as samp_ops
 
 log = logging.getLogger(__name__)
 
 GRAPH_DECODE = os.environ.get("PENROZ_GRAPH_DECODE", "1") != "0"
+# GPT-2-pattern bf16 models: the captured step is the explicit program below instead of the
+# module forward ("0": module forward, numerically identical to the eager decode path)
+DECODE_PROGRAM = os.environ.get("PENROZ_DECODE_PROGRAM", "1") != "0"
+# decode rows up to which the linears use the decode-shaped MFMA kernel instead of hipBLASLt
+# (measured: a win at batch 1, none at batch 64 — profiles/bench_r1_decode_graph.log)
+SKINNY_MAX_ROWS = int(os.environ.get("PENROZ_SKINNY_MAX_ROWS", "16"))
 
 
 class _GraphMode:
@@ -75,6 +87,84 @@ class StaticTurboKVCache(_GraphMode, kvc.TurboQuantKVCache):
                                          seq_len_dev=self.len_t)
 
 
+class GPTDecodeProgram:
+    """One decode step of a GPT-2-pattern bf16 model as an explicit kernel sequence.
+
+    The module forward costs ~12 kernels per block at decode shapes (residual adds and dtype
+    glue included) and every kernel has a fixed ~4-5 µs cost in a replayed graph at batch 64 —
+    more than most of them compute. Per block this runs 9: [add-residual + fc2 bias + LN1] →
+    QKV GEMM+bias → KV append → decode attention → proj GEMM → [add-residual + proj bias + LN2]
+    → fc GEMM+bias → GELU → fc2 GEMM, with the residual stream kept in fp32 (the training executor's
+    numerics; the module path rounds it to bf16 after every add). The embedding reads the
+    position from the device.
+    """
+
+    def __init__(self, model, spec):
+        self.spec = spec
+        dev = spec.wte.weight.device
+        # LayerNorm kernels take fp32 affine parameters
+        self.ln = [(b.ln1.weight.float(), b.ln1.bias.float(), b.ln1.eps, b.ln2.weight.float(), b.ln2.bias.float(),
+                    b.ln2.eps) for b in spec.blocks]
+        self.lnf = (spec.lnf.weight.float(), spec.lnf.bias.float(), spec.lnf.eps)
+        # proj / fc2 biases are added by the following add+LN kernel (fp32), so those two GEMMs
+        # run without a bias epilogue (hipBLASLt's pick for fc2 at M = 64 has none: torch then
+        # launches an extra bias-broadcast copy per call)
+        self.out_bias = [(b.proj.bias.float(), b.fc2.bias.float()) for b in spec.blocks]
+        self.device = dev
+
+    @staticmethod
+    def build(model):
+        if not DECODE_PROGRAM:
+            return None
+        from penroz.models.executor import GPTExecutor
+        spec = GPTExecutor.match(model, require_fp32=False)
+        if spec is None or any(p.dtype != torch.bfloat16 for p in model.parameters()):
+            return None
+        return GPTDecodeProgram(model, spec)
+
+    def _linear(self, x: Tensor, lin, bias: bool = True) -> Tensor:
+        b = lin.bias if bias else None
+        if x.shape[0] <= SKINNY_MAX_ROWS and gemm_ops.skinny_ok(x, lin.weight):
+            return gemm_ops.skinny_linear(x, lin.weight, b)
+        if b is not None:
+            return torch.addmm(b, x, lin.weight.t())
+        return torch.mm(x, lin.weight.t())
+
+    def forward(self, idx: Tensor, cache) -> Tensor:
+        """idx [rows, 1] -> logits [rows, V] (bf16); appends this step's K/V at cache.pos_t."""
+        sp = self.spec
+        rows, C, H, D = idx.shape[0], sp.C, sp.H, sp.D
+        x = fused_ops.embedding_fwd(idx, sp.wte.weight, sp.wpe.weight, 0, pos_dev=cache.pos_t)  # fp32 [rows, C]
+        x2 = torch.empty_like(x)  # the residual stream ping-pongs between x and x2 (no aliasing)
+
+        def add_ln(delta, w, b, eps, dbias=None):
+            nonlocal x, x2
+            y, _, _ = norm_ops.add_ln_fwd(x, delta, x2, w, b, eps, delta_bias=dbias)
+            x, x2 = x2, x
+            return y
+
+        delta = dbias = None
+        for l, blk in enumerate(sp.blocks):
+            w1, b1, e1, w2, b2, e2 = self.ln[l]
+            pb, fb = self.out_bias[l]
+            if delta is None:
+                y, _, _ = norm_ops.ln_fwd(x, w1, b1, e1)
+            else:
+                y = add_ln(delta, w1, b1, e1, dbias)
+            qkv = self._linear(y, blk.qkv).view(rows, 1, 3 * C)
+            q = qkv[:, :, :C].view(rows, 1, H, D)
+            k = qkv[:, :, C:2 * C].view(rows, 1, H, D)
+            v = qkv[:, :, 2 * C:].view(rows, 1, H, D)
+            o = cache._attend_graph(l, q, k, v)
+            d = self._linear(o.view(rows, C), blk.proj, bias=False)
+            y = add_ln(d, w2, b2, e2, pb)
+            h = self._linear(y, blk.fc)
+            h = act_ops.gelu_fwd(h, sp.gelu_approx, out=h)
+            delta, dbias = self._linear(h, blk.fc2, bias=False), fb
+        wf, bf, ef = self.lnf
+        return self._linear(add_ln(delta, wf, bf, ef, dbias), sp.head)
+
+
 def applicable(model) -> bool:
     if not GRAPH_DECODE or not torch.cuda.is_available():
         return False
@@ -102,6 +192,8 @@ class GraphDecoder:
         self.out = torch.zeros(rows, capacity, dtype=torch.long, device=self.device)
         self.step_t = torch.zeros(1, dtype=torch.long, device=self.device)
         self.graph: torch.cuda.CUDAGraph | None = None
+        gemm_ops.skinny_workspace(self.device)  # zeroed counters exist before any capture
+        self.program = GPTDecodeProgram.build(model)
 
     # ------------------------------------------------------------------ cache attachment
     def attach(self):
@@ -121,9 +213,13 @@ class GraphDecoder:
             p.position_offset_tensor = self.cache.pos_t
         self.cache.graph_mode = True
         try:
-            acts, _ = self.model(self.idx, skip_softmax=True)
-            logits = acts[-1]
-            last = logits[:, -1, :] if logits.ndim == 3 else logits
+            if self.program is not None:
+                last = self.program.forward(self.idx, self.cache)
+            else:
+                with gemm_ops.decode_gemms(max_rows=SKINNY_MAX_ROWS):
+                    acts, _ = self.model(self.idx, skip_softmax=True)
+                logits = acts[-1]
+                last = logits[:, -1, :] if logits.ndim == 3 else logits
             nxt = samp_ops.sample(last, self.temperature, self.top_k, device_rng=True)
             torch.add(nxt, 0, out=self.idx)  # a kernel, not a memcpy node
             self.out.index_copy_(1, self.step_t, nxt)

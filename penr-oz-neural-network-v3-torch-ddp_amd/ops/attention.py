@@ -140,7 +140,8 @@ def decode_attention(q: Tensor, k_cache: Tensor, v_cache: Tensor, seq_len: int,
     Tq = q.shape[1]
     if use_kernels(q) and q.shape[-1] in DECODE_HEAD_DIMS:
         # a view into the fused QKV rows is read in place (packed heads, uniform row stride)
-        if not (q.stride(3) == 1 and q.stride(2) == q.shape[3] and q.stride(0) == q.shape[1] * q.stride(1)):
+        if not (q.stride(3) == 1 and q.stride(2) == q.shape[3]
+                and (Tq == 1 or q.stride(0) == q.shape[1] * q.stride(1))):
             q = q.contiguous()
         return kernels().decode_attn(q, k_cache, v_cache, k_scale, v_scale, int(seq_len),
                                      int(seq_len - Tq), 1.0 / math.sqrt(q.shape[-1]), seq_len_dev)

@@ -31,11 +31,13 @@ def reference_embedding_fwd(idx: Tensor, wte: Tensor, wpe: Tensor, pos_offset: i
     return (wte[idx].float() + wpe[pos].float().unsqueeze(0)).reshape(B * T, -1)
 
 
-def embedding_fwd(idx: Tensor, wte: Tensor, wpe: Tensor, pos_offset: int = 0, out: Tensor | None = None) -> Tensor:
-    """idx [B,T] int64 -> fp32 [B*T, C] = wte[idx] + wpe[offset + t]."""
+def embedding_fwd(idx: Tensor, wte: Tensor, wpe: Tensor, pos_offset: int = 0, out: Tensor | None = None,
+                  pos_dev: Tensor | None = None) -> Tensor:
+    """idx [B,T] int64 -> fp32 [B*T, C] = wte[idx] + wpe[offset + t]; ``pos_dev`` (device int64
+    [1]) supplies the offset at run time instead (graph-replayed decode; clamped to the table)."""
     B, T = idx.shape
     out = torch.empty(B * T, wte.shape[1], dtype=torch.float32, device=idx.device) if out is None else out
-    kernels().embedding_fwd(idx, wte, wpe, int(pos_offset), out)
+    kernels().embedding_fwd(idx, wte, wpe, int(pos_offset), out, pos_dev)
     return out
 
 

@@ -75,3 +75,80 @@ def linear_dgrad(dy: Tensor, w: Tensor, out: Tensor) -> Tensor:
         kernels().gemm_bf16(dy, w, True, None, out)
         return out
     return torch.mm(dy, w, out=out)
+
+
+# ---- decode-shaped GEMMs (csrc/kernels/skinny_gemm.hip) --------------------------------------
+# out[M<=64, N] = x·Wᵀ (+ bias), bf16: one 16-column MFMA slice per workgroup over all rows,
+# K split across the 4 waves (and across workgroups, with an in-launch slab reduction, when the
+# output is narrow). Used for the graph-captured decode step (models/graph_decode.py), where a
+# library GEMM tile at M = 64 leaves most CUs idle (~10 µs for a 3.5 MB weight read).
+SKINNY_GEMM = os.environ.get("PENROZ_SKINNY_GEMM", "1") != "0"
+_skinny_ws: dict = {}
+
+
+def skinny_workspace(device: torch.device) -> tuple[Tensor, Tensor]:
+    """Per-device split-K workspace and arrival counters (zeroed once, outside any graph
+    capture; every launch leaves the counters zero again)."""
+    key = (device.type, device.index if device.index is not None else torch.cuda.current_device())
+    buf = _skinny_ws.get(key)
+    if buf is None:
+        dev = torch.device(*key)
+        buf = (torch.empty(1 << 19, device=dev, dtype=torch.float32), torch.zeros(1 << 12, device=dev, dtype=torch.int32))
+        _skinny_ws[key] = buf
+    return buf
+
+
+def skinny_ok(x: Tensor, w: Tensor) -> bool:
+    if not (SKINNY_GEMM and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16):
+        return False
+    K = x.shape[-1]
+    rows = x.numel() // K if K else 0
+    return (0 < rows <= 64 and K % 32 == 0 and w.is_contiguous() and w.shape[1] == K and w.data_ptr() % 16 == 0
+            and use_kernels(x))
+
+
+def skinny_linear(x: Tensor, w: Tensor, bias: Tensor | None) -> Tensor:
+    """nn.Linear forward for ≤ 64 rows of bf16 activations (any leading shape)."""
+    K, N = x.shape[-1], w.shape[0]
+    x2 = x.reshape(-1, K)
+    if x2.stride(1) != 1 or x2.stride(0) % 8 or x2.data_ptr() % 16:
+        x2 = x2.contiguous()
+    out = torch.empty(x2.shape[0], N, device=x.device, dtype=x.dtype)
+    ws, cnt = skinny_workspace(x.device)
+    kernels().skinny_gemm(x2, w, bias if bias is None or bias.dtype == torch.bfloat16 else bias.to(torch.bfloat16),
+                          out, ws, cnt)
+    return out.view(*x.shape[:-1], N)
+
+
+class decode_gemms:
+    """Context: ``nn.Linear`` modules run decode-shaped inputs through the skinny kernel (others
+    keep ``F.linear``). Entered by the graph decoder around the captured step."""
+
+    _orig = None
+
+    def __init__(self, max_rows: int = 64):
+        self.max_rows = max_rows
+
+    def __enter__(self):
+        if decode_gemms._orig is None and SKINNY_GEMM and self.max_rows > 0:
+            orig = torch.nn.Linear.forward
+            max_rows = self.max_rows
+
+            def forward(mod, x):
+                if (x.numel() <= max_rows * x.shape[-1] and skinny_ok(x, mod.weight)
+                        and (mod.bias is None or mod.bias.is_contiguous())):
+                    return skinny_linear(x, mod.weight, mod.bias)
+                return orig(mod, x)
+
+            decode_gemms._orig = orig
+            torch.nn.Linear.forward = forward
+            self._owner = True
+        else:
+            self._owner = False
+        return self
+
+    def __exit__(self, *exc):
+        if self._owner:
+            torch.nn.Linear.forward = decode_gemms._orig
+            decode_gemms._orig = None
+        return False

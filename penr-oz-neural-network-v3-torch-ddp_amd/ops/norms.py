@@ -59,13 +59,15 @@ def ln_fwd(x2d: Tensor, w: Tensor, b: Tensor, eps: float, out_dtype=torch.bfloat
 
 
 def add_ln_fwd(resid_in: Tensor, delta: Tensor, resid_out: Tensor, w: Tensor, b: Tensor, eps: float,
-               y: Tensor | None = None, mean: Tensor | None = None, rstd: Tensor | None = None):
-    """``resid_out = resid_in + delta`` (fp32 stream, bf16 delta) and LayerNorm(resid_out) -> bf16 y."""
+               y: Tensor | None = None, mean: Tensor | None = None, rstd: Tensor | None = None,
+               delta_bias: Tensor | None = None):
+    """``resid_out = resid_in + delta (+ delta_bias)`` (fp32 stream, bf16 delta, fp32 bias [C])
+    and LayerNorm(resid_out) -> bf16 y."""
     N, C = resid_in.shape
     y = torch.empty(N, C, dtype=torch.bfloat16, device=resid_in.device) if y is None else y
     mean = torch.empty(N, dtype=torch.float32, device=resid_in.device) if mean is None else mean
     rstd = torch.empty(N, dtype=torch.float32, device=resid_in.device) if rstd is None else rstd
-    kernels().add_layernorm_fwd(resid_in, delta, resid_out, w, b, float(eps), y, mean, rstd)
+    kernels().add_layernorm_fwd(resid_in, delta, resid_out, w, b, float(eps), y, mean, rstd, delta_bias)
     return y, mean, rstd
 
 

@@ -1,6 +1,10 @@
 """Graph-captured decoding (models/graph_decode.py) vs the eager per-token path on MI355X:
 greedy generation must produce identical tokens (same kernels, same cache contents), through the
-sliding-window re-prefill, with a stop token, streaming, multiple rows and the int8 cache."""
+sliding-window re-prefill, with a stop token, streaming, multiple rows and the int8 cache.
+
+The module-forward graph is compared with the eager module path token for token. The GPT decode
+program (fp32 residual stream, fused add+LN) is compared with the module step's logits within
+bf16 tolerance, and its graph replay with the same program run eagerly, token for token."""
 import pytest
 import torch
 
@@ -26,6 +30,7 @@ def _model(dtype):
 
 
 def _both(monkeypatch, fn):
+    monkeypatch.setattr(gd, "DECODE_PROGRAM", False)  # the module-forward graph: same numerics as eager
     monkeypatch.setattr(gd, "GRAPH_DECODE", False)
     eager = fn()
     monkeypatch.setattr(gd, "GRAPH_DECODE", True)
@@ -65,3 +70,56 @@ def test_sampling_and_int8_cache(monkeypatch):
     eager, graphed = _both(monkeypatch, lambda: m.generate_batch(ctx, 24, 10, temperature=0.0))
     assert graphed[0][:7] == eager[0][:7]  # int8 rounding may differ later (kernel vs torch quantiser)
     assert all(len(r) == 16 for r in graphed)
+
+
+class _EagerGraph:
+    """Stands in for a captured graph: replay() runs the decode step eagerly."""
+
+    def __init__(self, dec):
+        self.dec = dec
+
+    def replay(self):
+        self.dec._step()
+
+
+def test_decode_program_graph_replay_matches_eager_program(monkeypatch):
+    m = _model(torch.bfloat16)
+    assert gd.GPTDecodeProgram.build(m) is not None, "GPT pattern must select the decode program"
+    ctx = torch.randint(0, 256, (3, 5), generator=torch.Generator().manual_seed(2)).tolist()
+    graphed = m.generate_batch(ctx, 16, 40, temperature=0.0)  # through the sliding window too
+    assert all(d.program is not None and isinstance(d.graph, torch.cuda.CUDAGraph) for d in m._graph_decoders.values())
+    m.__dict__.pop("_graph_decoders")
+
+    def eager_capture(self, last_tok, cache_len):
+        self._set_state(last_tok, cache_len)
+        self.graph = _EagerGraph(self)
+
+    monkeypatch.setattr(gd.GraphDecoder, "_capture", eager_capture)
+    eager = m.generate_batch(ctx, 16, 40, temperature=0.0)
+    assert graphed == eager
+
+
+def test_decode_program_step_matches_module_step():
+    m = _model(torch.bfloat16)
+    rows, cap = 3, 32
+    dec = gd.GraphDecoder(m, rows, cap, 0.0, None)
+    assert dec.program is not None
+    idx = torch.randint(0, 256, (rows, 7), device="cuda", generator=torch.Generator("cuda").manual_seed(3))
+    with torch.inference_mode():
+        dec.attach()
+        try:
+            m(idx[:, :6], skip_softmax=True)  # prefill through the modules
+            assert dec.cache.seq_len() == 6
+            tok = idx[:, 6:]
+            dec._set_state(tok, 6)
+            for p in dec.pos_layers:
+                p.position_offset_tensor = dec.cache.pos_t
+            dec.cache.graph_mode = True
+            acts, _ = m(tok, skip_softmax=True)
+            ref = acts[-1][:, -1, :].float()
+            got = dec.program.forward(tok, dec.cache).float()  # rewrites the same cache slot
+        finally:
+            dec.cache.graph_mode = False
+            dec.detach()
+    rel = (got - ref).norm() / ref.norm()
+    assert rel < 2e-2, rel

@@ -55,6 +55,20 @@ def test_add_layernorm_fwd(C):
     _close(y, ry, 0.06, 0.01)
 
 
+@pytest.mark.parametrize("C", [768, 4100])  # register-resident and looping kernels
+def test_add_layernorm_fwd_delta_bias(C):
+    x = torch.randn(33, C, device=DEV)
+    d = torch.randn(33, C, device=DEV).to(torch.bfloat16)
+    db = torch.randn(C, device=DEV)
+    w, b = torch.randn(C, device=DEV), torch.randn(C, device=DEV)
+    out = torch.empty_like(x)
+    y, _, _ = Nm.add_ln_fwd(x, d, out, w, b, 1e-5, delta_bias=db)
+    ref = x + d.float() + db
+    _close(out, ref, 1e-5)
+    ry, _, _ = Nm.reference_layer_norm(ref, w, b, 1e-5)
+    _close(y, ry, 0.06, 0.01)
+
+
 @pytest.mark.parametrize("C", [768, 1600])
 def test_layernorm_bwd(C):
     torch.manual_seed(1)
@@ -258,6 +272,11 @@ def test_decode_attention(dtype, D, B, H, Hkv, S, Tq):
     out = A.decode_attention(q, kc, vc, S)
     ref = A.reference_cache_attention(q.float(), kc[:, :, :S].float(), vc[:, :, :S].float(), S - Tq)
     _close(out, ref, 0.02, 0.01)
+    if Tq == 1:  # q read in place from fused QKV rows (a size-1 dim's stride is arbitrary)
+        rows = torch.randn(B, 1, (H + 2 * Hkv) * D, device=DEV).to(dtype)
+        rows[:, :, :H * D] = q.reshape(B, 1, H * D)
+        qv = rows[:, :, :H * D].view(B, 1, H, D)
+        _close(A.decode_attention(qv, kc, vc, S), out, 0.0)
 
 
 def test_decode_attention_int8():
@@ -407,3 +426,26 @@ def test_native_gemm(M, K, N, epi, kn):
     _close(out, ref, 0.02 * ref.abs().max().item(), msg="gemm")
     if act is not None:
         _close(act, F.gelu(out.float()), 0.02, msg="gelu epilogue")
+
+
+@pytest.mark.parametrize("M,K,N", [(64, 768, 2304), (64, 768, 768), (64, 3072, 768), (64, 768, 3072), (1, 768, 50304),
+                                   (17, 96, 40), (33, 768, 2304), (64, 768, 50257), (5, 4096, 1024)])
+@pytest.mark.parametrize("with_bias", [True, False])
+def test_skinny_gemm(M, K, N, with_bias):
+    """Decode-shaped GEMM vs fp32 torch: split-K (narrow N), masked rows/columns, repeated calls
+    (the split-K arrival counters must come back to zero), strided x rows."""
+    from penroz.ops import gemm as Gm
+    torch.manual_seed(M + K + N)
+    big = torch.randn(M, K + 64, device=DEV).to(torch.bfloat16)
+    x = big[:, 32:32 + K]  # row stride K + 64, 16-B aligned
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).to(torch.bfloat16)
+    b = torch.randn(N, device=DEV).to(torch.bfloat16) if with_bias else None
+    ref = x.float() @ w.float().t() + (b.float() if with_bias else 0)
+    ws, cnt = Gm.skinny_workspace(x.device)
+    for _ in range(3):
+        out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        split = _ext.kernels().skinny_gemm(x, w, b, out, ws, cnt)
+        _close(out, ref, 0.03, 0.01, f"split={split}")
+    assert int(cnt.abs().sum()) == 0, "split-K counters must be reset by the last arriver"
+    assert Gm.skinny_ok(x, w)
+    _close(Gm.skinny_linear(x.reshape(1, M, K), w, b).view(M, N), ref, 0.03, 0.01, "module path")
