@@ -19,6 +19,7 @@ void gelu_bwd(torch::Tensor dy, torch::Tensor x, int64_t approx, c10::optional<t
 void colsum(torch::Tensor x, torch::Tensor out);
 torch::Tensor gated_act_fwd(torch::Tensor g, torch::Tensor u, int64_t kind);
 std::vector<torch::Tensor> gated_act_bwd(torch::Tensor dy, torch::Tensor g, torch::Tensor u, int64_t kind);
+void transpose_bf16(torch::Tensor in, torch::Tensor out);
 void embedding_fwd(torch::Tensor idx, torch::Tensor wte, torch::Tensor wpe, int64_t off, torch::Tensor out,
                    c10::optional<torch::Tensor> off_dev);
 void embedding_bwd(torch::Tensor dout, torch::Tensor idx, torch::Tensor dwte, torch::Tensor dwpe, int64_t off);
@@ -78,6 +79,7 @@ PYBIND11_MODULE(penroz_kernels, m) {
   m.def("colsum", &colsum);
   m.def("gated_act_fwd", &gated_act_fwd);
   m.def("gated_act_bwd", &gated_act_bwd);
+  m.def("transpose_bf16", &transpose_bf16, "out [C, R] = in [R, C]^T (bf16, dims % 64 == 0)");
   m.def("embedding_fwd", &embedding_fwd, pybind11::arg("idx"), pybind11::arg("wte"), pybind11::arg("wpe"),
         pybind11::arg("off"), pybind11::arg("out"), pybind11::arg("off_dev") = pybind11::none());
   m.def("embedding_bwd", &embedding_bwd);

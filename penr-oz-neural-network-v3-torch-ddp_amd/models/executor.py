@@ -199,6 +199,7 @@ class GPTExecutor:
             self.segments.append((start, off))
         self.params_in_order = params
         self.refresh_shadow()
+        self._init_transposed()
         opt = self.model.optimizer
         if hasattr(opt, "attach_flat") and len(opt.param_groups) == 1:
             opt.attach_flat(params, self.flat, self.flat_grad, self.shadow, [self.offsets[id(p)] for p in params])
@@ -208,6 +209,53 @@ class GPTExecutor:
 
     def refresh_shadow(self):
         self.shadow.copy_(self.flat)
+
+    # ---- transposed bf16 weight copies for the data-gradient GEMMs ----------------------------
+    # dx = dy·W with W [out, in] as stored reaches 0.94-1.32 PF on hipBLASLt at GPT-2 shapes; with
+    # W transposed ([in, out], so both operands are reduction-contiguous as in the forward) it
+    # reaches 1.11-1.53 PF (profiles/dgrad_layout_r1.log). The copies are rebuilt from the bf16
+    # shadow at the start of every micro-step on the side stream (overlapping the forward; ~0.2
+    # ms of memory traffic) and the backward's first dgrad waits for them. PENROZ_DGRAD_T=0: off.
+    def _init_transposed(self):
+        import os
+        self._tw, self._t_ready = {}, None
+        if self.device.type != "cuda" or os.environ.get("PENROZ_DGRAD_T", "1") == "0" or not _ext.available():
+            return
+        s = self.spec
+        lins = [s.head] + [l for b in s.blocks for l in (b.qkv, b.proj, b.fc, b.fc2)]
+        ws = [l.weight for l in lins if l.weight.shape[0] % 64 == 0 and l.weight.shape[1] % 64 == 0]
+        self.shadow_t = torch.empty(sum(w.numel() for w in ws), dtype=torch.bfloat16, device=self.device)
+        off = 0
+        for w in ws:
+            n = w.numel()
+            self._tw[id(w)] = (w, self.shadow_t[off:off + n].view(w.shape[1], w.shape[0]))
+            off += n
+
+    def _refresh_transposed(self):
+        if not self._tw:
+            return
+        k = _ext.kernels()
+        side = getattr(self, "_side", None)
+        if side is None:
+            for w, t in self._tw.values():
+                k.transpose_bf16(self.bf16(w), t)
+            return
+        with torch.cuda.stream(side):
+            side.wait_stream(torch.cuda.current_stream(self.device))
+            for w, t in self._tw.values():
+                k.transpose_bf16(self.bf16(w), t)
+            self._t_ready = torch.cuda.Event()
+            self._t_ready.record(side)
+
+    def _dgrad_w(self, w: Tensor) -> Tensor:
+        """The weight operand of dx = dy·W: the transposed copy (viewed back as [out, in]) or the shadow."""
+        tw = self._tw.get(id(w)) if self._tw else None
+        if tw is None:
+            return self.bf16(w)
+        if self._t_ready is not None:
+            torch.cuda.current_stream(self.device).wait_event(self._t_ready)
+            self._t_ready = None
+        return tw[1].t()
 
     def bf16(self, p: Tensor) -> Tensor:
         off = self.offsets[id(p)]
@@ -428,6 +476,7 @@ class GPTExecutor:
         N, C = B * T, s.C
         seed = self._step_seed
         self._step_seed += 1000
+        self._refresh_transposed()
         with trace_range("forward"):
             self._forward(idx, training=True, dropout_seed=seed)
         cap = capture and self._captured is None
@@ -440,7 +489,7 @@ class GPTExecutor:
         self._defer_reductions(True)
         rows = fused_ops.cross_entropy_fwd_bwd(self.logits, targets.reshape(-1), scale / N)
         loss = rows.sum() * (scale / N)
-        torch.mm(self.logits, self.bf16(s.head.weight), out=self.d_c)
+        torch.mm(self.logits, self._dgrad_w(s.head.weight), out=self.d_c)
         self._wgrad(self.logits, self.lnf_out, s.head.weight)
         mean, rstd = self.statsf
         last = s.blocks[-1]
@@ -461,10 +510,10 @@ class GPTExecutor:
             d_f, dqkv = self._reuse(self.d_f2[l & 1]), self._reuse(self.dqkv2[l & 1])
             dres_bf = self.dresid_bf2[rb]
             # ---- MLP branch
-            torch.mm(dres_bf, self.bf16(b.fc2.weight), out=d_f)
+            torch.mm(dres_bf, self._dgrad_w(b.fc2.weight), out=d_f)
             self._wgrad(dres_bf, self.fcact[l], b.fc2.weight)
             act_ops.gelu_bwd(d_f, self.fcpre[l], s.gelu_approx, self.grad(b.fc.bias), out=d_f)
-            torch.mm(d_f, self.bf16(b.fc.weight), out=self.d_c)
+            torch.mm(d_f, self._dgrad_w(b.fc.weight), out=self.d_c)
             self._wgrad(d_f, self.ln2[l], b.fc.weight)
             _, _, mean, rstd = self.stats[l]
             rb ^= 1
@@ -472,12 +521,12 @@ class GPTExecutor:
             norm_ops.ln_bwd(self.d_c, self.resid_mid[l], mean, rstd, b.ln2.weight, self.dresid, True,
                             dres_bf, self.grad(b.ln2.weight), self.grad(b.ln2.bias), self.grad(b.proj.bias))
             # ---- attention branch
-            torch.mm(dres_bf, self.bf16(b.proj.weight), out=self.d_c)
+            torch.mm(dres_bf, self._dgrad_w(b.proj.weight), out=self.d_c)
             self._wgrad(dres_bf, self.att[l], b.proj.weight)
             attn_ops.flash_bwd(self.d_c.view(B, T, C), self.qkv[l].view(B, T, 3 * C), self.att[l].view(B, T, C),
                                self.lse[l], s.H, s.H, s.D, b.attn.dropout, seed + l, dqkv=dqkv.view(B, T, 3 * C))
             self._side_call(dqkv, lambda: fused_ops.colsum(dqkv, self.grad(b.qkv.bias)))
-            torch.mm(dqkv, self.bf16(b.qkv.weight), out=self.d_c)
+            torch.mm(dqkv, self._dgrad_w(b.qkv.weight), out=self.d_c)
             self._wgrad(dqkv, self.ln1[l], b.qkv.weight)
             mean, rstd, _, _ = self.stats[l]
             prev_bias = self.grad(s.blocks[l - 1].fc2.bias) if l > 0 else None

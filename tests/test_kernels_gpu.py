@@ -449,3 +449,11 @@ def test_skinny_gemm(M, K, N, with_bias):
     assert int(cnt.abs().sum()) == 0, "split-K counters must be reset by the last arriver"
     assert Gm.skinny_ok(x, w)
     _close(Gm.skinny_linear(x.reshape(1, M, K), w, b).view(M, N), ref, 0.03, 0.01, "module path")
+
+
+@pytest.mark.parametrize("R,C", [(768, 2304), (3072, 768), (64, 64), (50304, 768)])
+def test_transpose_bf16(R, C):
+    x = torch.randn(R, C, device=DEV).to(torch.bfloat16)
+    out = torch.empty(C, R, device=DEV, dtype=torch.bfloat16)
+    _ext.kernels().transpose_bf16(x, out)
+    assert torch.equal(out, x.t())
