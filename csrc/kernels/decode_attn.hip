@@ -96,7 +96,8 @@ __global__ void __launch_bounds__(256) decode_kernel(const TQ* __restrict__ q, c
                                                      float* __restrict__ ws_o, float* __restrict__ ws_ml, int B,
                                                      int Tq, int H, int Hkv, int cap, int S, int q_offset,
                                                      int splits, float scale, const int64_t* __restrict__ S_dev,
-                                                     int64_t q_rs) {
+                                                     int64_t q_rs, const TQ* __restrict__ k_new,
+                                                     const TQ* __restrict__ v_new, int64_t kv_rs) {
   constexpr int GMAX = GC ? GC : kMaxGroup;
   constexpr int RB = D * (int)sizeof(TK);                 // cache row bytes
   constexpr int KC = RB * 256 <= 32768 ? 256 : 32768 / RB;  // keys per chunk (V chunk <= 32 KB of LDS)
@@ -149,11 +150,19 @@ __global__ void __launch_bounds__(256) decode_kernel(const TQ* __restrict__ q, c
   // chunk's P·V. V goes raw to LDS (16-B pieces XOR-swizzled by row: conflict-free both ways).
   dec_u32x4 kr[CPT], vr[CPT];
   float ksc = 1.f, vsc = 1.f;
+  // Fused append (k_new given, Tq == 1): the newest key S-1 is read from this step's QKV rows
+  // instead of the cache, and the thread(s) holding it write it into cache slot S-1 (int8 caches:
+  // quantised per token exactly like kv_append) — one kernel less per layer and step.
+  constexpr bool SAME = std::is_same<TQ, TK>::value;
+  const size_t new_off = (size_t)b * kv_rs + (size_t)g * D;
   auto load_chunk = [&](int c0) {
     const int key = c0 + kk;
     const size_t row = head_base + (key < k1 ? key : c0);
-    const char* ksrc = reinterpret_cast<const char*>(kc + row * D) + part * CPT * 16;
-    const char* vsrc = reinterpret_cast<const char*>(vc + row * D) + part * CPT * 16;
+    const bool fresh = SAME && k_new != nullptr && key == S - 1;  // pointer select, no branch
+    const char* ksrc = reinterpret_cast<const char*>(fresh ? reinterpret_cast<const TK*>(k_new) + new_off : kc + row * D) +
+                       part * CPT * 16;
+    const char* vsrc = reinterpret_cast<const char*>(fresh ? reinterpret_cast<const TK*>(v_new) + new_off : vc + row * D) +
+                       part * CPT * 16;
 #pragma unroll
     for (int c = 0; c < CPT; ++c) kr[c] = *reinterpret_cast<const dec_u32x4*>(ksrc + 16 * c);
 #pragma unroll
@@ -179,6 +188,45 @@ __global__ void __launch_bounds__(256) decode_kernel(const TQ* __restrict__ q, c
 
   for (int c0 = k0; c0 < k1; c0 += KC) {
     const bool valid = c0 + kk < k1;
+    if (k_new != nullptr && c0 + kk == S - 1) {
+      const size_t row = head_base + (S - 1);
+      if constexpr (std::is_same<TK, int8_t>::value) {
+        static_assert(!std::is_same<TK, int8_t>::value || (TPK == 1 && CPT * 16 == D), "int8 row per thread");
+        // quantise the new K and V rows (the thread holds whole rows)
+        auto quant = [&](const TQ* src, dec_u32x4 (&raw)[CPT], float& sc_out, float* sc_dst, TK* dst) {
+          float m = 0.f;
+          for (int d = 0; d < D; ++d) m = fmaxf(m, fabsf(to_f(src[d])));
+          float sc = m / 127.f;
+          if (sc == 0.f) sc = 1.f;
+#pragma unroll
+          for (int c = 0; c < CPT; ++c) {
+            uint32_t w[4];
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+              uint32_t acc = 0;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const float x = fminf(fmaxf(rintf(to_f(src[16 * c + 4 * q4 + e]) / sc), -128.f), 127.f);
+                acc |= ((uint32_t)(uint8_t)(int8_t)x) << (8 * e);
+              }
+              w[q4] = acc;
+            }
+            raw[c] = (dec_u32x4){w[0], w[1], w[2], w[3]};
+            *reinterpret_cast<dec_u32x4*>(dst + row * D + 16 * c) = raw[c];
+          }
+          sc_out = sc;
+          sc_dst[row] = sc;
+        };
+        quant(k_new + new_off, kr, ksc, const_cast<float*>(ks), const_cast<TK*>(kc));
+        quant(v_new + new_off, vr, vsc, const_cast<float*>(vs), const_cast<TK*>(vc));
+      } else {
+#pragma unroll
+        for (int c = 0; c < CPT; ++c) {
+          *reinterpret_cast<dec_u32x4*>(reinterpret_cast<char*>(const_cast<TK*>(kc) + row * D) + part * CPT * 16 + 16 * c) = kr[c];
+          *reinterpret_cast<dec_u32x4*>(reinterpret_cast<char*>(const_cast<TK*>(vc) + row * D) + part * CPT * 16 + 16 * c) = vr[c];
+        }
+      }
+    }
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
       const int pc = part * CPT + c;
@@ -358,9 +406,12 @@ using namespace penroz;
 // seq_len_dev (optional int64 [1] on the device): the cache length is read by the kernel at run
 // time (S / q_offset are then only upper bounds used to size the launch) — lets a captured HIP
 // graph replay the same decode step at every position.
+// k_new / v_new (optional, Tq == 1): this step's K / V rows [B, 1, Hkv, D] (views into the fused
+// QKV rows allowed): appended at slot S-1 by the kernel itself (see decode_kernel).
 torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c10::optional<torch::Tensor> k_scale,
                           c10::optional<torch::Tensor> v_scale, int64_t S, int64_t q_offset, double scale,
-                          c10::optional<torch::Tensor> seq_len_dev) {
+                          c10::optional<torch::Tensor> seq_len_dev, c10::optional<torch::Tensor> k_new,
+                          c10::optional<torch::Tensor> v_new) {
   TORCH_CHECK(q.is_cuda() && q.dim() == 4, "q must be [B, Tq, H, D]");
   // q may be a view into the fused QKV rows: unit dim stride, packed heads, uniform row stride
   // (a size-1 Tq dim may carry any stride: the row stride is then stride(0))
@@ -394,6 +445,19 @@ torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c
                 "seq_len_dev must be a device int64 [1]");
     sdev = seq_len_dev->data_ptr<int64_t>();
   }
+  const bool fuse = k_new.has_value() && k_new->defined();
+  int64_t kv_rs = 0;
+  if (fuse) {
+    TORCH_CHECK(v_new.has_value() && v_new->defined() && Tq == 1, "fused append: k_new and v_new, Tq == 1");
+    for (const auto* t : {&*k_new, &*v_new}) {
+      TORCH_CHECK(t->scalar_type() == q.scalar_type() && t->dim() == 4 && t->size(0) == B && t->size(1) == 1 &&
+                      t->size(2) == Hkv && t->size(3) == D && t->stride(3) == 1 && t->stride(2) == D &&
+                      reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0,
+                  "k_new / v_new must be [B, 1, Hkv, D] with packed heads");
+    }
+    TORCH_CHECK(k_new->stride(0) == v_new->stride(0) && k_new->stride(0) % 8 == 0, "k_new / v_new row stride");
+    kv_rs = k_new->stride(0);
+  }
   const float* ksp = quant ? k_scale->data_ptr<float>() : nullptr;
   const float* vsp = quant ? v_scale->data_ptr<float>() : nullptr;
   auto stream = at::hip::getCurrentHIPStream();
@@ -405,10 +469,12 @@ torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c
     const TK* kp = reinterpret_cast<const TK*>(kc.data_ptr());
     const TK* vp = reinterpret_cast<const TK*>(vc.data_ptr());
     TQ* op = reinterpret_cast<TQ*>(out.data_ptr());
+    const TQ* knp = fuse ? reinterpret_cast<const TQ*>(k_new->data_ptr()) : nullptr;
+    const TQ* vnp = fuse ? reinterpret_cast<const TQ*>(v_new->data_ptr()) : nullptr;
     const int G = H / Hkv;
 #define PENROZ_DECODE(DD, GC)                                                                                   \
   hipLaunchKernelGGL((decode_kernel<DD, GC, TQ, TK>), grid, dim3(256), 0, stream, qp, kp, vp, ksp, vsp, op, wo, wm, \
-                     B, Tq, H, Hkv, cap, (int)S, (int)q_offset, splits, (float)scale, sdev, q_rs)
+                     B, Tq, H, Hkv, cap, (int)S, (int)q_offset, splits, (float)scale, sdev, q_rs, knp, vnp, kv_rs)
 #define PENROZ_DECODE_G(DD)              \
   switch (G) {                           \
     case 1: PENROZ_DECODE(DD, 1); break; \

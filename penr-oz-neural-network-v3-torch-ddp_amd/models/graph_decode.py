@@ -12,9 +12,9 @@ feedback of the sampled token into the next step's input — is captured ONCE pe
 replayed. Everything that changes between steps lives on the device:
 
 * ``StaticKVCache.pos_t`` / ``len_t``: the slot this step writes and the cache length after it;
-  one kernel appends K/V (read in place from the fused QKV rows, int8-quantised for TurboQuant)
-  at ``pos_t`` and the decode-attention kernel reads q in place and ``len_t`` at run time
-  (``csrc/kernels/decode_attn.hip``: ``kv_append``, ``seq_len_dev``);
+  the decode-attention kernel reads q in place and ``len_t`` at run time, and appends this step's
+  K/V (read in place from the fused QKV rows, int8-quantised for TurboQuant) at slot
+  ``len_t - 1 = pos_t`` itself (``csrc/kernels/decode_attn.hip``: ``k_new``, ``seq_len_dev``);
 * ``PositionEmbedding.position_offset_tensor``: the learned position gathered at ``pos_t``;
 * the uniforms of temperature / top-k sampling are drawn on the device (graph-safe Philox);
 * the sampled token is copied into the step's input buffer and into a burst output buffer;
@@ -49,6 +49,9 @@ GRAPH_DECODE = os.environ.get("PENROZ_GRAPH_DECODE", "1") != "0"
 # GPT-2-pattern bf16 models: the captured step is the explicit program below instead of the
 # module forward ("0": module forward, numerically identical to the eager decode path)
 DECODE_PROGRAM = os.environ.get("PENROZ_DECODE_PROGRAM", "1") != "0"
+# the decode-attention kernel appends the step's K/V itself (one kernel less per layer); "0":
+# separate kv_append kernel
+FUSED_APPEND = os.environ.get("PENROZ_FUSED_APPEND", "1") != "0"
 # decode rows up to which the linears use the decode-shaped MFMA kernel instead of hipBLASLt
 # (measured: a win at batch 1, none at batch 64 — profiles/bench_r1_decode_graph.log)
 SKINNY_MAX_ROWS = int(os.environ.get("PENROZ_SKINNY_MAX_ROWS", "16"))
@@ -74,6 +77,8 @@ class StaticKVCache(_GraphMode, kvc.KVCache):
         # k, v, q are views into this layer's fused QKV rows: one kernel appends K/V at pos_t,
         # the decode kernel reads q in place and the cache length from len_t
         kc, vc = self._k[l], self._v[l]
+        if FUSED_APPEND:
+            return attn_ops.decode_attention(q, kc, vc, kc.shape[2], seq_len_dev=self.len_t, k_new=k, v_new=v)
         _ext.kernels().kv_append(k, v, kc, vc, None, None, self.pos_t, 0)
         return attn_ops.decode_attention(q, kc, vc, kc.shape[2], seq_len_dev=self.len_t)
 
@@ -81,8 +86,11 @@ class StaticKVCache(_GraphMode, kvc.KVCache):
 class StaticTurboKVCache(_GraphMode, kvc.TurboQuantKVCache):
     def _attend_graph(self, l: int, q: Tensor, k: Tensor, v: Tensor) -> Tensor:
         # same per-token int8 quantiser as the eager append (kv_quantize)
-        _ext.kernels().kv_append(k, v, self._k[l], self._v[l], self._sk[l], self._sv[l], self.pos_t, 0)
         self._dtype[l] = k.dtype
+        if FUSED_APPEND:
+            return attn_ops.decode_attention(q, self._k[l], self._v[l], self._k[l].shape[2], self._sk[l],
+                                             self._sv[l], seq_len_dev=self.len_t, k_new=k, v_new=v)
+        _ext.kernels().kv_append(k, v, self._k[l], self._v[l], self._sk[l], self._sv[l], self.pos_t, 0)
         return attn_ops.decode_attention(q, self._k[l], self._v[l], self._k[l].shape[2], self._sk[l], self._sv[l],
                                          seq_len_dev=self.len_t)
 

@@ -128,7 +128,8 @@ def reference_cache_attention(q: Tensor, k: Tensor, v: Tensor, q_offset: int) ->
 
 def decode_attention(q: Tensor, k_cache: Tensor, v_cache: Tensor, seq_len: int,
                      k_scale: Tensor | None = None, v_scale: Tensor | None = None,
-                     seq_len_dev: Tensor | None = None) -> Tensor:
+                     seq_len_dev: Tensor | None = None, k_new: Tensor | None = None,
+                     v_new: Tensor | None = None) -> Tensor:
     """Attention of ``q [B, Tq, H, D]`` against the first ``seq_len`` cache slots.
 
     Cache layout ``[B, Hkv, cap, D]`` (bf16/fp16/fp32, or int8 with per-token fp32 scales
@@ -136,6 +137,8 @@ def decode_attention(q: Tensor, k_cache: Tensor, v_cache: Tensor, seq_len: int,
     GPU: split-K decode kernel (``csrc/kernels/decode_attn.hip``). ``seq_len_dev`` (device int64
     [1], GPU only): the kernel reads the cache length at run time (``seq_len`` is then the
     capacity bound) — the form a captured HIP graph replays at every position.
+    ``k_new`` / ``v_new`` ([B, 1, Hkv, D], GPU kernel only): this step's K / V, appended at slot
+    ``seq_len - 1`` by the attention kernel itself (int8 caches: quantised as ``kv_quantize_into``).
     """
     Tq = q.shape[1]
     if use_kernels(q) and q.shape[-1] in DECODE_HEAD_DIMS:
@@ -144,7 +147,9 @@ def decode_attention(q: Tensor, k_cache: Tensor, v_cache: Tensor, seq_len: int,
                 and (Tq == 1 or q.stride(0) == q.shape[1] * q.stride(1))):
             q = q.contiguous()
         return kernels().decode_attn(q, k_cache, v_cache, k_scale, v_scale, int(seq_len),
-                                     int(seq_len - Tq), 1.0 / math.sqrt(q.shape[-1]), seq_len_dev)
+                                     int(seq_len - Tq), 1.0 / math.sqrt(q.shape[-1]), seq_len_dev, k_new, v_new)
+    if k_new is not None:
+        raise ValueError("fused KV append needs the decode kernel")
     if seq_len_dev is not None:
         seq_len = int(seq_len_dev.item())
     k = k_cache[:, :, :seq_len]

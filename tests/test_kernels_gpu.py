@@ -457,3 +457,36 @@ def test_transpose_bf16(R, C):
     out = torch.empty(C, R, device=DEV, dtype=torch.bfloat16)
     _ext.kernels().transpose_bf16(x, out)
     assert torch.equal(out, x.t())
+
+
+@pytest.mark.parametrize("dtype,int8", [(torch.bfloat16, False), (torch.float32, False), (torch.float16, False),
+                                        (torch.bfloat16, True)])
+@pytest.mark.parametrize("D,H,Hkv,S", [(64, 12, 12, 100), (128, 8, 2, 300), (64, 4, 1, 1), (128, 4, 4, 257)])
+def test_decode_attention_fused_append(dtype, int8, D, H, Hkv, S):
+    """Decode attention that appends this step's K/V itself (slot S-1, read from the fused QKV
+    rows) == kv_append followed by decode attention: same output, same cache contents."""
+    torch.manual_seed(S + D)
+    B, cap = 3, 320
+    rows = torch.randn(B, 1, (H + 2 * Hkv) * D, device=DEV).to(dtype)
+    q = rows[:, :, :H * D].view(B, 1, H, D)
+    k = rows[:, :, H * D:(H + Hkv) * D].view(B, 1, Hkv, D)
+    v = rows[:, :, (H + Hkv) * D:].view(B, 1, Hkv, D)
+    sl = torch.tensor([S], device=DEV)
+    pos = torch.tensor([S - 1], device=DEV)
+    if int8:
+        kc = torch.randint(-128, 127, (B, Hkv, cap, D), device=DEV, dtype=torch.int8)
+        vc = torch.randint(-128, 127, (B, Hkv, cap, D), device=DEV, dtype=torch.int8)
+        ks, vs = torch.rand(B, Hkv, cap, device=DEV) * 0.02, torch.rand(B, Hkv, cap, device=DEV) * 0.02
+    else:
+        kc = torch.randn(B, Hkv, cap, D, device=DEV).to(dtype)
+        vc = torch.randn(B, Hkv, cap, D, device=DEV).to(dtype)
+        ks = vs = None
+    c1 = [t.clone() if t is not None else None for t in (kc, vc, ks, vs)]
+    c2 = [t.clone() if t is not None else None for t in (kc, vc, ks, vs)]
+    _ext.kernels().kv_append(k, v, c1[0], c1[1], c1[2], c1[3], pos, 0)
+    ref = A.decode_attention(q, c1[0], c1[1], cap, c1[2], c1[3], seq_len_dev=sl)
+    out = A.decode_attention(q, c2[0], c2[1], cap, c2[2], c2[3], seq_len_dev=sl, k_new=k, v_new=v)
+    for a, b in zip(c1, c2):
+        if a is not None:
+            assert torch.equal(a, b), "cache contents differ"
+    _close(out, ref, 1e-6 if dtype != torch.float16 else 1e-3)
