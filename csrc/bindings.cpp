@@ -40,6 +40,9 @@ void multi_tensor_adam(std::vector<torch::Tensor> ps, std::vector<torch::Tensor>
 // sampling.hip
 torch::Tensor sample_tokens(torch::Tensor logits, c10::optional<torch::Tensor> uniform, double temperature,
                             int64_t top_k);
+void sample_step(torch::Tensor logits, double temperature, int64_t top_k, torch::Tensor seed, torch::Tensor step,
+                 torch::Tensor idx_out, torch::Tensor out_buf);
+void decode_advance(torch::Tensor a, torch::Tensor b, torch::Tensor c);
 // decode_attn.hip
 torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c10::optional<torch::Tensor> k_scale,
                           c10::optional<torch::Tensor> v_scale, int64_t S, int64_t q_offset, double scale,
@@ -92,6 +95,8 @@ PYBIND11_MODULE(penroz_kernels, m) {
   m.def("adam_step", &adam_step);
   m.def("multi_tensor_adam", &multi_tensor_adam);
   m.def("sample_tokens", &sample_tokens);
+  m.def("sample_step", &sample_step, "decode-step sampler: device-hashed uniforms, writes idx_out and out_buf[:, *step]");
+  m.def("decode_advance", &decode_advance, "+1 on three device int64 scalars");
   m.def("decode_attn", &decode_attn, pybind11::arg("q"), pybind11::arg("kc"), pybind11::arg("vc"), pybind11::arg("k_scale"),
         pybind11::arg("v_scale"), pybind11::arg("S"), pybind11::arg("q_offset"), pybind11::arg("scale"),
         pybind11::arg("seq_len_dev") = pybind11::none(), pybind11::arg("k_new") = pybind11::none(),

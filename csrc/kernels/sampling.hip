@@ -15,6 +15,31 @@ namespace penroz {
 
 constexpr int kST = 1024;
 
+// Where a row's uniform comes from and where its token goes. Default: uni[row] in, out[row] out.
+// The graph-replayed decode step (sample_step) instead hashes the uniform from (*seed, *step, row)
+// on the device and also writes the token into out2[row, *step] — the sampler then is the whole
+// token feedback (no RNG kernel, no copy / index kernels).
+struct SampleIO {
+  const float* uni;
+  const int64_t* seed;
+  const int64_t* step;
+  int64_t* out;
+  int64_t* out2;
+  int64_t out2_stride;
+  __device__ __forceinline__ float uniform(int row) const {
+    if (uni) return uni[row];
+    uint64_t z = (uint64_t)*seed + 0x9E3779B97F4A7C15ull * (uint64_t)(*step + 1) + 0xD1B54A32D192ED03ull * (uint64_t)(row + 1);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;  // splitmix64 finaliser
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return (float)(z >> 40) * (1.f / 16777216.f);  // 24 bits: [0, 1)
+  }
+  __device__ __forceinline__ void write(int row, int64_t tok) const {
+    out[row] = tok;
+    if (out2) out2[(size_t)row * out2_stride + *step] = tok;
+  }
+};
+
 __device__ __forceinline__ uint32_t order_key(float f) {
   const uint32_t u = __float_as_uint(f);
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
@@ -54,8 +79,8 @@ __device__ __forceinline__ void pick_digit(const uint32_t* bins, uint32_t* wtot,
 }
 
 template <typename T>
-__global__ void __launch_bounds__(kST) sample_kernel(const T* __restrict__ logits, const float* __restrict__ uni,
-                                                     int64_t* __restrict__ out, int V, float temperature, int top_k) {
+__global__ void __launch_bounds__(kST) sample_kernel(const T* __restrict__ logits, const SampleIO io, int V,
+                                                     float temperature, int top_k) {
   __shared__ float fred[kST / 64];
   __shared__ int ired[kST / 64];
   __shared__ uint32_t hist[256];
@@ -93,7 +118,7 @@ __global__ void __launch_bounds__(kST) sample_kernel(const T* __restrict__ logit
   __syncthreads();
   const float gmax = fred[0];
   if (temperature == 0.f) {
-    if (t == 0) out[row] = result;
+    if (t == 0) io.write(row, result);
     return;
   }
 
@@ -135,7 +160,7 @@ __global__ void __launch_bounds__(kST) sample_kernel(const T* __restrict__ logit
     __syncthreads();
   }
   const float total = scan[kST - 1];
-  const float target = uni[row] * total;
+  const float target = io.uniform(row) * total;
   const float before = t > 0 ? scan[t - 1] : 0.f;
   if (s > 0.f && target >= before && target < before + s) {
     float acc = before;
@@ -150,7 +175,7 @@ __global__ void __launch_bounds__(kST) sample_kernel(const T* __restrict__ logit
     if (pick >= 0) result = pick;
   }
   __syncthreads();
-  if (t == 0) out[row] = result;
+  if (t == 0) io.write(row, result);
 }
 
 // Register-resident variant (V % 8 == 0, V <= 8·1024·CPT): the row is read from memory ONCE
@@ -162,9 +187,8 @@ __global__ void __launch_bounds__(kST) sample_kernel(const T* __restrict__ logit
 constexpr int kRT = 512;  // 256 VGPRs per thread: room for a 104-logit slice
 
 template <int CPT, typename T>
-__global__ void __launch_bounds__(kRT) sample_reg_kernel(const T* __restrict__ logits, const float* __restrict__ uni,
-                                                         int64_t* __restrict__ out, int V, float temperature,
-                                                         int top_k) {
+__global__ void __launch_bounds__(kRT) sample_reg_kernel(const T* __restrict__ logits, const SampleIO io, int V,
+                                                         float temperature, int top_k) {
   __shared__ uint32_t hist[256 * 32];
   __shared__ uint32_t bins[256];
   __shared__ uint32_t wtot[4];
@@ -241,7 +265,7 @@ __global__ void __launch_bounds__(kRT) sample_reg_kernel(const T* __restrict__ l
   __syncthreads();
   const float gmax = fred[0];
   if (temperature == 0.f) {
-    if (t == 0) out[row] = result;
+    if (t == 0) io.write(row, result);
     return;
   }
   // ---- top-k threshold: radix select over order-preserving keys (4 × 8-bit digits). Counting
@@ -317,7 +341,7 @@ __global__ void __launch_bounds__(kRT) sample_reg_kernel(const T* __restrict__ l
   }
   __syncthreads();
   const float before = wsum[w] + incl - s;
-  const float target = uni[row] * total_s;
+  const float target = io.uniform(row) * total_s;
   if (s > 0.f && target >= before && target < before + s) {
     float acc = before;
     int pick = -1;
@@ -337,37 +361,29 @@ __global__ void __launch_bounds__(kRT) sample_reg_kernel(const T* __restrict__ l
     if (pick >= 0) result = pick;
   }
   __syncthreads();
-  if (t == 0) out[row] = result;
+  if (t == 0) io.write(row, result);
 }
 
 }  // namespace penroz
 
 using namespace penroz;
 
-torch::Tensor sample_tokens(torch::Tensor logits, c10::optional<torch::Tensor> uniform, double temperature,
-                            int64_t top_k) {
+static void launch_sample(const torch::Tensor& logits, const SampleIO& io, double temperature, int64_t top_k) {
   TORCH_CHECK(logits.is_cuda() && logits.is_contiguous() && logits.dim() == 2);
   const int B = logits.size(0), V = logits.size(1);
-  auto out = torch::empty({B, 1}, logits.options().dtype(torch::kInt64));
-  torch::Tensor u;
-  if (uniform.has_value() && uniform->defined()) u = uniform->to(torch::kFloat32).contiguous();
-  else u = torch::zeros({B}, logits.options().dtype(torch::kFloat32));
-  TORCH_CHECK(u.numel() == B && u.is_cuda());
   auto stream = at::hip::getCurrentHIPStream();
   int chunks = (V / 8 + kRT - 1) / kRT;
   for (int c : {1, 2, 3, 4, 6, 8, 10, 13, 16})  // instantiated slice sizes
     if (chunks <= c) { chunks = c; break; }
   const bool fits = chunks <= (logits.scalar_type() == torch::kBFloat16 ? 16 : 8);
+  const float tt = (float)temperature;
+  const int kk = (int)top_k;
   if (V % 8 == 0 && fits && logits.scalar_type() != torch::kFloat16) {
     auto launch = [&](auto tag) {
       using T = decltype(tag);
       const T* lp = reinterpret_cast<const T*>(logits.data_ptr());
-      float* up = u.data_ptr<float>();
-      int64_t* op = out.data_ptr<int64_t>();
-      const float tt = (float)temperature;
-      const int kk = (int)top_k;
 #define PENROZ_SAMPLE_REG(C) \
-  case C: hipLaunchKernelGGL((sample_reg_kernel<C, T>), dim3(B), dim3(kRT), 0, stream, lp, up, op, V, tt, kk); break;
+  case C: hipLaunchKernelGGL((sample_reg_kernel<C, T>), dim3(B), dim3(kRT), 0, stream, lp, io, V, tt, kk); break;
       switch (chunks) {
         PENROZ_SAMPLE_REG(1) PENROZ_SAMPLE_REG(2) PENROZ_SAMPLE_REG(3) PENROZ_SAMPLE_REG(4) PENROZ_SAMPLE_REG(6)
         PENROZ_SAMPLE_REG(8)
@@ -380,19 +396,59 @@ torch::Tensor sample_tokens(torch::Tensor logits, c10::optional<torch::Tensor> u
     };
     if (logits.scalar_type() == torch::kBFloat16) launch(bf16{});
     else launch(float{});
-    return out;
+    return;
   }
   if (logits.scalar_type() == torch::kBFloat16)
     hipLaunchKernelGGL(sample_kernel<bf16>, dim3(B), dim3(kST), 0, stream,
-                       reinterpret_cast<const bf16*>(logits.data_ptr()), u.data_ptr<float>(), out.data_ptr<int64_t>(),
-                       V, (float)temperature, (int)top_k);
+                       reinterpret_cast<const bf16*>(logits.data_ptr()), io, V, tt, kk);
   else if (logits.scalar_type() == torch::kFloat32)
-    hipLaunchKernelGGL(sample_kernel<float>, dim3(B), dim3(kST), 0, stream, logits.data_ptr<float>(),
-                       u.data_ptr<float>(), out.data_ptr<int64_t>(), V, (float)temperature, (int)top_k);
+    hipLaunchKernelGGL(sample_kernel<float>, dim3(B), dim3(kST), 0, stream, logits.data_ptr<float>(), io, V, tt, kk);
   else if (logits.scalar_type() == torch::kFloat16)
     hipLaunchKernelGGL(sample_kernel<__half>, dim3(B), dim3(kST), 0, stream,
-                       reinterpret_cast<const __half*>(logits.data_ptr()), u.data_ptr<float>(),
-                       out.data_ptr<int64_t>(), V, (float)temperature, (int)top_k);
+                       reinterpret_cast<const __half*>(logits.data_ptr()), io, V, tt, kk);
   else TORCH_CHECK(false, "unsupported logits dtype");
+}
+
+torch::Tensor sample_tokens(torch::Tensor logits, c10::optional<torch::Tensor> uniform, double temperature,
+                            int64_t top_k) {
+  TORCH_CHECK(logits.is_cuda() && logits.is_contiguous() && logits.dim() == 2);
+  const int B = logits.size(0);
+  auto out = torch::empty({B, 1}, logits.options().dtype(torch::kInt64));
+  torch::Tensor u;
+  if (uniform.has_value() && uniform->defined()) u = uniform->to(torch::kFloat32).contiguous();
+  else u = torch::zeros({B}, logits.options().dtype(torch::kFloat32));
+  TORCH_CHECK(u.numel() == B && u.is_cuda());
+  launch_sample(logits, SampleIO{u.data_ptr<float>(), nullptr, nullptr, out.data_ptr<int64_t>(), nullptr, 0}, temperature,
+                top_k);
   return out;
+}
+
+// Graph-replayed decode: token of row r -> idx_out[r] and out_buf[r, *step]; uniforms hashed
+// from (seed, *step, r) on the device. Then one tiny kernel advances the step counters.
+void sample_step(torch::Tensor logits, double temperature, int64_t top_k, torch::Tensor seed, torch::Tensor step,
+                 torch::Tensor idx_out, torch::Tensor out_buf) {
+  TORCH_CHECK(logits.dim() == 2 && step.is_cuda() && step.scalar_type() == torch::kInt64 && step.numel() == 1);
+  TORCH_CHECK(seed.is_cuda() && seed.scalar_type() == torch::kInt64 && seed.numel() == 1, "seed: device int64 [1]");
+  const int B = logits.size(0);
+  TORCH_CHECK(idx_out.scalar_type() == torch::kInt64 && idx_out.numel() == B && idx_out.is_contiguous());
+  TORCH_CHECK(out_buf.scalar_type() == torch::kInt64 && out_buf.dim() == 2 && out_buf.size(0) == B &&
+              out_buf.stride(1) == 1, "out_buf [B, n] int64");
+  launch_sample(logits, SampleIO{nullptr, seed.data_ptr<int64_t>(), step.data_ptr<int64_t>(), idx_out.data_ptr<int64_t>(),
+                                 out_buf.data_ptr<int64_t>(), out_buf.stride(0)}, temperature, top_k);
+}
+
+__global__ void decode_advance_kernel(int64_t* a, int64_t* b, int64_t* c) {
+  if (threadIdx.x == 0) {
+    ++*a;
+    ++*b;
+    ++*c;
+  }
+}
+
+// +1 on three device int64 scalars (cache position, cache length, burst step) in one launch
+void decode_advance(torch::Tensor a, torch::Tensor b, torch::Tensor c) {
+  for (const auto* t : {&a, &b, &c})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == torch::kInt64 && t->numel() == 1, "decode_advance: int64 [1]");
+  hipLaunchKernelGGL(decode_advance_kernel, dim3(1), dim3(64), 0, at::hip::getCurrentHIPStream(),
+                     a.data_ptr<int64_t>(), b.data_ptr<int64_t>(), c.data_ptr<int64_t>());
 }

@@ -16,8 +16,9 @@ replayed. Everything that changes between steps lives on the device:
   K/V (read in place from the fused QKV rows, int8-quantised for TurboQuant) at slot
   ``len_t - 1 = pos_t`` itself (``csrc/kernels/decode_attn.hip``: ``k_new``, ``seq_len_dev``);
 * ``PositionEmbedding.position_offset_tensor``: the learned position gathered at ``pos_t``;
-* the uniforms of temperature / top-k sampling are drawn on the device (graph-safe Philox);
-* the sampled token is copied into the step's input buffer and into a burst output buffer;
+* the sampler hashes its uniforms on the device from (per-burst seed, step, row) and writes the
+  token straight into the next step's input and the burst output buffer; one tiny kernel then
+  advances the position / length / step counters;
 * the step's ``nn.Linear`` GEMMs (M = rows ≤ 64) run on the decode-shaped MFMA kernel
   (``ops/gemm.py: decode_gemms``, ``csrc/kernels/skinny_gemm.hip``).
 
@@ -199,6 +200,7 @@ class GraphDecoder:
         self.idx = torch.zeros(rows, 1, dtype=torch.long, device=self.device)
         self.out = torch.zeros(rows, capacity, dtype=torch.long, device=self.device)
         self.step_t = torch.zeros(1, dtype=torch.long, device=self.device)
+        self.seed_t = torch.zeros(1, dtype=torch.long, device=self.device)  # per-run sampling salt
         self.graph: torch.cuda.CUDAGraph | None = None
         gemm_ops.skinny_workspace(self.device)  # zeroed counters exist before any capture
         self.program = GPTDecodeProgram.build(model)
@@ -228,18 +230,29 @@ class GraphDecoder:
                     acts, _ = self.model(self.idx, skip_softmax=True)
                 logits = acts[-1]
                 last = logits[:, -1, :] if logits.ndim == 3 else logits
-            nxt = samp_ops.sample(last, self.temperature, self.top_k, device_rng=True)
-            torch.add(nxt, 0, out=self.idx)  # a kernel, not a memcpy node
-            self.out.index_copy_(1, self.step_t, nxt)
-            self.cache.pos_t.add_(1)
-            self.cache.len_t.add_(1)
-            self.step_t.add_(1)
+            if _ext.available() and last.is_cuda:
+                # one sampler kernel writes the token into the next step's input and the burst
+                # buffer (uniforms hashed on the device), one kernel advances the counters
+                V = last.shape[-1]
+                k = 0 if self.top_k is None or self.top_k >= V else int(self.top_k)
+                _ext.kernels().sample_step(last.contiguous(), self.temperature, k, self.seed_t, self.step_t,
+                                           self.idx, self.out)
+                _ext.kernels().decode_advance(self.cache.pos_t, self.cache.len_t, self.step_t)
+            else:
+                nxt = samp_ops.sample(last, self.temperature, self.top_k, device_rng=True)
+                torch.add(nxt, 0, out=self.idx)  # a kernel, not a memcpy node
+                self.out.index_copy_(1, self.step_t, nxt)
+                self.cache.pos_t.add_(1)
+                self.cache.len_t.add_(1)
+                self.step_t.add_(1)
         finally:
             self.cache.graph_mode = False
             for p in self.pos_layers:
                 p.position_offset_tensor = None
 
     def _set_state(self, last_tok: Tensor, cache_len: int):
+        # drawn from torch's generator: reproducible under torch.manual_seed, fresh every burst
+        self.seed_t.fill_(int(torch.randint(0, 2 ** 62, (1,)).item()))
         self.idx.copy_(last_tok)
         self.cache.pos_t.fill_(cache_len)
         self.cache.len_t.fill_(cache_len + 1)

@@ -490,3 +490,35 @@ def test_decode_attention_fused_append(dtype, int8, D, H, Hkv, S):
         if a is not None:
             assert torch.equal(a, b), "cache contents differ"
     _close(out, ref, 1e-6 if dtype != torch.float16 else 1e-3)
+
+
+@pytest.mark.parametrize("V,dt", [(50304, torch.bfloat16), (50257, torch.bfloat16), (4096, torch.float32)])
+def test_sample_step_and_advance(V, dt):
+    """Graph-decode sampler: token -> idx_out[r] and out_buf[r, *step]; device-hashed uniforms
+    give valid top-k draws that follow the softmax; decode_advance bumps three counters."""
+    K = _ext.kernels()
+    B, n = 64, 8
+    torch.manual_seed(V)
+    logits = (torch.randn(B, V, device=DEV) * 2).to(dt)
+    seed, step = torch.tensor([1234], device=DEV), torch.tensor([3], device=DEV)
+    idx = torch.zeros(B, 1, dtype=torch.long, device=DEV)
+    out = torch.full((B, n), -1, dtype=torch.long, device=DEV)
+    K.sample_step(logits, 0.0, 0, seed, step, idx, out)
+    assert torch.equal(idx.view(-1), logits.float().argmax(-1)) and torch.equal(out[:, 3], idx.view(-1))
+    assert bool((out[:, [0, 1, 2, 4, 5, 6, 7]] == -1).all())
+    fifth = logits.float().topk(5, dim=-1).values[:, -1:]
+    K.sample_step(logits, 1.0, 5, seed, step, idx, out)
+    assert bool((logits.float().gather(1, idx) >= fifth).all()) and torch.equal(out[:, 3], idx.view(-1))
+    a, b, c = (torch.tensor([x], device=DEV) for x in (5, 6, 7))
+    K.decode_advance(a, b, c)
+    assert (a.item(), b.item(), c.item()) == (6, 7, 8)
+    # distribution over many (seed, step) pairs of one 3-way row
+    row = torch.full((1, V), -30.0, device=DEV)
+    row[0, :3] = torch.tensor([1.0, 0.5, 0.0], device=DEV)
+    rows = row.to(dt).expand(B, V).contiguous()
+    counts = torch.zeros(3)
+    for s in range(40):
+        seed.fill_(s * 7919)
+        K.sample_step(rows, 1.0, 0, seed, step, idx, out)
+        counts += torch.bincount(idx.view(-1).cpu(), minlength=3)[:3].float()
+    assert torch.allclose(counts / counts.sum(), torch.softmax(torch.tensor([1.0, 0.5, 0.0]), -1), atol=0.03)
