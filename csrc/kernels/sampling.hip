@@ -268,6 +268,128 @@ __global__ void __launch_bounds__(kRT) sample_reg_kernel(const T* __restrict__ l
     if (t == 0) io.write(row, result);
     return;
   }
+  // ---- top-k, k <= 512: rank by counting. (1) The k-th largest of the 512 per-thread maxima,
+  // L, bounds the row's k-th largest from below (k maxima, so k elements, are >= L); each
+  // thread ranks its maximum against the other 511 (LDS broadcast reads). (2) The elements >= L —
+  // typically not many more than k — are compacted into LDS in index order, ranked the same way
+  // (value descending, index ascending), and the k best are laid out in rank order. (3) Softmax
+  // and the inverse-CDF draw run over those k in rank order (the reference's sorted top-k order).
+  // More than 512 candidates (heavy ties): the radix select below.
+  if (top_k > 0 && top_k < V && top_k <= kRT) {
+    uint32_t* ck = hist;                                       // [512] candidate keys (first: maxima)
+    int* ci = reinterpret_cast<int*>(hist + kRT);              // [512] candidate indices
+    float* pr = reinterpret_cast<float*>(hist + 2 * kRT);      // [512] weights in rank order
+    int* pix = reinterpret_cast<int*>(hist + 3 * kRT);         // [512] indices in rank order
+    ck[t] = tkey;
+    __syncthreads();
+    int rk = 0;  // 16-B broadcast reads, 8 in flight (a serial 4-B loop waits out the LDS latency)
+    const uint4* ck4 = reinterpret_cast<const uint4*>(ck);
+#pragma unroll 8
+    for (int j4 = 0; j4 < kRT / 4; ++j4) {
+      const uint4 o = ck4[j4];
+      const int j = 4 * j4;
+      rk += (o.x > tkey) || (o.x == tkey && j < t);
+      rk += (o.y > tkey) || (o.y == tkey && j + 1 < t);
+      rk += (o.z > tkey) || (o.z == tkey && j + 2 < t);
+      rk += (o.w > tkey) || (o.w == tkey && j + 3 < t);
+    }
+    if (rk == top_k - 1) sel_prefix = tkey;
+    __syncthreads();
+    const uint32_t lo = sel_prefix;
+    opaque();
+    int cnt = 0;
+#pragma unroll
+    for (int k = 0; k < CPT; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) cnt += (8 * (t + kRT * k) + j < V && order_key(val(k, j)) >= lo) ? 1 : 0;
+    int incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int n = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += n;
+    }
+    if (lane == 63) ired[w] = incl;
+    __syncthreads();
+    if (t == 0) {
+      int run = 0;
+      for (int i = 0; i < kRT / 64; ++i) {
+        const int x = ired[i];
+        ired[i] = run;
+        run += x;
+      }
+      sel_k = run;
+    }
+    __syncthreads();
+    const int ncand = sel_k;
+    if (ncand <= kRT) {
+      int off = ired[w] + incl - cnt;
+      opaque();
+#pragma unroll
+      for (int k = 0; k < CPT; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int i = 8 * (t + kRT * k) + j;
+          const uint32_t key = order_key(val(k, j));
+          if (i < V && key >= lo) {
+            ck[off] = key;
+            ci[off] = i;
+            ++off;
+          }
+        }
+      const int npad = (ncand + 31) & ~31;  // key 0 ranks below every real key
+      if (t >= ncand && t < npad) ck[t] = 0;
+      __syncthreads();
+      const float invT = 1.f / temperature;
+      const float m = gmax * invT;
+      if (t < ncand) {
+        const uint32_t mk = ck[t];
+        const int mi = ci[t];
+        int r = 0;
+        for (int j4 = 0; j4 < npad / 4; j4 += 8) {
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const uint4 o = ck4[j4 + u];
+            const int j = 4 * (j4 + u);
+            r += (o.x > mk) || (o.x == mk && ci[j] < mi);
+            r += (o.y > mk) || (o.y == mk && ci[j + 1] < mi);
+            r += (o.z > mk) || (o.z == mk && ci[j + 2] < mi);
+            r += (o.w > mk) || (o.w == mk && ci[j + 3] < mi);
+          }
+        }
+        if (r < top_k) {
+          const uint32_t bits = (mk & 0x80000000u) ? (mk & 0x7fffffffu) : ~mk;  // order_key⁻¹
+          pr[r] = __expf(__uint_as_float(bits) * invT - m);
+          pix[r] = mi;
+        }
+      }
+      __syncthreads();
+      const float pv = t < top_k ? pr[t] : 0.f;
+      float inc = pv;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const float n = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += n;
+      }
+      if (lane == 63) wsum[w] = inc;
+      __syncthreads();
+      if (t == 0) {
+        float run = 0.f;
+        for (int i = 0; i < kRT / 64; ++i) {
+          const float x = wsum[i];
+          wsum[i] = run;
+          run += x;
+        }
+        total_s = run;
+      }
+      __syncthreads();
+      const float cum = wsum[w] + inc;
+      const float target = io.uniform(row) * total_s;
+      if (t < top_k && pv > 0.f && cum > target && cum - pv <= target) result = pix[t];
+      __syncthreads();
+      if (t == 0) io.write(row, result);
+      return;
+    }
+  }
   // ---- top-k threshold: radix select over order-preserving keys (4 × 8-bit digits). Counting
   // every logit costs 4·V LDS atomics, and those that hit one bin serialise (~80 µs per 50 K
   // row), so the select runs twice over small sets instead: (1) over the 512 per-thread maxima,
