@@ -191,8 +191,9 @@ __global__ void __launch_bounds__(256) decode_kernel(const TQ* __restrict__ q, c
     if (k_new != nullptr && c0 + kk == S - 1) {
       const size_t row = head_base + (S - 1);
       if constexpr (std::is_same<TK, int8_t>::value) {
-        static_assert(!std::is_same<TK, int8_t>::value || (TPK == 1 && CPT * 16 == D), "int8 row per thread");
-        // quantise the new K and V rows (the thread holds whole rows)
+        static_assert(!std::is_same<TK, int8_t>::value || TPK * CPT * 16 == D, "int8 row split over TPK threads");
+        // quantise the new K and V rows: every thread of the key takes the whole row's absmax
+        // (identical result), then quantises and stores its own 16-B pieces
         auto quant = [&](const TQ* src, dec_u32x4 (&raw)[CPT], float& sc_out, float* sc_dst, TK* dst) {
           float m = 0.f;
           for (int d = 0; d < D; ++d) m = fmaxf(m, fabsf(to_f(src[d])));
@@ -206,16 +207,16 @@ __global__ void __launch_bounds__(256) decode_kernel(const TQ* __restrict__ q, c
               uint32_t acc = 0;
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
-                const float x = fminf(fmaxf(rintf(to_f(src[16 * c + 4 * q4 + e]) / sc), -128.f), 127.f);
+                const float x = fminf(fmaxf(rintf(to_f(src[16 * (part * CPT + c) + 4 * q4 + e]) / sc), -128.f), 127.f);
                 acc |= ((uint32_t)(uint8_t)(int8_t)x) << (8 * e);
               }
               w[q4] = acc;
             }
             raw[c] = (dec_u32x4){w[0], w[1], w[2], w[3]};
-            *reinterpret_cast<dec_u32x4*>(dst + row * D + 16 * c) = raw[c];
+            *reinterpret_cast<dec_u32x4*>(dst + row * D + 16 * (part * CPT + c)) = raw[c];
           }
           sc_out = sc;
-          sc_dst[row] = sc;
+          if (part == 0) sc_dst[row] = sc;
         };
         quant(k_new + new_off, kr, ksc, const_cast<float*>(ks), const_cast<TK*>(kc));
         quant(v_new + new_off, vr, vsc, const_cast<float*>(vs), const_cast<TK*>(vc));
@@ -422,7 +423,7 @@ torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c
   const int Hkv = kc.size(1), cap = kc.size(2);
   TORCH_CHECK(kc.size(0) == B && kc.size(3) == D && H % Hkv == 0 && H / Hkv <= kMaxGroup);
   TORCH_CHECK(S <= cap && q_offset >= 0 && q_offset + Tq <= S, "bad cache extent");
-  TORCH_CHECK(D == 64 || D == 128, "decode attention supports head_dim 64/128");
+  TORCH_CHECK(D == 64 || D == 128 || D == 256, "decode attention supports head_dim 64/128/256");
   const bool quant = kc.scalar_type() == torch::kInt8;
   TORCH_CHECK(!quant || (k_scale.has_value() && v_scale.has_value()), "int8 cache needs scales");
   TORCH_CHECK(quant || kc.scalar_type() == q.scalar_type(), "cache dtype must match q");
@@ -483,7 +484,8 @@ torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c
     default: PENROZ_DECODE(DD, 0);       \
   }
     if (D == 64) PENROZ_DECODE_G(64)
-    else PENROZ_DECODE_G(128)
+    else if (D == 128) PENROZ_DECODE_G(128)
+    else PENROZ_DECODE_G(256)  // Gemma
 #undef PENROZ_DECODE_G
 #undef PENROZ_DECODE
     if (splits > 1) {

@@ -24,8 +24,9 @@ replayed. Everything that changes between steps lives on the device:
 
 The host only tracks the cache length (one per replay) to switch to the reference's
 sliding-window re-prefill when the window is full, and copies each burst of tokens back once
-(stop-token checks per burst). Prefill and re-prefill run eagerly. Models with RoPE (Gemma)
-keep the eager path: their rotary offset is a host integer per layer.
+(stop-token checks per burst). Prefill and re-prefill run eagerly. RoPE models (Gemma) rotate
+with a cos/sin table computed on the device from ``pos_t`` once per step
+(``_GraphMode.rope_table``); their head_dim 256 runs on the same decode-attention kernel.
 """
 from __future__ import annotations
 
@@ -42,6 +43,7 @@ from penroz.ops import attention as attn_ops
 from penroz.ops import fused as fused_ops
 from penroz.ops import gemm as gemm_ops
 from penroz.ops import norms as norm_ops
+from penroz.ops import rope as rope_ops
 from penroz.ops import sampling as samp_ops
 
 log = logging.getLogger(__name__)
@@ -66,6 +68,19 @@ class _GraphMode:
     def init_graph_state(self, device):
         self.pos_t = torch.zeros(1, dtype=torch.long, device=device)  # slot written by the step
         self.len_t = torch.ones(1, dtype=torch.long, device=device)   # cache length after it
+        self._rope_tables: dict = {}
+
+    def begin_step(self):
+        self._rope_tables.clear()
+
+    def rope_table(self, key, inv_freq: Tensor, T: int):
+        """cos / sin for positions pos_t..pos_t+T-1, computed on the device once per step and
+        ``key`` = (theta, head_dim): layers with the same rotary setup share it."""
+        key = (*key, T)
+        tab = self._rope_tables.get(key)
+        if tab is None:
+            tab = self._rope_tables[key] = rope_ops.rope_table(inv_freq, 0, T, inv_freq.device, offset_dev=self.pos_t)
+        return tab
 
     def attend(self, layer_idx: int, q: Tensor, k: Tensor, v: Tensor) -> Tensor:
         if not self.graph_mode:
@@ -181,7 +196,9 @@ def applicable(model) -> bool:
     if p is None or not p.is_cuda:
         return False
     attn = model._find_attention_layers()
-    return bool(attn) and all(a.rope_theta is None for a in attn)
+    # RoPE layers rotate with a device-offset table; their decode attention must be the HIP kernel
+    # (head_dim known up front: the HF Gemma builders set it)
+    return bool(attn) and all(a.rope_theta is None or a.head_dim in attn_ops.DECODE_HEAD_DIMS for a in attn)
 
 
 class GraphDecoder:
@@ -222,6 +239,7 @@ class GraphDecoder:
         for p in self.pos_layers:
             p.position_offset_tensor = self.cache.pos_t
         self.cache.graph_mode = True
+        self.cache.begin_step()
         try:
             if self.program is not None:
                 last = self.program.forward(self.idx, self.cache)
@@ -295,7 +313,7 @@ class GraphDecoder:
 
 def get_decoder(model, rows: int, block_size: int, temperature: float, top_k: int | None) -> GraphDecoder | None:
     """Cached per model and (rows, block size, sampling settings, weights identity); None when the
-    model does not qualify (CPU, no attention, RoPE) or ``PENROZ_GRAPH_DECODE=0``."""
+    model does not qualify (CPU, no attention, RoPE head_dim without a decode kernel) or ``PENROZ_GRAPH_DECODE=0``."""
     if not applicable(model):
         return None
     p = next(model.parameters())

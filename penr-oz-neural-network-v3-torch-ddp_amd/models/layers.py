@@ -72,8 +72,13 @@ class CausalSelfAttention(nn.Module):
         offset = cache.seq_len(self._layer_idx) if cache is not None else 0
 
         if self.rope_theta is not None:
+            inv_freq = self._inv_freq(head_dim, query_key_value.device)
+            # graph-replayed decode: positions come from the cache's device counter (one table per
+            # (theta, head_dim) and step, shared by the layers)
+            table = (cache.rope_table((self.rope_theta, head_dim), inv_freq, block_size)
+                     if getattr(cache, "graph_mode", False) else None)
             qkv = rope_ops.apply_rope_qkv(query_key_value, self.num_heads, self.num_kv_heads, head_dim,
-                                          self._inv_freq(head_dim, query_key_value.device), offset)
+                                          inv_freq, offset, table=table)
         else:
             qkv = query_key_value
 

@@ -29,7 +29,7 @@ from penroz.ops._ext import use_kernels, kernels
 # and decode attention (csrc/kernels/decode_attn.hip). Other head dims (e.g. Gemma's 256) run
 # torch SDPA on the GPU.
 SUPPORTED_HEAD_DIMS = (64,)
-DECODE_HEAD_DIMS = (64, 128)
+DECODE_HEAD_DIMS = (64, 128, 256)
 
 
 def reference_causal_attention_qkv(qkv: Tensor, H: int, Hkv: int, D: int, dropout_p: float = 0.0) -> Tensor:

@@ -14,8 +14,13 @@ from torch import Tensor
 from penroz.ops._ext import use_kernels, kernels
 
 
-def rope_table(inv_freq: Tensor, offset: int, T: int, device) -> tuple[Tensor, Tensor]:
-    t = torch.arange(offset, offset + T, device=device, dtype=torch.float32)
+def rope_table(inv_freq: Tensor, offset: int, T: int, device, offset_dev: Tensor | None = None) -> tuple[Tensor, Tensor]:
+    """cos / sin [T, D/2] for positions offset..offset+T-1; ``offset_dev`` (device int64 [1])
+    supplies the offset at run time instead (graph-replayed decode)."""
+    if offset_dev is not None:
+        t = offset_dev.to(torch.float32) + torch.arange(T, device=device, dtype=torch.float32)
+    else:
+        t = torch.arange(offset, offset + T, device=device, dtype=torch.float32)
     freqs = torch.outer(t, inv_freq.to(device=device, dtype=torch.float32))
     return freqs.cos().contiguous(), freqs.sin().contiguous()
 
@@ -52,8 +57,13 @@ class _RopeFn(torch.autograd.Function):
         return kernels().rope_qkv(dy.contiguous(), cos, sin, H, Hkv, D, True), None, None, None, None, None
 
 
-def apply_rope_qkv(qkv: Tensor, H: int, Hkv: int, D: int, inv_freq: Tensor, offset: int) -> Tensor:
+def apply_rope_qkv(qkv: Tensor, H: int, Hkv: int, D: int, inv_freq: Tensor, offset: int,
+                   table: tuple[Tensor, Tensor] | None = None) -> Tensor:
+    """``table``: a precomputed (cos, sin) for these positions (graph-replayed decode shares one
+    device-offset table between the layers of a step)."""
     if use_kernels(qkv) and D % 2 == 0:
-        cos, sin = rope_table(inv_freq, offset, qkv.shape[1], qkv.device)
+        cos, sin = table if table is not None else rope_table(inv_freq, offset, qkv.shape[1], qkv.device)
         return _RopeFn.apply(qkv, H, Hkv, D, cos, sin)
+    if table is not None:
+        raise ValueError("a precomputed RoPE table needs the HIP kernel")
     return reference_apply_rope_qkv(qkv, H, Hkv, D, inv_freq, offset)

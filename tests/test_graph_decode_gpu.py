@@ -123,3 +123,30 @@ def test_decode_program_step_matches_module_step():
             dec.detach()
     rel = (got - ref).norm() / ref.norm()
     assert rel < 2e-2, rel
+
+
+def _gemma_model(head_dim):
+    """Tiny Gemma-3 style model (RoPE, GQA 4:1, RMSNorm, gated MLP) from the HF config builder."""
+    from types import SimpleNamespace
+    tc = SimpleNamespace(vocab_size=256, hidden_size=64, num_attention_heads=4, num_key_value_heads=1,
+                         head_dim=head_dim, num_hidden_layers=2, intermediate_size=128, rms_norm_eps=1e-6,
+                         rope_theta=10000.0, attention_dropout=0.0, hidden_activation="gelu_pytorch_tanh",
+                         model_type="gemma3_text")
+    torch.manual_seed(5)
+    m = NeuralNetworkModel("gg", Mapper(Mapper.from_hf_config(tc), {"adamw": {"lr": 1e-3}})).to("cuda")
+    return m.to(dtype=torch.bfloat16)
+
+
+@pytest.mark.parametrize("head_dim", [64, 256])
+def test_rope_model_graph_decode_matches_eager(monkeypatch, head_dim):
+    """RoPE models replay the module forward with a device-offset cos/sin table: same tokens as
+    the eager per-token path, through the sliding-window re-prefill, and with the int8 cache."""
+    m = _gemma_model(head_dim)
+    assert gd.applicable(m)
+    ctx = torch.randint(0, 256, (2, 5), generator=torch.Generator().manual_seed(4)).tolist()
+    eager, graphed = _both(monkeypatch, lambda: m.generate_batch(ctx, 16, 30, temperature=0.0))
+    assert graphed == eager
+    assert any(d.graph is not None and d.program is None for d in m._graph_decoders.values()), "graph path not taken"
+    monkeypatch.setattr(kvc, "TURBO_QUANT_ENABLED", True)
+    eager, graphed = _both(monkeypatch, lambda: m.generate_batch(ctx, 24, 10, temperature=0.0))
+    assert graphed[0][:7] == eager[0][:7]

@@ -257,7 +257,7 @@ def test_flash_dropout_matches_masked_reference():
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32, torch.float16])
-@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("D", [64, 128, 256])
 @pytest.mark.parametrize("B,H,Hkv,S,Tq", [(2, 4, 4, 300, 1), (1, 8, 2, 1024, 1), (3, 4, 4, 64, 5), (64, 12, 12, 600, 1),
                                           (2, 16, 1, 777, 1), (1, 12, 12, 1, 1)])
 def test_decode_attention(dtype, D, B, H, Hkv, S, Tq):
@@ -461,7 +461,8 @@ def test_transpose_bf16(R, C):
 
 @pytest.mark.parametrize("dtype,int8", [(torch.bfloat16, False), (torch.float32, False), (torch.float16, False),
                                         (torch.bfloat16, True)])
-@pytest.mark.parametrize("D,H,Hkv,S", [(64, 12, 12, 100), (128, 8, 2, 300), (64, 4, 1, 1), (128, 4, 4, 257)])
+@pytest.mark.parametrize("D,H,Hkv,S", [(64, 12, 12, 100), (128, 8, 2, 300), (64, 4, 1, 1), (128, 4, 4, 257),
+                                       (256, 8, 1, 300), (256, 4, 2, 65)])  # Gemma head_dim 256
 def test_decode_attention_fused_append(dtype, int8, D, H, Hkv, S):
     """Decode attention that appends this step's K/V itself (slot S-1, read from the fused QKV
     rows) == kv_append followed by decode attention: same output, same cache contents."""
