@@ -13,11 +13,14 @@ void layernorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor mean, torch:
 // rmsnorm.hip
 std::vector<torch::Tensor> rmsnorm_fwd(torch::Tensor x, torch::Tensor w, double eps);
 std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor w, torch::Tensor rstd);
+std::vector<torch::Tensor> rms_residual(torch::Tensor x, torch::Tensor a, c10::optional<torch::Tensor> w1,
+                                        c10::optional<torch::Tensor> w2, int64_t mode, double eps1, double eps2);
 // elementwise.hip
 void gelu_fwd(torch::Tensor x, int64_t approx, torch::Tensor y);
 void gelu_bwd(torch::Tensor dy, torch::Tensor x, int64_t approx, c10::optional<torch::Tensor> dbias, torch::Tensor out);
 void colsum(torch::Tensor x, torch::Tensor out);
 torch::Tensor gated_act_fwd(torch::Tensor g, torch::Tensor u, int64_t kind);
+torch::Tensor gated_act_packed(torch::Tensor gu, int64_t kind);
 std::vector<torch::Tensor> gated_act_bwd(torch::Tensor dy, torch::Tensor g, torch::Tensor u, int64_t kind);
 void transpose_bf16(torch::Tensor in, torch::Tensor out);
 void embedding_fwd(torch::Tensor idx, torch::Tensor wte, torch::Tensor wpe, int64_t off, torch::Tensor out,
@@ -78,10 +81,12 @@ PYBIND11_MODULE(penroz_kernels, m) {
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
   m.def("rmsnorm_bwd", &rmsnorm_bwd);
+  m.def("rms_residual", &rms_residual);
   m.def("gelu_fwd", &gelu_fwd);
   m.def("gelu_bwd", &gelu_bwd);
   m.def("colsum", &colsum);
   m.def("gated_act_fwd", &gated_act_fwd);
+  m.def("gated_act_packed", &gated_act_packed);
   m.def("gated_act_bwd", &gated_act_bwd);
   m.def("transpose_bf16", &transpose_bf16, "out [C, R] = in [R, C]^T (bf16, dims % 64 == 0)");
   m.def("embedding_fwd", &embedding_fwd, pybind11::arg("idx"), pybind11::arg("wte"), pybind11::arg("wpe"),

@@ -104,6 +104,21 @@ __global__ void __launch_bounds__(256) gated_fwd_kernel(const T* __restrict__ g,
   }
 }
 
+// decode: gate and up halves of one fused [N, 2I] projection -> act(gate) * up [N, I]
+template <typename T>
+__global__ void __launch_bounds__(256) gated_packed_kernel(const T* __restrict__ gu, T* __restrict__ y, int64_t n8,
+                                                           int I8, int kind) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / I8, c = i - r * I8;
+    float gv[8], uv[8];
+    Vec8<T>::load(gu + 8 * (r * 2 * I8 + c), gv);
+    Vec8<T>::load(gu + 8 * (r * 2 * I8 + I8 + c), uv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) gv[k] = act_f(gv[k], kind) * uv[k];
+    Vec8<T>::store(y + 8 * i, gv);
+  }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) gated_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ g,
                                                         const T* __restrict__ u, T* __restrict__ dg,
@@ -411,6 +426,21 @@ torch::Tensor gated_act_fwd(torch::Tensor g, torch::Tensor u, int64_t kind) {
     hipLaunchKernelGGL(gated_fwd_kernel<T>, dim3(grid_for(n8)), dim3(256), 0, stream,
                        reinterpret_cast<const T*>(g.data_ptr()), reinterpret_cast<const T*>(u.data_ptr()),
                        reinterpret_cast<T*>(y.data_ptr()), n8, (int)kind))
+  return y;
+}
+
+torch::Tensor gated_act_packed(torch::Tensor gu, int64_t kind) {
+  TORCH_CHECK(gu.is_cuda() && gu.is_contiguous() && gu.dim() == 2 && gu.size(1) % 16 == 0, "gu: [N, 2I], I % 8 == 0");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(gu.data_ptr()) % 16 == 0);
+  const int64_t N = gu.size(0), I = gu.size(1) / 2;
+  auto y = torch::empty({N, I}, gu.options());
+  const int64_t n8 = N * I / 8;
+  if (n8 == 0) return y;
+  auto stream = at::hip::getCurrentHIPStream();
+  FOR_FLOAT_TYPES(gu.scalar_type(), T,
+    hipLaunchKernelGGL(gated_packed_kernel<T>, dim3(grid_for(n8)), dim3(256), 0, stream,
+                       reinterpret_cast<const T*>(gu.data_ptr()), reinterpret_cast<T*>(y.data_ptr()), n8, (int)(I / 8),
+                       (int)kind))
   return y;
 }
 

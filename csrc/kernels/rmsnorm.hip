@@ -67,6 +67,83 @@ __global__ void __launch_bounds__(256) rms_finish_kernel(const float* __restrict
   out[c] = s;
 }
 
+
+// Decode-step fusion for Gemma blocks: residual add + post-norm + the next norm in one pass.
+// The row lives in registers (one wave per row, NV 8-value vectors per lane). Every intermediate is
+// rounded to T where the module path rounds (torch adds / RMSNorm output), so the result equals
+// the module sequence  h = post(x, a); y = rms(h) * w2:
+//   mode 0: h = rms(x + a) * w1        (Gemma 3+: post norm on the residual sum)
+//   mode 1: h = x + rms(a) * w1        (Gemma 2: post norm on the branch output)
+//   mode 2: h = x + a                  (Gemma 1: no post norms)
+// y is skipped when w2 is null (h alone: the last block feeds the final norm separately).
+template <int NV, typename T>
+__global__ void __launch_bounds__(256) rms_residual_kernel(const T* __restrict__ x, const T* __restrict__ a,
+                                                           const T* __restrict__ w1, const T* __restrict__ w2,
+                                                           T* __restrict__ h, T* __restrict__ y, int N, int C,
+                                                           int mode, float eps1, float eps2) {
+  // lane owns 8-value vectors j = lane + 64 i (i < NV). Every load is issued before any use
+  // (out-of-range vectors re-read the row's last one and are masked), so a row costs one memory
+  // round trip instead of one per element.
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= N) return;
+  const int nvec = C / 8;
+  const T* xr = x + (size_t)row * C;
+  const T* ar = a + (size_t)row * C;
+  float xv[NV][8], v[NV][8];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int j = min(lane + 64 * i, nvec - 1);
+    Vec8<T>::load(ar + 8 * j, v[i]);
+    Vec8<T>::load(xr + 8 * j, xv[i]);
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const bool ok = lane + 64 * i < nvec;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if (mode == 0) v[i][e] = to_f(from_f<T>(xv[i][e] + v[i][e]));  // torch's rounded add
+      else if (mode == 2) v[i][e] = to_f(from_f<T>(xv[i][e] + v[i][e]));
+      if (mode != 2 && ok) ss += v[i][e] * v[i][e];
+    }
+  }
+  if (mode != 2) {
+    const float r = rsqrtf(wave_sum(ss) / C + eps1);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      float wv[8];
+      Vec8<T>::load(w1 + 8 * min(lane + 64 * i, nvec - 1), wv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float n = to_f(from_f<T>(to_f(from_f<T>(v[i][e] * r)) * wv[e]));
+        v[i][e] = mode == 0 ? n : to_f(from_f<T>(xv[i][e] + n));
+      }
+    }
+  }
+  ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int j = lane + 64 * i;
+    if (j < nvec) {
+      Vec8<T>::store(h + (size_t)row * C + 8 * j, v[i]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ss += v[i][e] * v[i][e];
+    }
+  }
+  if (w2 == nullptr) return;
+  const float r2 = rsqrtf(wave_sum(ss) / C + eps2);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int j = lane + 64 * i;
+    float wv[8];
+    Vec8<T>::load(w2 + 8 * min(j, nvec - 1), wv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[i][e] = to_f(from_f<T>(v[i][e] * r2)) * wv[e];
+    if (j < nvec) Vec8<T>::store(y + (size_t)row * C + 8 * j, v[i]);
+  }
+}
+
 }  // namespace penroz
 
 using namespace penroz;
@@ -112,4 +189,45 @@ std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor dy, torch::Tensor x, torch:
   hipLaunchKernelGGL(rms_finish_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, part.data_ptr<float>(), G, C,
                      dw.data_ptr<float>());
   return {dx, dw};
+}
+
+// x, a: [N, C] (same dtype as w1 / w2); returns {h, y} (y undefined when w2 is absent)
+std::vector<torch::Tensor> rms_residual(torch::Tensor x, torch::Tensor a, c10::optional<torch::Tensor> w1,
+                                        c10::optional<torch::Tensor> w2, int64_t mode, double eps1, double eps2) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && a.is_contiguous() && x.dim() == 2 && a.sizes() == x.sizes() &&
+              a.scalar_type() == x.scalar_type(), "x, a: [N, C] contiguous, same dtype");
+  TORCH_CHECK(mode >= 0 && mode <= 2 && (mode == 2 || (w1.has_value() && w1->defined())), "rms_residual mode");
+  const int N = x.size(0), C = x.size(1);
+  for (auto* w : {&w1, &w2})
+    if (w->has_value() && (*w)->defined())
+      TORCH_CHECK((*w)->is_contiguous() && (*w)->numel() == C && (*w)->scalar_type() == x.scalar_type(), "norm weight");
+  TORCH_CHECK(C % 8 == 0 && C <= 64 * 8 * 12, "rms_residual: width % 8 == 0, <= 6144");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0,
+              "rms_residual: 16-B aligned rows");
+  auto h = torch::empty_like(x);
+  const bool has_y = w2.has_value() && w2->defined();
+  torch::Tensor y = has_y ? torch::empty_like(x) : torch::Tensor();
+  if (N == 0) return {h, y};
+  auto stream = at::hip::getCurrentHIPStream();
+  const int nv = (C / 8 + 63) / 64;  // 8-value vectors per lane
+  auto launch = [&](auto tag) {
+    using T = decltype(tag);
+    const T* w1p = mode != 2 ? reinterpret_cast<const T*>(w1->data_ptr()) : nullptr;
+    const T* w2p = has_y ? reinterpret_cast<const T*>(w2->data_ptr()) : nullptr;
+    T* yp = has_y ? reinterpret_cast<T*>(y.data_ptr()) : nullptr;
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3((N + 3) / 4), dim3(256), 0, stream, reinterpret_cast<const T*>(x.data_ptr()),
+                         reinterpret_cast<const T*>(a.data_ptr()), w1p, w2p, reinterpret_cast<T*>(h.data_ptr()), yp, N,
+                         C, (int)mode, (float)eps1, (float)eps2);
+    };
+    if (nv <= 1) go(rms_residual_kernel<1, T>);
+    else if (nv <= 2) go(rms_residual_kernel<2, T>);
+    else if (nv <= 3) go(rms_residual_kernel<3, T>);
+    else if (nv <= 4) go(rms_residual_kernel<4, T>);
+    else if (nv <= 6) go(rms_residual_kernel<6, T>);
+    else if (nv <= 8) go(rms_residual_kernel<8, T>);
+    else go(rms_residual_kernel<12, T>);
+  };
+  RMS_TYPES(x.scalar_type(), T, launch(T{}))
+  return {h, y};
 }

@@ -189,6 +189,107 @@ class GPTDecodeProgram:
         return self._linear(add_ln(delta, wf, bf, ef, dbias), sp.head)
 
 
+class GemmaDecodeProgram:
+    """One decode step of a Gemma-family bf16 model (``models/hf.py`` layer list) as an explicit
+    kernel sequence.
+
+    The module forward runs ~16 kernels per block at decode shapes (four RMSNorms, two residual
+    adds, separate gate and up GEMMs). Per block this runs 8 (+1 split-K combine): QKV GEMM →
+    RoPE (device-offset table) → decode attention with fused K/V append → O GEMM →
+    [residual add + post-attention norm + pre-MLP norm] → gate|up GEMM (one concatenated weight)
+    → gated activation on the packed halves → down GEMM → [residual add + post-MLP norm + the next
+    block's input norm]. Rounding follows the module path (bf16 residual stream, torch's rounding
+    points), so only the GEMM accumulation order of the fused gate|up projection can differ.
+    Reference block semantics: ``neural_net_layers.py:188-225``.
+    """
+
+    def __init__(self, emb, blocks, norm_f, head):
+        self.emb, self.norm_f, self.head = emb, norm_f, head
+        self.blocks = []
+        for b in blocks:
+            in_norm, qkv, attn, o = list(b.attn_block)
+            pre_mlp, mlp = list(b.mlp_block)
+            if b.post_attn_norm is None:
+                mode = 2
+            else:
+                mode = 0 if b.post_norm_on_residual else 1
+            self.blocks.append(dict(
+                in_norm=in_norm, qkv=qkv.weight, attn=attn, o=o.weight, pre_mlp=pre_mlp, mode=mode,
+                post_attn=b.post_attn_norm, post_mlp=b.post_mlp_norm,
+                gu=torch.cat([mlp.gate_proj.weight, mlp.up_proj.weight]).contiguous(), down=mlp.down_proj.weight,
+                kind=act_ops._GATED[mlp.act_kind], inter=mlp.gate_proj.out_features))
+
+    @staticmethod
+    def build(model):
+        if not DECODE_PROGRAM:
+            return None
+        from torch import nn
+        from penroz.models import layers as L
+        mods = list(model.layers)
+        if mods and isinstance(mods[-1], L.SoftmaxOnLast):
+            mods = mods[:-1]
+        if (len(mods) < 4 or not isinstance(mods[0], L.ScaledEmbedding) or not isinstance(mods[-2], L.RMSNorm)
+                or not isinstance(mods[-1], nn.Linear) or mods[-1].bias is not None):
+            return None
+        if any(p.dtype != torch.bfloat16 for p in model.parameters()):
+            return None
+        C = mods[0].embedding_dim
+        if C % 8 or C > 6144:
+            return None
+        for b in mods[1:-2]:
+            if not isinstance(b, L.TransformerBlock) or (b.post_attn_norm is None) != (b.post_mlp_norm is None):
+                return None
+            ab, mb = list(b.attn_block), list(b.mlp_block)
+            if not (len(ab) == 4 and isinstance(ab[0], L.RMSNorm) and isinstance(ab[1], nn.Linear)
+                    and isinstance(ab[2], L.CausalSelfAttention) and isinstance(ab[3], nn.Linear)
+                    and len(mb) == 2 and isinstance(mb[0], L.RMSNorm) and isinstance(mb[1], L.GatedMLP)):
+                return None
+            a, mlp = ab[2], mb[1]
+            if (ab[1].bias is not None or ab[3].bias is not None or mlp.gate_proj.bias is not None
+                    or mlp.down_proj.bias is not None or a.head_dim not in attn_ops.DECODE_HEAD_DIMS
+                    or mlp.gate_proj.out_features % 8):
+                return None
+            norms = [ab[0], mb[0]] + ([b.post_attn_norm, b.post_mlp_norm] if b.post_attn_norm is not None else [])
+            if any(not isinstance(n, L.RMSNorm) for n in norms):
+                return None
+        return GemmaDecodeProgram(mods[0], mods[1:-2], mods[-2], mods[-1])
+
+    def forward(self, idx: Tensor, cache) -> Tensor:
+        """idx [rows, 1] -> logits [rows, V] (bf16); appends this step's K/V at cache.pos_t."""
+        K = _ext.kernels()
+        rows = idx.shape[0]
+        x = torch.nn.functional.embedding(idx.view(rows), self.emb.weight) * self.emb.scale
+        first = self.blocks[0]["in_norm"]
+        y = K.rmsnorm_fwd(x, first.weight, first.eps)[0]
+        for l, b in enumerate(self.blocks):
+            a = b["attn"]
+            H, Hkv, D = a.num_heads, a.num_kv_heads, a.head_dim
+            qkv = _linear(y, b["qkv"]).view(rows, 1, -1)
+            if a.rope_theta is not None:
+                inv = a._inv_freq(D, qkv.device)
+                qkv = rope_ops.apply_rope_qkv(qkv, H, Hkv, D, inv, 0,
+                                              table=cache.rope_table((a.rope_theta, D), inv, 1))
+            q, k, v = qkv.split([H * D, Hkv * D, Hkv * D], dim=2)
+            att = cache.attend(l, q.reshape(rows, 1, H, D), k.view(rows, 1, Hkv, D), v.view(rows, 1, Hkv, D))
+            o = _linear(att.view(rows, H * D), b["o"])
+            pa, pm, pre = b["post_attn"], b["post_mlp"], b["pre_mlp"]
+            h, y = K.rms_residual(x, o, pa.weight if pa is not None else None, pre.weight, b["mode"],
+                                  pa.eps if pa is not None else 0.0, pre.eps)
+            g = K.gated_act_packed(_linear(y, b["gu"]), b["kind"])
+            d = _linear(g, b["down"])
+            nxt = self.blocks[l + 1]["in_norm"] if l + 1 < len(self.blocks) else self.norm_f
+            x, y = K.rms_residual(h, d, pm.weight if pm is not None else None, nxt.weight, b["mode"],
+                                  pm.eps if pm is not None else 0.0, nxt.eps)
+        return _linear(y, self.head.weight)
+
+
+def _linear(x: Tensor, w: Tensor) -> Tensor:
+    """x [M, K] · wᵀ without bias: the decode-shaped MFMA kernel up to SKINNY_MAX_ROWS rows."""
+    if x.shape[0] <= SKINNY_MAX_ROWS and gemm_ops.skinny_ok(x, w):
+        return gemm_ops.skinny_linear(x, w, None)
+    return torch.mm(x, w.t())
+
+
 def applicable(model) -> bool:
     if not GRAPH_DECODE or not torch.cuda.is_available():
         return False
@@ -220,7 +321,7 @@ class GraphDecoder:
         self.seed_t = torch.zeros(1, dtype=torch.long, device=self.device)  # per-run sampling salt
         self.graph: torch.cuda.CUDAGraph | None = None
         gemm_ops.skinny_workspace(self.device)  # zeroed counters exist before any capture
-        self.program = GPTDecodeProgram.build(model)
+        self.program = GPTDecodeProgram.build(model) or GemmaDecodeProgram.build(model)
 
     # ------------------------------------------------------------------ cache attachment
     def attach(self):

@@ -125,13 +125,13 @@ def test_decode_program_step_matches_module_step():
     assert rel < 2e-2, rel
 
 
-def _gemma_model(head_dim):
-    """Tiny Gemma-3 style model (RoPE, GQA 4:1, RMSNorm, gated MLP) from the HF config builder."""
+def _gemma_model(head_dim, model_type="gemma3_text"):
+    """Tiny Gemma style model (RoPE, GQA 4:1, RMSNorm, gated MLP) from the HF config builder."""
     from types import SimpleNamespace
     tc = SimpleNamespace(vocab_size=256, hidden_size=64, num_attention_heads=4, num_key_value_heads=1,
                          head_dim=head_dim, num_hidden_layers=2, intermediate_size=128, rms_norm_eps=1e-6,
                          rope_theta=10000.0, attention_dropout=0.0, hidden_activation="gelu_pytorch_tanh",
-                         model_type="gemma3_text")
+                         model_type=model_type)
     torch.manual_seed(5)
     m = NeuralNetworkModel("gg", Mapper(Mapper.from_hf_config(tc), {"adamw": {"lr": 1e-3}})).to("cuda")
     return m.to(dtype=torch.bfloat16)
@@ -142,7 +142,7 @@ def test_rope_model_graph_decode_matches_eager(monkeypatch, head_dim):
     """RoPE models replay the module forward with a device-offset cos/sin table: same tokens as
     the eager per-token path, through the sliding-window re-prefill, and with the int8 cache."""
     m = _gemma_model(head_dim)
-    assert gd.applicable(m)
+    assert gd.applicable(m) and gd.GemmaDecodeProgram.build(m) is not None
     ctx = torch.randint(0, 256, (2, 5), generator=torch.Generator().manual_seed(4)).tolist()
     eager, graphed = _both(monkeypatch, lambda: m.generate_batch(ctx, 16, 30, temperature=0.0))
     assert graphed == eager
@@ -150,3 +150,45 @@ def test_rope_model_graph_decode_matches_eager(monkeypatch, head_dim):
     monkeypatch.setattr(kvc, "TURBO_QUANT_ENABLED", True)
     eager, graphed = _both(monkeypatch, lambda: m.generate_batch(ctx, 24, 10, temperature=0.0))
     assert graphed[0][:7] == eager[0][:7]
+
+
+@pytest.mark.parametrize("model_type", ["gemma", "gemma2", "gemma3_text"])  # post-norm modes 2, 1, 0
+def test_gemma_program_step_matches_module_step(model_type):
+    m = _gemma_model(256, model_type)
+    rows, cap = 3, 32
+    dec = gd.GraphDecoder(m, rows, cap, 0.0, None)
+    assert isinstance(dec.program, gd.GemmaDecodeProgram)
+    idx = torch.randint(0, 256, (rows, 7), device="cuda", generator=torch.Generator("cuda").manual_seed(3))
+    with torch.inference_mode():
+        dec.attach()
+        try:
+            m(idx[:, :6], skip_softmax=True)  # prefill through the modules
+            tok = idx[:, 6:]
+            dec._set_state(tok, 6)
+            dec.cache.graph_mode = True
+            dec.cache.begin_step()
+            acts, _ = m(tok, skip_softmax=True)
+            ref = acts[-1][:, -1, :].float()
+            dec.cache.begin_step()
+            got = dec.program.forward(tok, dec.cache).float()  # rewrites the same cache slot
+        finally:
+            dec.cache.graph_mode = False
+            dec.detach()
+    rel = (got - ref).norm() / ref.norm()
+    assert rel < 2e-2, rel
+
+
+def test_gemma_program_graph_replay_matches_eager_program(monkeypatch):
+    m = _gemma_model(256)
+    ctx = torch.randint(0, 256, (2, 5), generator=torch.Generator().manual_seed(6)).tolist()
+    graphed = m.generate_batch(ctx, 16, 30, temperature=0.0)
+    assert all(isinstance(d.program, gd.GemmaDecodeProgram) and isinstance(d.graph, torch.cuda.CUDAGraph)
+               for d in m._graph_decoders.values())
+    m.__dict__.pop("_graph_decoders")
+
+    def eager_capture(self, last_tok, cache_len):
+        self._set_state(last_tok, cache_len)
+        self.graph = _EagerGraph(self)
+
+    monkeypatch.setattr(gd.GraphDecoder, "_capture", eager_capture)
+    assert m.generate_batch(ctx, 16, 30, temperature=0.0) == graphed

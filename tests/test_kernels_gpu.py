@@ -523,3 +523,38 @@ def test_sample_step_and_advance(V, dt):
         K.sample_step(rows, 1.0, 0, seed, step, idx, out)
         counts += torch.bincount(idx.view(-1).cpu(), minlength=3)[:3].float()
     assert torch.allclose(counts / counts.sum(), torch.softmax(torch.tensor([1.0, 0.5, 0.0]), -1), atol=0.03)
+
+
+@pytest.mark.parametrize("C", [64, 1152, 2304, 5376])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("with_y", [True, False])
+def test_rms_residual(C, mode, with_y):
+    """Fused residual add + post norm + next norm (Gemma decode program) == the module sequence
+    of torch bf16 adds and reference RMSNorms."""
+    from penroz.ops import norms as Nm
+    torch.manual_seed(C + mode)
+    N = 5
+    x, a = (torch.randn(N, C, device=DEV) * 3).to(torch.bfloat16), torch.randn(N, C, device=DEV).to(torch.bfloat16)
+    w1, w2 = (1 + torch.rand(C, device=DEV)).to(torch.bfloat16), (1 + torch.rand(C, device=DEV)).to(torch.bfloat16)
+    if mode == 0:
+        h = Nm.reference_rms_norm(x + a, w1, 1e-6)
+    elif mode == 1:
+        h = x + Nm.reference_rms_norm(a, w1, 1e-6)
+    else:
+        h = x + a
+    gh, gy = _ext.kernels().rms_residual(x, a, w1 if mode != 2 else None, w2 if with_y else None, mode, 1e-6, 1e-5)
+    _close(gh.float(), h.float(), 0.02, 0.02)
+    assert (gh.float() - h.float()).abs().gt(0.05 * h.float().abs() + 0.05).float().mean() < 1e-3
+    if with_y:
+        _close(gy.float(), Nm.reference_rms_norm(gh, w2, 1e-5).float(), 0.02, 0.02)
+    else:
+        assert gy is None  # an undefined tensor crosses pybind as None
+
+
+@pytest.mark.parametrize("kind", ["gelu", "gelu_tanh", "silu"])
+def test_gated_act_packed(kind):
+    from penroz.ops import activations as Ac
+    gu = torch.randn(7, 2 * 6912, device=DEV).to(torch.bfloat16)
+    out = _ext.kernels().gated_act_packed(gu, Ac._GATED[kind])
+    ref = Ac.reference_gated_act(gu[:, :6912].float(), gu[:, 6912:].float(), kind)
+    _close(out.float(), ref, 0.02, 0.02)
