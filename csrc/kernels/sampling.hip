@@ -6,7 +6,8 @@
 //   uniform u: thread-major order (thread t owns elements t, t+1024, …), one block scan of
 //   the per-thread sums finds the owning thread, which walks its own elements.
 // The whole decision stays on the device (no sort, no host round trip per token).
-// sample_reg_kernel (default for V % 8 == 0, V <= 64 Ki) keeps the row in registers.
+// sample_reg_kernel (default for V % 8 == 0, V <= 64 Ki) keeps the row in registers; wider rows
+// (greedy / top-k <= 64, V <= 256 Ki) go through the two-stage sample_part_kernel + sample_merge_kernel.
 #include "common.h"
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
@@ -486,6 +487,249 @@ __global__ void __launch_bounds__(kRT) sample_reg_kernel(const T* __restrict__ l
   if (t == 0) io.write(row, result);
 }
 
+
+// ------------------------------------------------------------------------------------------
+// Two-stage form for wide rows (V > 64 Ki: Gemma's 262 144-token vocabulary), greedy or
+// top-k <= kPartK = 64. One 1024-thread workgroup per row reads the row seven times; here the row is
+// split into <= 64 parts of 4096 logits (V <= 256 Ki), one 256-thread workgroup each (16 logits per thread in
+// registers, read once):
+//   stage 1 (grid parts x rows): the part's argmax, and its top-k by a 4-pass radix select on
+//     the registers; every logit > the part's k-th largest, then the ties at it, go to a
+//     candidate list (<= kPartC per part: only ties at the threshold can be dropped).
+//     Every element >= the row's k-th largest is >= its part's k-th largest, so the candidates
+//     hold the row's whole top-k (ties included) and its k-th largest key is the row's.
+//   stage 2 (one workgroup per row): argmax merge; radix select over the candidates; the kept
+//     ones are ranked by token index (the draw order of the one-stage kernels), softmax(v/T),
+//     inverse-CDF draw with the row's uniform.
+constexpr int kPartN = 4096, kPartK = 64, kPartC = 128, kPartKeep = 1024, kPartMaxP = 64,
+              kPartLds = kPartMaxP * kPartC;  // every part's candidates fit: none dropped in the merge
+
+__device__ __forceinline__ float key_value(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) sample_part_kernel(const T* __restrict__ logits, int V, int P, int top_k,
+                                                          float* __restrict__ pval, int* __restrict__ pidx,
+                                                          uint32_t* __restrict__ ckey, int* __restrict__ cidx,
+                                                          int* __restrict__ cnt) {
+  __shared__ uint32_t hist[256];
+  __shared__ uint32_t wtot[4];
+  __shared__ float fred[4];
+  __shared__ int ired[4];
+  __shared__ uint32_t sel_prefix, sel_mask;
+  __shared__ int sel_k, ncand;
+  const int part = blockIdx.x, row = blockIdx.y, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const T* lp = logits + (size_t)row * V;
+  const int base = part * kPartN;
+  float v[2][8];
+  bool ok[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int e0 = base + 8 * (t + 256 * c);
+    ok[c] = e0 < V;  // V % 8 == 0: a chunk is all in or all out
+    Vec8<T>::load(lp + (ok[c] ? e0 : 0), v[c]);
+  }
+  float bm = -INFINITY;
+  int bi = 0x7fffffff;
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int i = base + 8 * (t + 256 * c) + e;
+      if (ok[c] && (v[c][e] > bm || (v[c][e] == bm && i < bi))) { bm = v[c][e]; bi = i; }
+    }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(bm, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (om > bm || (om == bm && oi < bi)) { bm = om; bi = oi; }
+  }
+  if (lane == 0) { fred[w] = bm; ired[w] = bi; }
+  __syncthreads();
+  if (t == 0) {
+    float m = fred[0];
+    int ix = ired[0];
+    for (int i = 1; i < 4; ++i)
+      if (fred[i] > m || (fred[i] == m && ired[i] < ix)) { m = fred[i]; ix = ired[i]; }
+    pval[(size_t)row * P + part] = m;
+    pidx[(size_t)row * P + part] = ix;
+  }
+  if (top_k <= 0) return;
+  uint32_t key[2][8];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) key[c][e] = ok[c] ? order_key(v[c][e]) : 0u;
+  if (t == 0) { sel_prefix = 0; sel_mask = 0; sel_k = top_k; ncand = 0; }
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    hist[t] = 0;
+    __syncthreads();
+    const uint32_t pre = sel_prefix, msk = sel_mask;
+    const int kk = sel_k;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (ok[c] && (key[c][e] & msk) == pre) atomicAdd(&hist[(key[c][e] >> shift) & 255u], 1u);
+    __syncthreads();
+    pick_digit(hist, wtot, shift, pre, msk, kk, &sel_prefix, &sel_mask, &sel_k);
+    __syncthreads();
+  }
+  const uint32_t thr = sel_prefix;
+  const size_t cb = ((size_t)row * P + part) * kPartC;
+  // the < k logits above the threshold first (always kept), then the ties at it
+  for (int tie = 0; tie < 2; ++tie) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (ok[c] && (tie ? key[c][e] == thr : key[c][e] > thr)) {
+          const int slot = atomicAdd(&ncand, 1);
+          if (slot < kPartC) {
+            ckey[cb + slot] = key[c][e];
+            cidx[cb + slot] = base + 8 * (t + 256 * c) + e;
+          }
+        }
+    __syncthreads();
+  }
+  if (t == 0) cnt[(size_t)row * P + part] = min(ncand, kPartC);
+}
+
+__global__ void __launch_bounds__(256) sample_merge_kernel(const SampleIO io, int P, float temperature, int top_k,
+                                                           const float* __restrict__ pval, const int* __restrict__ pidx,
+                                                           const uint32_t* __restrict__ ckey,
+                                                           const int* __restrict__ cidx, const int* __restrict__ cnt) {
+  __shared__ uint32_t hist[256];
+  __shared__ uint32_t wtot[4];
+  __shared__ float fred[4];
+  __shared__ int ired[4];
+  __shared__ uint32_t sel_prefix, sel_mask;
+  __shared__ int sel_k, nkeep;
+  __shared__ float kval[kPartKeep];
+  __shared__ int kidx[kPartKeep];
+  __shared__ float sval[kPartKeep];
+  __shared__ int sidx[kPartKeep];
+  extern __shared__ __attribute__((aligned(16))) uint32_t dyn_lds[];  // kPartLds keys + indices (64 KB)
+  uint32_t* lkey = dyn_lds;
+  int* lidx = reinterpret_cast<int*>(dyn_lds + kPartLds);
+  __shared__ int coff[256];
+  __shared__ int ctot;
+  const int row = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  float bm = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int p = t; p < P; p += 256) {
+    const float pv = pval[(size_t)row * P + p];
+    const int pi = pidx[(size_t)row * P + p];
+    if (pv > bm || (pv == bm && pi < bi)) { bm = pv; bi = pi; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(bm, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (om > bm || (om == bm && oi < bi)) { bm = om; bi = oi; }
+  }
+  if (lane == 0) { fred[w] = bm; ired[w] = bi; }
+  __syncthreads();
+  float gmax = fred[0];
+  int gidx = ired[0];
+  for (int i = 1; i < 4; ++i)
+    if (fred[i] > gmax || (fred[i] == gmax && ired[i] < gidx)) { gmax = fred[i]; gidx = ired[i]; }
+  if (temperature == 0.f || top_k <= 0) {
+    if (t == 0) io.write(row, gidx);
+    return;
+  }
+  __syncthreads();  // fred / ired are reused below
+  // compact the valid candidates of all parts into LDS (part order), then work from there
+  const int* nr = cnt + (size_t)row * P;
+  int c = 0, incl = 0;
+  if (t < P) c = nr[t];
+  incl = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) ired[w] = incl;
+  __syncthreads();
+  for (int i = 0; i < w; ++i) incl += ired[i];
+  if (t < P) coff[t] = incl - c;
+  if (t == 255) ctot = min(incl, kPartLds);
+  __syncthreads();
+  const int NCg = P * kPartC;
+  for (int f = t; f < NCg; f += 256) {
+    const int p = f / kPartC, j = f - p * kPartC;
+    if (j < nr[p] && coff[p] + j < kPartLds) {
+      lkey[coff[p] + j] = ckey[(size_t)row * NCg + f];
+      lidx[coff[p] + j] = cidx[(size_t)row * NCg + f];
+    }
+  }
+  const int NC = ctot;
+  const uint32_t* kr = lkey;
+  const int* ir = lidx;
+  if (t == 0) { sel_prefix = 0; sel_mask = 0; sel_k = top_k; nkeep = 0; }
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    hist[t] = 0;
+    __syncthreads();
+    const uint32_t pre = sel_prefix, msk = sel_mask;
+    const int kk = sel_k;
+    for (int f = t; f < NC; f += 256) {
+      const uint32_t k = kr[f];
+      if ((k & msk) == pre) atomicAdd(&hist[(k >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    pick_digit(hist, wtot, shift, pre, msk, kk, &sel_prefix, &sel_mask, &sel_k);
+    __syncthreads();
+  }
+  const uint32_t thr = sel_prefix;
+  for (int tie = 0; tie < 2; ++tie) {  // above the threshold first, then the ties at it
+    for (int f = t; f < NC; f += 256) {
+      if (tie ? kr[f] != thr : kr[f] <= thr) continue;
+      const int slot = atomicAdd(&nkeep, 1);
+      if (slot < kPartKeep) {
+        kval[slot] = key_value(kr[f]);
+        kidx[slot] = ir[f];
+      }
+    }
+    __syncthreads();
+  }
+  const int n = min(nkeep, kPartKeep);
+  const float invT = 1.f / temperature;
+  float part_sum = 0.f;
+  for (int e = t; e < n; e += 256) {  // rank by token index: the draw walks the kept set in index order
+    const int ix = kidx[e];
+    int r = 0;
+    for (int j = 0; j < n; ++j) r += kidx[j] < ix;
+    const float wgt = __expf((kval[e] - gmax) * invT);
+    sval[r] = wgt;
+    sidx[r] = ix;
+    part_sum += wgt;
+  }
+  part_sum = wave_sum(part_sum);
+  if (lane == 0) fred[w] = part_sum;
+  __syncthreads();
+  if (w != 0) return;
+  const float total = (fred[0] + fred[1]) + (fred[2] + fred[3]);
+  const float target = io.uniform(row) * total;
+  float carry = 0.f;
+  int pick = n > 0 ? sidx[n - 1] : gidx;
+  for (int b0 = 0; b0 < n; b0 += 64) {
+    const int e = b0 + lane;
+    float incl = e < n ? sval[e] : 0.f;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const float y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    const uint64_t hit = __ballot(e < n && carry + incl > target);
+    if (hit) {
+      pick = sidx[b0 + __ffsll((unsigned long long)hit) - 1];
+      break;
+    }
+    carry += __shfl(incl, 63, 64);
+  }
+  if (lane == 0) io.write(row, pick);
+}
 }  // namespace penroz
 
 using namespace penroz;
@@ -500,6 +744,39 @@ static void launch_sample(const torch::Tensor& logits, const SampleIO& io, doubl
   const bool fits = chunks <= (logits.scalar_type() == torch::kBFloat16 ? 16 : 8);
   const float tt = (float)temperature;
   const int kk = (int)top_k;
+  if (V % 8 == 0 && !fits && logits.scalar_type() != torch::kFloat16 &&
+      V <= kPartMaxP * kPartN && (temperature == 0.0 || (top_k > 0 && top_k <= kPartK))) {
+    const int P = (V + kPartN - 1) / kPartN;
+    const bool topk = temperature != 0.0;
+    auto opt = logits.options();
+    auto pval = torch::empty({B, P}, opt.dtype(torch::kFloat32));
+    auto pidx = torch::empty({B, P}, opt.dtype(torch::kInt32));
+    torch::Tensor ckey, cidx, cnt;
+    if (topk) {
+      ckey = torch::empty({B, P, kPartC}, opt.dtype(torch::kInt32));
+      cidx = torch::empty({B, P, kPartC}, opt.dtype(torch::kInt32));
+      cnt = torch::empty({B, P}, opt.dtype(torch::kInt32));
+    }
+    uint32_t* ckp = topk ? reinterpret_cast<uint32_t*>(ckey.data_ptr()) : nullptr;
+    int* cip = topk ? cidx.data_ptr<int>() : nullptr;
+    int* cnp = topk ? cnt.data_ptr<int>() : nullptr;
+    const int kpart = topk ? kk : 0;
+    if (logits.scalar_type() == torch::kBFloat16)
+      hipLaunchKernelGGL(sample_part_kernel<bf16>, dim3(P, B), dim3(256), 0, stream,
+                         reinterpret_cast<const bf16*>(logits.data_ptr()), V, P, kpart, pval.data_ptr<float>(),
+                         pidx.data_ptr<int>(), ckp, cip, cnp);
+    else
+      hipLaunchKernelGGL(sample_part_kernel<float>, dim3(P, B), dim3(256), 0, stream, logits.data_ptr<float>(), V, P,
+                         kpart, pval.data_ptr<float>(), pidx.data_ptr<int>(), ckp, cip, cnp);
+    static bool lds_set = [] {  // > 64 KB of LDS per workgroup must be requested
+      return hipFuncSetAttribute(reinterpret_cast<const void*>(sample_merge_kernel),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, kPartLds * 8) == hipSuccess;
+    }();
+    TORCH_CHECK(lds_set, "sample_merge_kernel: LDS request refused");
+    hipLaunchKernelGGL(sample_merge_kernel, dim3(B), dim3(256), kPartLds * 8, stream, io, P, tt, kpart, pval.data_ptr<float>(),
+                       pidx.data_ptr<int>(), ckp, cip, cnp);
+    return;
+  }
   if (V % 8 == 0 && fits && logits.scalar_type() != torch::kFloat16) {
     auto launch = [&](auto tag) {
       using T = decltype(tag);

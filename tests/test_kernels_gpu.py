@@ -558,3 +558,36 @@ def test_gated_act_packed(kind):
     out = _ext.kernels().gated_act_packed(gu, Ac._GATED[kind])
     ref = Ac.reference_gated_act(gu[:, :6912].float(), gu[:, 6912:].float(), kind)
     _close(out.float(), ref, 0.02, 0.02)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_sampling_two_stage_wide_vocab(dt):
+    """V = 262 144 (Gemma): the two-stage sampler (4096-logit parts, candidate merge) for greedy
+    and top-k <= 64 — argmax exact, draws inside the top-k (ties included), the kept set in index
+    order equals the torch reference's kept set, and planted logits in different parts are drawn
+    with softmax(v / T) frequencies."""
+    torch.manual_seed(1)
+    B, V = 16, 262144
+    logits = (torch.randn(B, V, device=DEV) * 3).to(dt)
+    lf = logits.float()
+    assert torch.equal(Sa.sample(logits, 0.0, None).view(-1), lf.argmax(-1))
+    K = _ext.kernels()
+    for k in (1, 50, 64, 100):  # 100: the one-stage streaming kernel
+        top = lf.topk(k, dim=-1).values[:, -1:]
+        for u in (0.0, 0.37, 0.999):
+            t = K.sample_tokens(logits, torch.full((B,), u, device=DEV), 0.8, k)
+            assert bool((lf.gather(1, t) >= top).all())  # k = 1 with a tied maximum: either one
+    # u -> token is the inverse CDF over the kept set in index order: u = 0 draws the lowest index
+    u0 = K.sample_tokens(logits, torch.zeros(B, device=DEV), 0.8, 50).view(-1)
+    kept = lf >= lf.topk(50, dim=-1).values[:, -1:]
+    first = torch.argmax(kept.int(), dim=-1)
+    assert torch.equal(u0, first)
+    row = torch.full((1, V), -20.0, device=DEV)
+    hot = [7, 70000, 150001, V - 1]
+    row[0, hot] = torch.tensor([2.0, 1.5, 1.0, 0.0], device=DEV)
+    rows = row.to(dt).expand(2000, V).contiguous()
+    draws = Sa.sample(rows, 1.0, 3).view(-1).cpu()
+    assert bool(torch.isin(draws, torch.tensor(hot[:3])).all())
+    freq = torch.stack([(draws == h).float().mean() for h in hot[:3]])
+    probs = torch.softmax(torch.tensor([2.0, 1.5, 1.0]), -1)
+    assert torch.allclose(freq, probs, atol=0.04), (freq, probs)
