@@ -3,7 +3,14 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--engine fused|generic|reference]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
-One process per GPU (RANK/LOCAL_RANK/WORLD_SIZE from the environment; backend nccl = RCCL).
+One process per GPU (backend nccl = RCCL).  Under torchrun (or any launcher that sets
+``WORLD_SIZE``) each process is one rank.  Started plainly with ``--gpus N > 1`` the script is
+its own launcher, like the reference's ``ddp.py:43-73`` (one worker per visible device): the
+parent never touches the GPU (``torch.cuda.device_count()`` does not initialise HIP), checks
+that N devices are visible — failing loudly otherwise instead of silently measuring one GPU —
+spawns N child ranks with ``RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 /
+MASTER_PORT``, tears the group down if any rank fails, and exits with the first failing code.
+
 Model: the reference's example GPT-2 layer list (``main.py:57-83``: V=50304, C=768, 12 layers,
 12 heads, untied lm_head, 163.1 M params), AdamW(6e-4, (0.9, 0.95), 1e-8, wd 0.01), bf16 compute.
 Data: synthetic uniform token ids of shape [B, T] per rank per step (random-init weights), copied
@@ -12,6 +19,17 @@ tokens per GPU per step (default B=64 → 65,536 tokens/GPU/step, one micro-step
 Timed region: W untimed warmup steps, then exactly K full optimizer steps (forward, backward,
 gradient all-reduce, fused AdamW) bracketed by barrier + synchronize; the max over ranks is
 reported.  Rank 0 prints one JSON line.
+
+Extra fields (outside the timed region):
+  * ``comm``: bucket plan, wire dtype, transport, RCCL version, ranks seen by the communicator,
+    and ``allreduce_exposed_ms`` = ms/step of the timed run minus ms/step of a few further
+    steps with the gradient all-reduce switched off (the part of the collective NOT hidden
+    behind the backward);
+  * ``vs_reference_eager_same_gpu``: the same config through the ``reference`` engine (stock
+    PyTorch eager + autocast + foreach AdamW, the reference's semantics) measured in this same
+    process right after (1 GPU only; ``--ref-steps 0`` skips it).
+``--device cpu`` (gloo, generic engine, pair it with ``--model tiny``) is the plumbing rehearsal
+used by the CPU tests; the headline is always ``--device cuda``.
 """
 from __future__ import annotations
 
@@ -19,6 +37,7 @@ import argparse
 import json
 import math
 import os
+import subprocess
 import sys
 import time
 
@@ -29,10 +48,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-# Reference-semantics eager PyTorch on MI355X, same config (bench/ref_eager_gpt2.py, B=64, T=1024,
-# measured on one MI355X this round: profiles/probe_env_r1.log).  BASELINE.md publishes no GPU
-# number for the reference, so vs_baseline is null and this figure is reported separately.
-REFERENCE_EAGER_TOK_S_PER_GPU = 482820.8
+METRIC = "tokens/sec (whole node) GPT-2 124M DDP train at 1/2/4/8 MI355X"
 
 
 def gpt2_layers(V=50304, C=768, L=12, H=12, P=1024):
@@ -61,105 +77,273 @@ def gpt2_layers(V=50304, C=768, L=12, H=12, P=1024):
 MODELS = {
     "gpt2-124m": dict(V=50304, C=768, L=12, H=12, P=1024),
     "gpt2-xl": dict(V=50304, C=1600, L=48, H=25, P=1024),
+    "tiny": dict(V=512, C=64, L=2, H=2, P=64),  # plumbing rehearsal only
 }
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU); self-launched when WORLD_SIZE is unset")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=64, help="sequences per GPU per step")
-    ap.add_argument("--seq", type=int, default=1024)
-    ap.add_argument("--engine", default="fused", choices=["fused", "generic", "reference"])
+    ap.add_argument("--batch", type=int, default=None, help="sequences per GPU per step (default 64; tiny: 4)")
+    ap.add_argument("--seq", type=int, default=None, help="tokens per sequence (default 1024; tiny: 32)")
+    ap.add_argument("--engine", default=None, choices=["fused", "generic", "reference"],
+                    help="default: fused on cuda, generic on cpu")
     ap.add_argument("--model", default="gpt2-124m", choices=list(MODELS))
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"])
+    ap.add_argument("--ref-steps", type=int, default=4,
+                    help="steps of the reference engine measured after the run for vs_reference_eager_same_gpu "
+                         "(1 GPU, gpt2-124m only; 0 = skip)")
+    ap.add_argument("--nocomm-steps", type=int, default=4,
+                    help="steps without the gradient all-reduce, for allreduce_exposed_ms (world > 1; 0 = skip)")
     ap.add_argument("--profile", default=None, metavar="DIR",
                     help="after the timed steps, profile 3 more under torch.profiler into DIR "
                          "(Chrome trace + per-kernel table); set PENROZ_ROCTX=1 for roctx phase ranges")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
+    tiny = args.model == "tiny"
+    args.batch = args.batch or (4 if tiny else 64)
+    args.seq = args.seq or (32 if tiny else 1024)
+    args.engine = args.engine or ("fused" if args.device == "cuda" else "generic")
+    if args.device == "cpu" and args.engine == "fused":
+        raise SystemExit("the fused engine needs --device cuda")
+    return args
 
+
+# ------------------------------------------------------------------------------- self-launch
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args, argv: list[str], poll_s: float = 0.2) -> int:
+    """Spawn ``args.gpus`` child ranks of this script and supervise them (parent: no GPU use)."""
+    n = args.gpus
+    if args.device == "cuda":
+        visible = torch.cuda.device_count()  # does not initialise HIP on this image
+        if visible < n:
+            print(f"bench.py: --gpus {n} requested but only {visible} GPU(s) are visible; refusing to "
+                  f"report a {n}-GPU number from fewer devices", file=sys.stderr, flush=True)
+            return 2
+    port = _free_port()
+    threads = max(1, (os.cpu_count() or 2) // n)
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+                    "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+                    "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+        if args.device == "cpu":
+            env.setdefault("OMP_NUM_THREADS", str(threads))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            time.sleep(poll_s)
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    print(f"bench.py: rank {procs.index(p)} exited with code {code}; stopping the group",
+                          file=sys.stderr, flush=True)
+                    for q in live:
+                        q.terminate()
+    finally:
+        for p in procs:
+            try:
+                p.wait(timeout=60)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    return rc if rc >= 0 else 128 - rc
+
+
+# ------------------------------------------------------------------------------- one rank
+def _sync(device):
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+
+
+def _comm_info(runner, world: int) -> dict:
+    red = None
+    ex = getattr(runner, "exec", None)
+    if ex is not None:
+        red = ex.reducer
+    elif getattr(runner, "reducer", None) is not None:
+        red = runner.reducer.reducer
+    info = {"nranks": dist.get_world_size() if dist.is_initialized() else 1}
+    try:
+        v = torch.cuda.nccl.version()
+        info["rccl_version"] = ".".join(map(str, v)) if isinstance(v, tuple) else str(v)
+    except Exception:  # no RCCL in this build
+        info["rccl_version"] = None
+    if red is not None:
+        sizes = [(e - s) * red.flat_grad.element_size() / 2**20 for s, e in red.buckets]
+        info.update({"buckets": len(sizes), "bucket_mb": [round(x, 2) for x in sizes],
+                     "wire": "bf16" if red._wire is not None else str(red.flat_grad.dtype).replace("torch.", ""),
+                     "transport": "native-rccl" if red._native is not None else red.backend,
+                     "grad_mb": round(sum(sizes), 2)})
+    return info
+
+
+def _timed(step, n, world, device):
+    if world > 1:
+        dist.barrier()
+    _sync(device)
+    t0 = time.perf_counter()
+    loss = None
+    for i in range(n):
+        loss = step(i)
+    _sync(device)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=device if device.type == "cuda" else "cpu", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt, loss
+
+
+def _build(args, cfg, device, engine, world):
+    from penroz.models.mapper import Mapper
+    from penroz.models.model import NeuralNetworkModel, _make_runner
+    os.environ["PENROZ_ENGINE"] = engine
+    torch.manual_seed(1234)
+    model = NeuralNetworkModel("bench", Mapper(gpt2_layers(**cfg),
+                                               {"adamw": {"lr": 6e-4, "betas": [0.9, 0.95], "eps": 1e-8}}))
+    model.to(device)
+    runner = _make_runner(model, engine, device, distributed=world > 1)
+    model.train()
+    return model, runner
+
+
+def _make_step(runner, pool, device, sync_grads=True):
+    def step(i):
+        buf = pool[i % len(pool)].to(device, non_blocking=True)
+        x, y = buf[:, :-1], buf[:, 1:]
+        runner.zero_grad()
+        loss = runner.micro_step(x.contiguous(), y.contiguous(), 1.0, first=True, last=sync_grads, capture=False)
+        runner.step()
+        return loss
+    return step
+
+
+def _reference_eager_tok_s(args, cfg, device, pool) -> float | None:
+    """Same config through the reference-semantics engine, in this process (1 GPU)."""
+    from penroz.ops import _ext
+    try:
+        model, runner = _build(args, cfg, device, "reference", 1)
+        step = _make_step(runner, pool, device)
+        for i in range(2):
+            step(i)
+        dt, _ = _timed(step, args.ref_steps, 1, device)
+        del model, runner
+        return args.batch * args.seq * args.ref_steps / dt
+    except torch.OutOfMemoryError:
+        return None
+    finally:
+        _ext.FORCE_TORCH = False
+        torch.cuda.empty_cache()
+
+
+def run_rank(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and args.gpus != world:
         raise SystemExit(f"--gpus {args.gpus} != WORLD_SIZE {world}")
-    # PENROZ_BENCH_DEVICE / PENROZ_DIST_BACKEND: rehearsal knobs only (e.g. 2 ranks sharing the
-    # one GPU of a test box over gloo); the headline runs use LOCAL_RANK and nccl (= RCCL).
-    local = int(os.environ.get("PENROZ_BENCH_DEVICE", local))
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    if args.device == "cuda":
+        # PENROZ_BENCH_DEVICE / PENROZ_DIST_BACKEND: rehearsal knobs only (e.g. 2 ranks sharing the
+        # one GPU of a test box over gloo); the headline runs use LOCAL_RANK and nccl (= RCCL).
+        local = int(os.environ.get("PENROZ_BENCH_DEVICE", local))
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+    else:
+        device = torch.device("cpu")
     if world > 1:
-        backend = os.environ.get("PENROZ_DIST_BACKEND", "nccl")
+        backend = os.environ.get("PENROZ_DIST_BACKEND", "nccl" if args.device == "cuda" else "gloo")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=device)
         else:
             dist.init_process_group(backend)
-    os.environ["PENROZ_ENGINE"] = args.engine
-
-    from penroz.models.mapper import Mapper
-    from penroz.models.model import NeuralNetworkModel, _make_runner
 
     cfg = MODELS[args.model]
-    torch.manual_seed(1234)
-    model = NeuralNetworkModel("bench", Mapper(gpt2_layers(**cfg),
-                                               {"adamw": {"lr": 6e-4, "betas": [0.9, 0.95], "eps": 1e-8}}))
-    model.to(device)
-    runner = _make_runner(model, args.engine, device, distributed=world > 1)
-    model.train()
-
     B, T, V = args.batch, args.seq, cfg["V"]
+    if T > cfg["P"]:
+        raise SystemExit(f"--seq {T} exceeds the {args.model} position table ({cfg['P']})")
+    model, runner = _build(args, cfg, device, args.engine, world)
     g = torch.Generator().manual_seed(rank)
-    pool = [torch.randint(0, V, (B, T + 1), generator=g).pin_memory() for _ in range(4)]
-
-    def step(i):
-        buf = pool[i % len(pool)].to(device, non_blocking=True)
-        x, y = buf[:, :-1], buf[:, 1:]
-        runner.zero_grad()
-        loss = runner.micro_step(x.contiguous(), y.contiguous(), 1.0, first=True, last=True, capture=False)
-        runner.step()
-        return loss
+    pool = [torch.randint(0, V, (B, T + 1), generator=g) for _ in range(4)]
+    if device.type == "cuda":
+        pool = [p.pin_memory() for p in pool]
+    step = _make_step(runner, pool, device)
 
     for i in range(args.warmup):
         step(i)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        loss = step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    dt, loss = _timed(step, args.steps, world, device)
     ms = dt / args.steps * 1e3
     tok_s = world * B * T * args.steps / dt
-    if rank == 0:
-        flops_per_tok = 6 * (sum(p.numel() for p in model.parameters()) - cfg["V"] * cfg["C"] - cfg["P"] * cfg["C"]) \
-            + 12 * cfg["L"] * cfg["C"] * T
-        print(json.dumps({
-            "metric": "tokens/sec (whole node) GPT-2 124M DDP train at 1/2/4/8 MI355X" if args.model == "gpt2-124m"
-            else f"tokens/sec (whole node) {args.model} DDP train",
-            "value": tok_s, "unit": "tokens/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "vs_reference_eager_same_gpu": tok_s / (world * REFERENCE_EAGER_TOK_S_PER_GPU) if args.model == "gpt2-124m" else None,
-            "mfu_bf16_dense": tok_s / world * flops_per_tok / 2.5e15,
-            "final_loss": float(loss.item()), "engine": args.engine,
-            "dtype": "bf16", "data": "synthetic uniform tokens, random-init weights",
-            "config": {"model": args.model, "global_batch": world * B, "seq_len": T, "micro_batch_per_gpu": B,
-                       "tokens_per_step": world * B * T, "parallelism": f"dp{world}"},
-        }), flush=True)
+    final_loss = float(loss.item())
+
+    comm = _comm_info(runner, world)
+    if world > 1 and args.nocomm_steps > 0:  # outside the timed region
+        dt0, _ = _timed(_make_step(runner, pool, device, sync_grads=False), args.nocomm_steps, world, device)
+        comm["ms_per_step_without_allreduce"] = dt0 / args.nocomm_steps * 1e3
+        comm["allreduce_exposed_ms"] = max(0.0, ms - comm["ms_per_step_without_allreduce"])
+    elif world == 1:
+        comm["allreduce_exposed_ms"] = 0.0
+
     if args.profile:  # outside the timed region
         from penroz.utils.profiling import profile_steps
         out = os.path.join(args.profile, f"rank{rank}")
         table = profile_steps(lambda: step(0), 3, out)
         if rank == 0:
             print(table, file=sys.stderr)
+
+    n_params = sum(p.numel() for p in model.parameters())
+    ref_tok_s = None
+    if (world == 1 and device.type == "cuda" and args.engine == "fused" and args.ref_steps > 0
+            and args.model == "gpt2-124m"):
+        ex = getattr(runner, "exec", None)
+        if ex is not None:
+            ex.free_buffers()
+        del runner, model
+        torch.cuda.empty_cache()
+        ref_tok_s = _reference_eager_tok_s(args, cfg, device, pool)
+
+    if rank == 0:
+        flops_per_tok = 6 * (n_params - cfg["V"] * cfg["C"] - cfg["P"] * cfg["C"]) + 12 * cfg["L"] * cfg["C"] * T
+        print(json.dumps({
+            "metric": METRIC if args.model == "gpt2-124m" else f"tokens/sec (whole node) {args.model} DDP train",
+            "value": tok_s, "unit": "tokens/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "vs_reference_eager_same_gpu": (tok_s / ref_tok_s) if ref_tok_s else None,
+            "reference_eager_tok_s": ref_tok_s,
+            "mfu_bf16_dense": tok_s / world * flops_per_tok / 2.5e15 if device.type == "cuda" else None,
+            "final_loss": final_loss, "engine": args.engine, "device": args.device,
+            "dtype": "bf16" if device.type == "cuda" else "fp32",
+            "data": "synthetic uniform tokens, random-init weights",
+            "comm": comm,
+            "config": {"model": args.model, "global_batch": world * B, "seq_len": T, "micro_batch_per_gpu": B,
+                       "tokens_per_step": world * B * T, "parallelism": f"dp{world}"},
+        }), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse_args(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args, argv))
+    run_rank(args)
 
 
 if __name__ == "__main__":

@@ -57,3 +57,51 @@ def test_bench_cli_help():
     assert r.returncode == 0
     for flag in ("--gpus", "--steps", "--warmup", "--profile"):
         assert flag in r.stdout
+
+
+def _run_bench(args, env_extra=None, timeout=300):
+    import subprocess
+    import sys
+    env = dict(os.environ)
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                          timeout=timeout, env=env)
+
+
+def _json_line(out: str) -> dict:
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+@pytest.mark.slow
+def test_bench_self_launches_ranks_cpu_gloo():
+    """`python bench.py --gpus 2` (no torchrun) spawns 2 ranks itself; rank 0 prints ONE JSON line
+    with n_gpus == 2 and the communicator's view of the group (2-rank gloo rehearsal)."""
+    r = _run_bench(["--gpus", "2", "--device", "cpu", "--model", "tiny", "--steps", "2", "--warmup", "1",
+                    "--nocomm-steps", "1"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2"
+    assert d["config"]["global_batch"] == 2 * d["config"]["micro_batch_per_gpu"]
+    assert d["comm"]["nranks"] == 2 and d["comm"]["transport"] == "gloo" and d["comm"]["buckets"] >= 1
+    assert d["comm"]["allreduce_exposed_ms"] >= 0.0
+    assert d["steps"] == 2 and d["warmup"] == 1 and d["value"] > 0
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    """No silent 1-GPU number for `--gpus 2` on a box with fewer devices (here: none)."""
+    r = _run_bench(["--gpus", "2", "--steps", "1", "--warmup", "0"], timeout=120)
+    assert r.returncode != 0
+    assert "GPU(s) are visible" in r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+@pytest.mark.slow
+def test_bench_rank_failure_stops_group():
+    """A failing rank ends the self-launched group with a nonzero exit code (no hang)."""
+    r = _run_bench(["--gpus", "2", "--device", "cpu", "--model", "tiny", "--steps", "1", "--warmup", "0",
+                    "--seq", "4096"], timeout=120)
+    assert r.returncode != 0
