@@ -16,11 +16,14 @@ replayed. Everything that changes between steps lives on the device:
   K/V (read in place from the fused QKV rows, int8-quantised for TurboQuant) at slot
   ``len_t - 1 = pos_t`` itself (``csrc/kernels/decode_attn.hip``: ``k_new``, ``seq_len_dev``);
 * ``PositionEmbedding.position_offset_tensor``: the learned position gathered at ``pos_t``;
-* the sampler hashes its uniforms on the device from (per-burst seed, step, row) and writes the
-  token straight into the next step's input and the burst output buffer; one tiny kernel then
-  advances the position / length / step counters;
+* the sampler hashes its uniforms on the device from (seed of the generate call, absolute token
+  index, row) and writes the token straight into the next step's input and the burst output
+  buffer; one tiny kernel then advances the position / length / step counters. Streaming and
+  non-streaming calls therefore draw identical tokens under the same ``torch.manual_seed``;
 * the step's ``nn.Linear`` GEMMs (M = rows ≤ 64) run on the decode-shaped MFMA kernel
-  (``ops/gemm.py: decode_gemms``, ``csrc/kernels/skinny_gemm.hip``).
+  (``csrc/kernels/skinny_gemm.hip``): called explicitly by the decode programs, or — for the
+  module-forward fallback — through ``ops/gemm.py: decode_gemms(model)``, which re-routes only
+  that model's own ``nn.Linear`` instances for the capture.
 
 The host only tracks the cache length (one per replay) to switch to the reference's
 sliding-window re-prefill when the window is full, and copies each burst of tokens back once
@@ -345,7 +348,7 @@ class GraphDecoder:
             if self.program is not None:
                 last = self.program.forward(self.idx, self.cache)
             else:
-                with gemm_ops.decode_gemms(max_rows=SKINNY_MAX_ROWS):
+                with gemm_ops.decode_gemms(self.model, max_rows=SKINNY_MAX_ROWS):
                     acts, _ = self.model(self.idx, skip_softmax=True)
                 logits = acts[-1]
                 last = logits[:, -1, :] if logits.ndim == 3 else logits
@@ -369,43 +372,60 @@ class GraphDecoder:
             for p in self.pos_layers:
                 p.position_offset_tensor = None
 
-    def _set_state(self, last_tok: Tensor, cache_len: int):
-        # drawn from torch's generator: reproducible under torch.manual_seed, fresh every burst
-        self.seed_t.fill_(int(torch.randint(0, 2 ** 62, (1,)).item()))
+    # The sampler kernel hashes each uniform from (seed_t, step_t, row) as
+    #   seed + G·(step + 1) + R·(row + 1)  (mod 2^64, csrc/kernels/sampling.hip),
+    # with step_t counting from 0 inside a burst. Loading seed_t = run_seed + G·start for a burst
+    # that starts at absolute token index ``start`` makes every draw a function of
+    # (run seed, absolute index, row) alone: how the tokens are cut into bursts (streaming = bursts
+    # of 1, non-streaming = one long burst), and whether the graph was captured in this call or
+    # reused, no longer changes them.
+    _HASH_STEP = 0x9E3779B97F4A7C15
+
+    def begin(self, run_seed: int):
+        """Once per generate call: the seed every burst of this call derives from."""
+        self.run_seed = int(run_seed) & (2 ** 64 - 1)
+
+    def _burst_seed(self, start: int) -> int:
+        v = (getattr(self, "run_seed", 0) + self._HASH_STEP * int(start)) & (2 ** 64 - 1)
+        return v - 2 ** 64 if v >= 2 ** 63 else v
+
+    def _set_state(self, last_tok: Tensor, cache_len: int, start: int = 0):
+        self.seed_t.fill_(self._burst_seed(start))
         self.idx.copy_(last_tok)
         self.cache.pos_t.fill_(cache_len)
         self.cache.len_t.fill_(cache_len + 1)
         self.step_t.zero_()
 
-    def _capture(self, last_tok: Tensor, cache_len: int):
+    def _capture(self, last_tok: Tensor, cache_len: int, start: int = 0):
         # warm-up run on a side stream (lazy allocations, kernel loading), then capture. The
         # warm-up really executes a step, so it must start from the true state: it then writes
         # exactly the cache slot the first real step rewrites.
-        self._set_state(last_tok, cache_len)
+        self._set_state(last_tok, cache_len, start)
         side = torch.cuda.Stream(device=self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):
             self._step()
         torch.cuda.current_stream(self.device).wait_stream(side)
-        self._set_state(last_tok, cache_len)
+        self._set_state(last_tok, cache_len, start)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self._step()
         self.graph = g
-        self._set_state(last_tok, cache_len)  # capture does not execute; state is as before
+        self._set_state(last_tok, cache_len, start)  # capture does not execute; state is as before
         log.info(f"captured decode graph: rows={self.rows} block={self.capacity} "
                  f"temperature={self.temperature} top_k={self.top_k}")
 
     @torch.inference_mode()
-    def run(self, last_tok: Tensor, n_steps: int) -> Tensor:
+    def run(self, last_tok: Tensor, n_steps: int, start: int = 0) -> Tensor:
         """Decode ``n_steps`` tokens after ``last_tok`` [rows, 1] from the current cache; returns
-        the [rows, n_steps] new tokens (device). The cache must have room for n_steps more."""
+        the [rows, n_steps] new tokens (device). ``start``: absolute index (within this generate
+        call) of the first of them. The cache must have room for n_steps more."""
         cache_len = self.cache.seq_len()
         assert 0 < cache_len and cache_len + n_steps <= self.capacity, (cache_len, n_steps, self.capacity)
         if self.graph is None:
-            self._capture(last_tok, cache_len)
+            self._capture(last_tok, cache_len, start)
         else:
-            self._set_state(last_tok, cache_len)
+            self._set_state(last_tok, cache_len, start)
         for _ in range(n_steps):
             self.graph.replay()
         self.cache._len = [cache_len + n_steps] * self.cache.num_layers

@@ -119,9 +119,10 @@ class NeuralNetworkModel(nn.Module):
         if ddp.master_proc():
             log.info(f"Caching model to {shm_path}...")
         ckpt.atomic_torch_save(data, shm_path)
-        ckpt.atomic_json(self._progress_doc(), ckpt.sidecar_path(shm_path))
+        for base in (shm_path, model_path):  # small JSON sidecars: /progress and /stats never load weights
+            ckpt.atomic_json(self._progress_doc(), ckpt.sidecar_path(base))
+            ckpt.atomic_json({"stats": self.stats}, ckpt.sidecar_path(base, "stats"))
         ckpt.flush_async(shm_path, model_path)
-        ckpt.atomic_json(self._progress_doc(), ckpt.sidecar_path(model_path))
 
     @classmethod
     def _ensure_cached(cls, model_id: str) -> str:
@@ -173,6 +174,18 @@ class NeuralNetworkModel(nn.Module):
         return m._progress_doc()
 
     @classmethod
+    def read_stats(cls, model_id: str):
+        """Training stats from the stats sidecar, falling back to the checkpoint."""
+        model_path = cls.get_model_path(model_id)
+        for p in (ckpt.sidecar_path(os.path.join(cls.SHM_PATH, model_path), "stats"),
+                  ckpt.sidecar_path(model_path, "stats")):
+            if os.path.exists(p):
+                import json
+                with open(p) as f:
+                    return json.load(f)["stats"]
+        return cls.deserialize(model_id).stats
+
+    @classmethod
     def mark_status(cls, model_id: str, code: str, message: str):
         """Rewrite a stored model's status (e.g. ``Error`` after a worker crash)."""
         model = cls.deserialize(model_id)
@@ -184,7 +197,8 @@ class NeuralNetworkModel(nn.Module):
     def delete(cls, model_id: str):
         model_path = cls.get_model_path(model_id)
         shm_path = os.path.join(cls.SHM_PATH, model_path)
-        for p in (shm_path, ckpt.sidecar_path(shm_path), model_path, ckpt.sidecar_path(model_path)):
+        for p in (shm_path, ckpt.sidecar_path(shm_path), ckpt.sidecar_path(shm_path, "stats"), model_path,
+                  ckpt.sidecar_path(model_path), ckpt.sidecar_path(model_path, "stats")):
             try:
                 os.remove(p)
             except FileNotFoundError as e:
@@ -389,11 +403,15 @@ class NeuralNetworkModel(nn.Module):
         if dec is None:
             cache, pos = self._attach_kv_cache(capacity=block_size)
         else:
+            # one seed per generate call, drawn from torch's generator before any token: graph-
+            # sampled tokens depend on (seed, absolute index, row) only (graph_decode.begin)
+            dec.begin(int(torch.randint(0, 2 ** 62, (1,)).item()) if temperature else 0)
             dec.attach()
             cache, pos = dec.cache, dec.pos_layers
             cache.clear()
         try:
             remaining = max_new_tokens
+            produced = 0
             last = None
             while remaining > 0:
                 n = cache.seq_len() if cache is not None else 0
@@ -404,10 +422,11 @@ class NeuralNetworkModel(nn.Module):
                         p.position_offset = 0
                 else:
                     k = min(remaining, block_size - n, burst)
-                    new = dec.run(last, k)
+                    new = dec.run(last, k, start=produced)
                 context = torch.cat((context, new.to(context.device)), dim=1)
                 last = context[:, -1:]
                 remaining -= new.shape[1]
+                produced += new.shape[1]
                 yield new
         finally:
             if cache is not None:
@@ -615,6 +634,7 @@ class NeuralNetworkModel(nn.Module):
             self._record_training_overall_progress(runner.captured())
             self.serialize()
         runner.close()
+        ckpt.wait_flushes()  # the disk copy is complete when training returns
 
     @torch.no_grad()
     def _record_training_overall_progress(self, captured):

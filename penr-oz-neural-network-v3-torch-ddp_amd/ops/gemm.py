@@ -121,34 +121,37 @@ def skinny_linear(x: Tensor, w: Tensor, bias: Tensor | None) -> Tensor:
 
 
 class decode_gemms:
-    """Context: ``nn.Linear`` modules run decode-shaped inputs through the skinny kernel (others
-    keep ``F.linear``). Entered by the graph decoder around the captured step."""
+    """Context: the ``nn.Linear`` modules of ``model`` run decode-shaped inputs through the skinny
+    kernel (others keep ``F.linear``). Entered by the graph decoder around the captured step of a
+    model without a decode program. Only that model's own Linear instances are re-routed (an
+    instance-level ``forward``, removed on exit): other models, and other threads serving them,
+    are untouched; the serving lock keeps concurrent requests off the same model."""
 
-    _orig = None
-
-    def __init__(self, max_rows: int = 64):
+    def __init__(self, model: torch.nn.Module, max_rows: int = 64):
+        self.model = model
         self.max_rows = max_rows
+        self._patched: list[torch.nn.Linear] = []
 
     def __enter__(self):
-        if decode_gemms._orig is None and SKINNY_GEMM and self.max_rows > 0:
-            orig = torch.nn.Linear.forward
-            max_rows = self.max_rows
+        if not (SKINNY_GEMM and self.max_rows > 0):
+            return self
+        max_rows = self.max_rows
+        for mod in self.model.modules():
+            if type(mod) is not torch.nn.Linear or "forward" in mod.__dict__:
+                continue
 
-            def forward(mod, x):
+            def forward(x, mod=mod):
                 if (x.numel() <= max_rows * x.shape[-1] and skinny_ok(x, mod.weight)
                         and (mod.bias is None or mod.bias.is_contiguous())):
                     return skinny_linear(x, mod.weight, mod.bias)
-                return orig(mod, x)
+                return torch.nn.functional.linear(x, mod.weight, mod.bias)
 
-            decode_gemms._orig = orig
-            torch.nn.Linear.forward = forward
-            self._owner = True
-        else:
-            self._owner = False
+            mod.forward = forward
+            self._patched.append(mod)
         return self
 
     def __exit__(self, *exc):
-        if self._owner:
-            torch.nn.Linear.forward = decode_gemms._orig
-            decode_gemms._orig = None
+        for mod in self._patched:
+            mod.__dict__.pop("forward", None)
+        self._patched.clear()
         return False

@@ -199,6 +199,21 @@ _cache_lock = threading.Lock()
 _model_cache: dict[str, tuple[float, NeuralNetworkModel]] = {}
 
 
+def serving_lock(model: NeuralNetworkModel) -> threading.Lock:
+    """The lock every request holds while it runs on ``model``.
+
+    A cached serving model is ONE module tree shared by all requests; generation attaches its
+    KV cache / graph decoder to that tree and moves position offsets, so two requests must never
+    run on it at once (the reference rebuilt a private model per request, ``main.py:401-434``).
+    A plain ``Lock`` (not ``RLock``): a streaming response acquires it on the threadpool thread
+    of its first chunk and may release it on another."""
+    lk = model.__dict__.get("_serve_lock")
+    if lk is None:
+        with _cache_lock:
+            lk = model.__dict__.setdefault("_serve_lock", threading.Lock())
+    return lk
+
+
 def _checkpoint_mtime(model_id: str) -> float | None:
     p = os.path.join(NeuralNetworkModel.SHM_PATH, NeuralNetworkModel.get_model_path(model_id))
     if not os.path.exists(p):
@@ -305,15 +320,17 @@ def tokenize_text(body: TokenizeTextRequest = Body(...)):
 @app.post("/output/")
 def compute_model_output(body: OutputRequest = Body(...)):
     model = load_for_serving(body.model_id)
-    output, cost = model.compute_output(body.input, body.target)
+    with serving_lock(model):
+        output, cost = model.compute_output(body.input, body.target)
     return {"output": output, "cost": cost}
 
 
 @app.post("/evaluate/")
 def evaluate_model(body: EvaluateRequest = Body(...)):
     model = load_for_serving(body.model_id)
-    cost = model.evaluate_model(body.dataset_id, body.target_dataset_id, body.shard, body.epochs, body.batch_size,
-                                body.block_size, body.step_size)
+    with serving_lock(model):
+        cost = model.evaluate_model(body.dataset_id, body.target_dataset_id, body.shard, body.epochs,
+                                    body.batch_size, body.block_size, body.step_size)
     return {"cost": cost}
 
 
@@ -322,12 +339,16 @@ def model_generate(body: GenerateRequest = Body(...)):
     model = load_for_serving(body.model_id)
     if body.stream:
         def token_stream():
-            for token in model.generate_tokens_stream(body.input, body.block_size, body.max_new_tokens,
-                                                      body.temperature, body.top_k, body.stop_token):
-                yield f"{token}\n"
+            # held for the stream's whole lifetime (the KV cache stays attached between chunks);
+            # a disconnected client's generator is closed on collection, which releases it
+            with serving_lock(model):
+                for token in model.generate_tokens_stream(body.input, body.block_size, body.max_new_tokens,
+                                                          body.temperature, body.top_k, body.stop_token):
+                    yield f"{token}\n"
         return StreamingResponse(token_stream(), media_type="text/plain")
-    tokens = model.generate_tokens(body.input, body.block_size, body.max_new_tokens, body.temperature, body.top_k,
-                                   body.stop_token)
+    with serving_lock(model):
+        tokens = model.generate_tokens(body.input, body.block_size, body.max_new_tokens, body.temperature,
+                                       body.top_k, body.stop_token)
     return {"tokens": tokens}
 
 
@@ -379,7 +400,7 @@ def model_progress(model_id: str = ModelIdQuery(...)):
 
 @app.get("/stats/")
 def model_stats(model_id: str = ModelIdQuery(...)):
-    return NeuralNetworkModel.deserialize(model_id).stats
+    return NeuralNetworkModel.read_stats(model_id)
 
 
 @app.delete("/model/")

@@ -71,25 +71,53 @@ def atomic_json(obj, path: str):
     _atomic_write(path, w)
 
 
+_flush_lock = threading.Lock()
+_flush_dst: dict[str, dict] = {}   # absolute destination -> {"gen", "lock"}
 _flushers: list[threading.Thread] = []
 
 
+def _flush_one(src: str, dst: str, st: dict, gen: int):
+    with st["lock"]:  # one copy at a time per destination, in queue order
+        if st["gen"] != gen:
+            return  # a newer save of this destination is queued behind us: its copy wins
+        try:
+            atomic_copy(src, dst)
+        except FileNotFoundError:  # the cached file was deleted (model deleted) before the flush
+            log.warning(f"flush skipped: {src} no longer exists")
+
+
 def flush_async(src: str, dst: str) -> threading.Thread:
-    t = threading.Thread(target=atomic_copy, args=(src, dst), name=f"flush-{os.path.basename(dst)}")
+    """Copy ``src`` to ``dst`` atomically on a background thread.
+
+    Paths are made absolute when the flush is queued (a later ``chdir`` cannot redirect it).
+    Flushes to one destination are serialised and carry a generation number: a flush whose
+    save has been superseded before it starts copying is skipped, so the disk copy can only
+    move forward to the newest snapshot, never back to an older one."""
+    src, dst = os.path.abspath(src), os.path.abspath(dst)
+    with _flush_lock:
+        st = _flush_dst.setdefault(dst, {"gen": 0, "lock": threading.Lock()})
+        st["gen"] += 1
+        gen = st["gen"]
+        t = threading.Thread(target=_flush_one, args=(src, dst, st, gen), name=f"flush-{os.path.basename(dst)}")
+        _flushers[:] = [x for x in _flushers if x.is_alive()]
+        _flushers.append(t)
     t.start()
-    _flushers.append(t)
-    _flushers[:] = [x for x in _flushers if x.is_alive()]
     return t
 
 
 def wait_flushes():
-    for t in list(_flushers):
+    with _flush_lock:
+        pending = list(_flushers)
+    for t in pending:
         t.join()
-    _flushers.clear()
+    with _flush_lock:
+        _flushers[:] = [x for x in _flushers if x.is_alive()]
 
 
-def sidecar_path(pth_path: str) -> str:
-    return pth_path[:-4] + ".progress.json" if pth_path.endswith(".pth") else pth_path + ".progress.json"
+def sidecar_path(pth_path: str, kind: str = "progress") -> str:
+    """``model_x.pth`` -> ``model_x.progress.json`` (progress/status) or ``model_x.stats.json``."""
+    base = pth_path[:-4] if pth_path.endswith(".pth") else pth_path
+    return f"{base}.{kind}.json"
 
 
 def load(path: str) -> dict:

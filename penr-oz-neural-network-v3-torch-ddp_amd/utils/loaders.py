@@ -10,8 +10,9 @@ Fixes / MI355X-first changes:
   * progress logging never divides by zero for small shards (bug 13);
   * ``target_offset=0`` returns the same ``(input, target)`` tuple shape (targets may come from
     a second loader; the reference's evaluate path crashed on it — bug 1);
-  * shards are memory-mapped (``mmap_mode='r'``) so 288 GB-class corpora stream instead of
-    being loaded whole per rank;
+  * shards are memory-mapped (``mmap_mode='r'``) and never converted whole: the loader keeps a
+    view of (the unread tail of the previous shard, the current shard) and converts only each
+    batch window to int32, so a rank touches the pages it reads and nothing more;
   * :func:`synthetic_shards` writes uniform-random shards for benchmarks/tests (no network).
 """
 from __future__ import annotations
@@ -97,7 +98,7 @@ class Loader:
         self.buffer_size = buffer_size
         self.idx_offset = idx_offset
         self.token_idx = begin_idx
-        self.tokens = np.empty((0,), dtype=np.int32)
+        self.tokens = _Window([])
 
     def list(self) -> list[str]:
         return self.shards
@@ -107,24 +108,65 @@ class Loader:
             os.remove(os.path.join(DATA_FOLDER, shard))
 
     def _load(self) -> np.ndarray:
+        """The current shard as a read-only memory map (uint16/uint32 on disk, not converted)."""
         if not self.shards:
             raise KeyError("no shards found for dataset")
-        arr = np.load(os.path.join(DATA_FOLDER, self.shards[self.shard_idx % len(self.shards)]), mmap_mode="r")
-        return np.asarray(arr, dtype=np.int32)
+        return np.load(os.path.join(DATA_FOLDER, self.shards[self.shard_idx % len(self.shards)]), mmap_mode="r")
 
     def next_batch(self, target_offset: int = 1) -> Tuple[np.ndarray, np.ndarray | None]:
+        """Reference semantics (``loaders.py:65-87``): input = tokens[i : i+buffer], target shifted
+        by ``target_offset``, advance by ``idx_offset``; when the window would run past the
+        buffered tokens, the unread tail is carried over and the next shard appended (wrapping)."""
         if len(self.tokens) == 0:
-            self.tokens = self._load()
+            self.tokens = _Window([self._load()])
         for _ in range(max(1, len(self.shards))):
             if len(self.tokens) < self.token_idx + self.idx_offset + target_offset:
                 self.shard_idx = (self.shard_idx + 1) % len(self.shards)
-                self.tokens = np.concatenate((self.tokens[self.token_idx:], self._load()))
+                self.tokens = _Window(self.tokens.tail(self.token_idx) + [self._load()])
                 self.token_idx = 0
             else:
                 break
-        inp = self.tokens[self.token_idx: self.token_idx + self.buffer_size]
+        i = self.token_idx
+        inp = self.tokens.slice(i, i + self.buffer_size)
         tgt = None
         if target_offset > 0:
-            tgt = self.tokens[self.token_idx + target_offset: self.token_idx + self.buffer_size + target_offset]
+            tgt = self.tokens.slice(i + target_offset, i + self.buffer_size + target_offset)
         self.token_idx += self.idx_offset
         return inp, tgt
+
+
+class _Window:
+    """A logical concatenation of 1-D arrays (memory maps or views) without copying them."""
+
+    def __init__(self, parts: list[np.ndarray]):
+        self.parts = [p for p in parts if len(p)]
+        self.n = sum(len(p) for p in self.parts)
+
+    def __len__(self) -> int:
+        return self.n
+
+    def tail(self, start: int) -> list[np.ndarray]:
+        """Views of everything from ``start`` on."""
+        out = []
+        for p in self.parts:
+            if start >= len(p):
+                start -= len(p)
+                continue
+            out.append(p[start:])
+            start = 0
+        return out
+
+    def slice(self, a: int, b: int) -> np.ndarray:
+        """tokens[a:b] as int32 (only this window is read from the shard files)."""
+        b = min(b, self.n)
+        chunks, off = [], 0
+        for p in self.parts:
+            lo, hi = max(a - off, 0), min(b - off, len(p))
+            if lo < hi:
+                chunks.append(np.asarray(p[lo:hi], dtype=np.int32))
+            off += len(p)
+            if off >= b:
+                break
+        if not chunks:
+            return np.empty((0,), dtype=np.int32)
+        return chunks[0] if len(chunks) == 1 else np.concatenate(chunks)

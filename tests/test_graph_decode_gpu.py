@@ -192,3 +192,24 @@ def test_gemma_program_graph_replay_matches_eager_program(monkeypatch):
 
     monkeypatch.setattr(gd.GraphDecoder, "_capture", eager_capture)
     assert m.generate_batch(ctx, 16, 30, temperature=0.0) == graphed
+
+
+@pytest.mark.parametrize("top_k", [None, 5])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_seeded_stream_equals_non_stream_with_sampling(dtype, top_k):
+    """Reference test_neural_net_model.py:289-304 at temperature 1.0 on the GPU: under the same
+    torch.manual_seed the streamed tokens (graph bursts of 1) equal the non-streamed ones (one long
+    burst), through the sliding-window re-prefill, with a freshly captured AND a reused graph."""
+    m = _model(dtype)
+    ctx = [[7, 3, 9]]
+    for _ in range(2):  # 1st: the stream captures the graph; 2nd: both reuse it
+        torch.manual_seed(42)
+        streamed = list(m.generate_tokens_stream(ctx, 16, 40, temperature=1.0, top_k=top_k))
+        torch.manual_seed(42)
+        full = m.generate_tokens(ctx, 16, 40, temperature=1.0, top_k=top_k)
+        assert len(streamed) == 40
+        assert full == ctx[0] + streamed
+    assert any(d.graph is not None for d in m._graph_decoders.values()), "graph path not taken"
+    torch.manual_seed(43)
+    other = m.generate_tokens(ctx, 16, 40, temperature=1.0, top_k=top_k)
+    assert other != full  # the seed matters

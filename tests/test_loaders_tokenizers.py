@@ -91,3 +91,51 @@ def test_tokenizer_tiktoken():
     with patch.dict(sys.modules, {"tiktoken": fake}):
         t = tokenizers.Tokenizer("tiktoken/gpt2")
         assert t.tokenize("x") == [1, 2, 50256] and t.decode([1]) == "ok"
+
+
+class _EagerLoader:
+    """The reference loader's arithmetic (loaders.py:65-87) on fully materialised int32 shards."""
+
+    def __init__(self, shards, begin_shard, begin_idx, buffer_size, idx_offset):
+        self.shards, self.shard_idx = shards, begin_shard
+        self.buffer_size, self.idx_offset, self.token_idx = buffer_size, idx_offset, begin_idx
+        self.tokens = np.empty((0,), dtype=np.int32)
+
+    def next_batch(self, target_offset=1):
+        if len(self.tokens) == 0:
+            self.tokens = self.shards[self.shard_idx % len(self.shards)].astype(np.int32)
+        for _ in range(len(self.shards)):
+            if len(self.tokens) < self.token_idx + self.idx_offset + target_offset:
+                self.shard_idx = (self.shard_idx + 1) % len(self.shards)
+                self.tokens = np.concatenate((self.tokens[self.token_idx:], self.shards[self.shard_idx].astype(np.int32)))
+                self.token_idx = 0
+            else:
+                break
+        i = self.token_idx
+        inp = self.tokens[i:i + self.buffer_size]
+        tgt = self.tokens[i + target_offset:i + self.buffer_size + target_offset] if target_offset > 0 else None
+        self.token_idx += self.idx_offset
+        return inp, tgt
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_mmap_window_loader_matches_eager_semantics(workdir, seed):
+    import penroz.utils.loaders as L
+    rng = np.random.default_rng(seed)
+    nsh = int(rng.integers(1, 4))
+    sizes = [int(rng.integers(20, 120)) for _ in range(nsh)]
+    arrs = [rng.integers(0, 70000 if seed % 2 else 500, n) for n in sizes]
+    for i, a in enumerate(arrs):
+        L.save_shard(f"w{seed}", i, a, 70000 if seed % 2 else 500)
+    buf = int(rng.integers(4, 24))
+    world = int(rng.integers(1, 3))
+    rank = int(rng.integers(0, world))
+    tofs = int(rng.integers(0, 2))
+    got = L.Loader(f"w{seed}", 0, buf * rank, buf, buf * world)
+    assert isinstance(got._load(), np.memmap)
+    ref = _EagerLoader([np.asarray(a) for a in arrs], 0, buf * rank, buf, buf * world)
+    for _ in range(25):
+        gi, gt = got.next_batch(tofs)
+        ri, rt = ref.next_batch(tofs)
+        assert gi.dtype == np.int32 and np.array_equal(gi, ri)
+        assert (gt is None and rt is None) or np.array_equal(gt, rt)
