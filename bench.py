@@ -77,8 +77,19 @@ def gpt2_layers(V=50304, C=768, L=12, H=12, P=1024):
 MODELS = {
     "gpt2-124m": dict(V=50304, C=768, L=12, H=12, P=1024),
     "gpt2-xl": dict(V=50304, C=1600, L=48, H=25, P=1024),
+    # the /import/ of HF "gpt2": V = 50257, tanh GELU, embd/resid/attn dropout 0.1, bf16 params
+    # (reference mappers.py:122-176, neural_net_model.py:222); random init, no download
+    "gpt2-hf": dict(V=50257, C=768, L=12, H=12, P=1024, hf=True),
     "tiny": dict(V=512, C=64, L=2, H=2, P=64),  # plumbing rehearsal only
 }
+
+
+def hf_gpt2_layers(V, C, L, H, P, pdrop=0.1):
+    from types import SimpleNamespace
+    from penroz.models import hf
+    cfg = SimpleNamespace(vocab_size=V, n_embd=C, n_head=H, n_layer=L, n_positions=P, activation_function="gelu_new",
+                          resid_pdrop=pdrop, embd_pdrop=pdrop, attn_pdrop=pdrop, model_type="gpt2")
+    return hf.gpt2_layers(cfg)
 
 
 def parse_args(argv=None):
@@ -216,9 +227,16 @@ def _build(args, cfg, device, engine, world):
     from penroz.models.model import NeuralNetworkModel, _make_runner
     os.environ["PENROZ_ENGINE"] = engine
     torch.manual_seed(1234)
-    model = NeuralNetworkModel("bench", Mapper(gpt2_layers(**cfg),
-                                               {"adamw": {"lr": 6e-4, "betas": [0.9, 0.95], "eps": 1e-8}}))
+    dims = {k: cfg[k] for k in ("V", "C", "L", "H", "P")}
+    layers = hf_gpt2_layers(**dims) if cfg.get("hf") else gpt2_layers(**dims)
+    model = NeuralNetworkModel("bench", Mapper(layers, {"adamw": {"lr": 6e-4, "betas": [0.9, 0.95], "eps": 1e-8}}))
+    if cfg.get("hf"):
+        for mod in model.modules():
+            if isinstance(mod, (torch.nn.Linear, torch.nn.Embedding)):
+                torch.nn.init.normal_(mod.weight, 0.0, 0.02)
     model.to(device)
+    if cfg.get("hf") and device.type == "cuda":
+        model.to(dtype=torch.bfloat16)  # what /import/ produces
     runner = _make_runner(model, engine, device, distributed=world > 1)
     model.train()
     return model, runner

@@ -6,10 +6,10 @@ void layernorm_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor b, double eps
                    torch::Tensor rstd);
 void add_layernorm_fwd(torch::Tensor resid_in, torch::Tensor delta, torch::Tensor resid_out, torch::Tensor w,
                        torch::Tensor b, double eps, torch::Tensor y, torch::Tensor mean, torch::Tensor rstd,
-                       c10::optional<torch::Tensor> delta_bias);
+                       c10::optional<torch::Tensor> delta_bias, double dropout_p, int64_t dropout_seed);
 void layernorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor mean, torch::Tensor rstd, torch::Tensor w,
                    torch::Tensor dresid, bool accumulate, c10::optional<torch::Tensor> dresid_bf, torch::Tensor dw,
-                   torch::Tensor db, c10::optional<torch::Tensor> dbias_prev);
+                   torch::Tensor db, c10::optional<torch::Tensor> dbias_prev, double dropout_p, int64_t dropout_seed);
 // rmsnorm.hip
 std::vector<torch::Tensor> rmsnorm_fwd(torch::Tensor x, torch::Tensor w, double eps);
 std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor w, torch::Tensor rstd);
@@ -24,8 +24,9 @@ torch::Tensor gated_act_packed(torch::Tensor gu, int64_t kind);
 std::vector<torch::Tensor> gated_act_bwd(torch::Tensor dy, torch::Tensor g, torch::Tensor u, int64_t kind);
 void transpose_bf16(torch::Tensor in, torch::Tensor out);
 void embedding_fwd(torch::Tensor idx, torch::Tensor wte, torch::Tensor wpe, int64_t off, torch::Tensor out,
-                   c10::optional<torch::Tensor> off_dev);
-void embedding_bwd(torch::Tensor dout, torch::Tensor idx, torch::Tensor dwte, torch::Tensor dwpe, int64_t off);
+                   c10::optional<torch::Tensor> off_dev, double dropout_p, int64_t dropout_seed);
+void embedding_bwd(torch::Tensor dout, torch::Tensor idx, torch::Tensor dwte, torch::Tensor dwpe, int64_t off,
+                   double dropout_p, int64_t dropout_seed);
 torch::Tensor rope_qkv(torch::Tensor qkv, torch::Tensor cosv, torch::Tensor sinv, int64_t H, int64_t Hkv, int64_t D,
                        bool inverse);
 void kv_quantize(torch::Tensor x, torch::Tensor q, torch::Tensor scale, int64_t pos);
@@ -77,8 +78,12 @@ PYBIND11_MODULE(penroz_kernels, m) {
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("add_layernorm_fwd", &add_layernorm_fwd, pybind11::arg("resid_in"), pybind11::arg("delta"),
         pybind11::arg("resid_out"), pybind11::arg("w"), pybind11::arg("b"), pybind11::arg("eps"), pybind11::arg("y"),
-        pybind11::arg("mean"), pybind11::arg("rstd"), pybind11::arg("delta_bias") = pybind11::none());
-  m.def("layernorm_bwd", &layernorm_bwd);
+        pybind11::arg("mean"), pybind11::arg("rstd"), pybind11::arg("delta_bias") = pybind11::none(),
+        pybind11::arg("dropout_p") = 0.0, pybind11::arg("dropout_seed") = 0);
+  m.def("layernorm_bwd", &layernorm_bwd, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("mean"),
+        pybind11::arg("rstd"), pybind11::arg("w"), pybind11::arg("dresid"), pybind11::arg("accumulate"),
+        pybind11::arg("dresid_bf"), pybind11::arg("dw"), pybind11::arg("db"), pybind11::arg("dbias_prev"),
+        pybind11::arg("dropout_p") = 0.0, pybind11::arg("dropout_seed") = 0);
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
   m.def("rmsnorm_bwd", &rmsnorm_bwd);
   m.def("rms_residual", &rms_residual);
@@ -90,8 +95,11 @@ PYBIND11_MODULE(penroz_kernels, m) {
   m.def("gated_act_bwd", &gated_act_bwd);
   m.def("transpose_bf16", &transpose_bf16, "out [C, R] = in [R, C]^T (bf16, dims % 64 == 0)");
   m.def("embedding_fwd", &embedding_fwd, pybind11::arg("idx"), pybind11::arg("wte"), pybind11::arg("wpe"),
-        pybind11::arg("off"), pybind11::arg("out"), pybind11::arg("off_dev") = pybind11::none());
-  m.def("embedding_bwd", &embedding_bwd);
+        pybind11::arg("off"), pybind11::arg("out"), pybind11::arg("off_dev") = pybind11::none(),
+        pybind11::arg("dropout_p") = 0.0, pybind11::arg("dropout_seed") = 0);
+  m.def("embedding_bwd", &embedding_bwd, pybind11::arg("dout"), pybind11::arg("idx"), pybind11::arg("dwte"),
+        pybind11::arg("dwpe"), pybind11::arg("off"), pybind11::arg("dropout_p") = 0.0,
+        pybind11::arg("dropout_seed") = 0);
   m.def("rope_qkv", &rope_qkv);
   m.def("kv_quantize", &kv_quantize);
   m.def("tensor_stats", &tensor_stats);

@@ -155,6 +155,13 @@ __device__ __forceinline__ float uniform01(uint64_t seed, uint64_t counter) {
   return (hash_u32(seed * 0x9E3779B97F4A7C15ULL + counter) >> 8) * (1.0f / 16777216.0f);
 }
 
+// Element dropout multiplier for the residual-branch / embedding dropout of the fused GPT
+// executor: 1/(1-p) when element `counter` of stream `seed` is kept, else 0. Forward and backward
+// regenerate the same mask from (seed, row·C + col) — nothing is stored.
+__device__ __forceinline__ float dropout_mult(uint64_t seed, uint64_t counter, float p, float inv_keep) {
+  return uniform01(seed, counter) >= p ? inv_keep : 0.f;
+}
+
 
 // ---- LDS-DMA (global_load_lds_dwordx4) ----------------------------------------------------
 typedef __attribute__((address_space(3))) void lds_void_t;

@@ -9,6 +9,9 @@
 // logits, so the lm_head backward GEMM reads it directly: one HBM read + one write per row,
 // no fp32 logits (the reference's autocast CE materialises fp32 log-softmax of [B·T, V]).
 // Rows with target == ignore_index contribute 0 loss and 0 gradient.
+// Any V: rows live at a row stride ld (a multiple of 8, ≥ V rounded up to 8 — the executor pads
+// the logits buffer, e.g. HF GPT-2's V = 50257 → ld 50264), so every 16-B chunk stays inside its
+// row's allocation; elements at or past V count as −∞ logits and get a zero gradient.
 #include "common.h"
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
@@ -30,11 +33,11 @@ __device__ __forceinline__ float block_reduce(float v, float* sh, bool is_max) {
 
 template <int CPT, typename T>
 __global__ void __launch_bounds__(kCEThreads) ce_kernel(T* __restrict__ logits, const int64_t* __restrict__ targets,
-                                                        float* __restrict__ loss, int V, float scale,
+                                                        float* __restrict__ loss, int V, int ld, float scale,
                                                         int64_t ignore_index) {
   __shared__ float sh[16];
   const int row = blockIdx.x;
-  T* rp = logits + (size_t)row * V;
+  T* rp = logits + (size_t)row * ld;
   const int64_t tgt = targets[row];
   PZ_DEVICE_CHECK(tgt == ignore_index || (tgt >= 0 && tgt < V));
   const int t = threadIdx.x;
@@ -45,6 +48,10 @@ __global__ void __launch_bounds__(kCEThreads) ce_kernel(T* __restrict__ logits, 
     const int c = 8 * (t + kCEThreads * k);
     if (c < V) {
       Vec8<T>::load(rp + c, v[k]);
+      if (c + 8 > V) {  // the row's last, partial chunk
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[k][j] = c + j < V ? v[k][j] : -INFINITY;
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) m = fmaxf(m, v[k][j]);
     }
@@ -78,15 +85,15 @@ __global__ void __launch_bounds__(kCEThreads) ce_kernel(T* __restrict__ logits, 
   }
 }
 
-// Any-V fallback (V % 8 == 0): three streamed passes through L2.
+// Wide-V fallback (more than 8 chunks per thread): three streamed passes through L2.
 template <typename T>
 __global__ void __launch_bounds__(kCEThreads) ce_loop_kernel(T* __restrict__ logits,
                                                              const int64_t* __restrict__ targets,
-                                                             float* __restrict__ loss, int V, float scale,
+                                                             float* __restrict__ loss, int V, int ld, float scale,
                                                              int64_t ignore_index) {
   __shared__ float sh[16];
   const int row = blockIdx.x;
-  T* rp = logits + (size_t)row * V;
+  T* rp = logits + (size_t)row * ld;
   const int64_t tgt = targets[row];
   PZ_DEVICE_CHECK(tgt == ignore_index || (tgt >= 0 && tgt < V));
   float m = -INFINITY;
@@ -94,7 +101,7 @@ __global__ void __launch_bounds__(kCEThreads) ce_loop_kernel(T* __restrict__ log
     float v[8];
     Vec8<T>::load(rp + c, v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) m = fmaxf(m, v[j]);
+    for (int j = 0; j < 8; ++j) m = fmaxf(m, c + j < V ? v[j] : -INFINITY);
   }
   m = block_reduce(m, sh, true);
   float s = 0.f;
@@ -102,7 +109,7 @@ __global__ void __launch_bounds__(kCEThreads) ce_loop_kernel(T* __restrict__ log
     float v[8];
     Vec8<T>::load(rp + c, v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s += __expf(v[j] - m);
+    for (int j = 0; j < 8; ++j) s += c + j < V ? __expf(v[j] - m) : 0.f;
   }
   s = block_reduce(s, sh, false);
   const float lse = m + __logf(s);
@@ -115,7 +122,7 @@ __global__ void __launch_bounds__(kCEThreads) ce_loop_kernel(T* __restrict__ log
     float v[8];
     Vec8<T>::load(rp + c, v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (__expf(v[j] - lse) - (c + j == tgt ? 1.f : 0.f)) * sc;
+    for (int j = 0; j < 8; ++j) v[j] = c + j < V ? (__expf(v[j] - lse) - (c + j == tgt ? 1.f : 0.f)) * sc : 0.f;
     Vec8<T>::store(rp + c, v);
   }
 }
@@ -125,15 +132,21 @@ __global__ void __launch_bounds__(kCEThreads) ce_loop_kernel(T* __restrict__ log
 using namespace penroz;
 
 torch::Tensor cross_entropy_fwd_bwd(torch::Tensor logits, torch::Tensor targets, double scale, int64_t ignore_index) {
-  TORCH_CHECK(logits.is_cuda() && logits.is_contiguous() && logits.dim() == 2);
+  TORCH_CHECK(logits.is_cuda() && logits.dim() == 2 && logits.stride(1) == 1, "logits: [N, V] with unit column stride");
   TORCH_CHECK(targets.scalar_type() == torch::kInt64 && targets.numel() == logits.size(0));
   const int N = logits.size(0), V = logits.size(1);
-  TORCH_CHECK(V % 8 == 0, "vocabulary must be a multiple of 8");
+  const int ld = N > 1 ? (int)logits.stride(0) : ((V + 7) & ~7);
+  TORCH_CHECK(ld % 8 == 0 && ld >= ((V + 7) & ~7) && reinterpret_cast<uintptr_t>(logits.data_ptr()) % 16 == 0,
+              "logits rows must start 16-B aligned with a row stride that is a multiple of 8 and >= V rounded up to "
+              "8 (pad the buffer: [N, ld][:, :V])");
+  TORCH_CHECK(N <= 1 || logits.storage().nbytes() >= (size_t)(logits.storage_offset() + (int64_t)(N - 1) * ld +
+                                                              ((V + 7) & ~7)) * logits.element_size(),
+              "logits: the last row's padding must be allocated");
   auto loss = torch::empty({N}, logits.options().dtype(torch::kFloat32));
   if (N == 0) return loss;
   auto tg = targets.contiguous();
   auto stream = at::hip::getCurrentHIPStream();
-  const int chunks = (V / 8 + kCEThreads - 1) / kCEThreads;
+  const int chunks = ((V + 7) / 8 + kCEThreads - 1) / kCEThreads;
   auto launch = [&](auto tag) {
     using T = decltype(tag);
     T* lp = reinterpret_cast<T*>(logits.data_ptr());
@@ -141,15 +154,15 @@ torch::Tensor cross_entropy_fwd_bwd(torch::Tensor logits, torch::Tensor targets,
     float* op = loss.data_ptr<float>();
     const float sc = (float)scale;
     switch (chunks) {
-      case 1: hipLaunchKernelGGL((ce_kernel<1, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, sc, ignore_index); break;
-      case 2: hipLaunchKernelGGL((ce_kernel<2, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, sc, ignore_index); break;
-      case 3: hipLaunchKernelGGL((ce_kernel<3, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, sc, ignore_index); break;
-      case 4: hipLaunchKernelGGL((ce_kernel<4, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, sc, ignore_index); break;
-      case 5: hipLaunchKernelGGL((ce_kernel<5, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, sc, ignore_index); break;
-      case 6: hipLaunchKernelGGL((ce_kernel<6, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, sc, ignore_index); break;
-      case 7: hipLaunchKernelGGL((ce_kernel<7, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, sc, ignore_index); break;
-      case 8: hipLaunchKernelGGL((ce_kernel<8, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, sc, ignore_index); break;
-      default: hipLaunchKernelGGL((ce_loop_kernel<T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, sc, ignore_index);
+      case 1: hipLaunchKernelGGL((ce_kernel<1, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index); break;
+      case 2: hipLaunchKernelGGL((ce_kernel<2, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index); break;
+      case 3: hipLaunchKernelGGL((ce_kernel<3, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index); break;
+      case 4: hipLaunchKernelGGL((ce_kernel<4, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index); break;
+      case 5: hipLaunchKernelGGL((ce_kernel<5, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index); break;
+      case 6: hipLaunchKernelGGL((ce_kernel<6, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index); break;
+      case 7: hipLaunchKernelGGL((ce_kernel<7, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index); break;
+      case 8: hipLaunchKernelGGL((ce_kernel<8, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index); break;
+      default: hipLaunchKernelGGL((ce_loop_kernel<T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index);
     }
   };
   if (logits.scalar_type() == torch::kBFloat16) launch(bf16{});

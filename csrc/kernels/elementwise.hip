@@ -144,7 +144,7 @@ template <typename TW>
 __global__ void __launch_bounds__(256) embed_fwd_kernel(const int64_t* __restrict__ idx, const TW* __restrict__ wte,
                                                         const TW* __restrict__ wpe, float* __restrict__ out, int N,
                                                         int T, int C, int off, int V, const int64_t* __restrict__ off_dev,
-                                                        int P) {
+                                                        int P, uint64_t dseed, float dp) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= N) return;
@@ -159,6 +159,11 @@ __global__ void __launch_bounds__(256) embed_fwd_kernel(const int64_t* __restric
     Vec8<TW>::load(wpe + (size_t)pos * C + c, b);
 #pragma unroll
     for (int k = 0; k < 8; ++k) a[k] += b[k];
+    if (dp > 0.f) {  // embedding dropout (HF GPT-2 embd_pdrop); the backward regenerates the mask
+      const float inv = 1.f / (1.f - dp);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) a[k] *= dropout_mult(dseed, (size_t)row * C + c + k, dp, inv);
+    }
     Vec8<float>::store(out + (size_t)row * C + c, a);
   }
 }
@@ -199,7 +204,8 @@ __global__ void __launch_bounds__(256) transpose_bf16_kernel(const uint16_t* __r
 // dwte[idx[n]] += dout[n]  (fp32 atomics; each wave instruction = 256 contiguous bytes)
 __global__ void __launch_bounds__(256) embed_bwd_tok_kernel(const float* __restrict__ dout,
                                                             const int64_t* __restrict__ idx,
-                                                            float* __restrict__ dwte, int N, int C, int V) {
+                                                            float* __restrict__ dwte, int N, int C, int V,
+                                                            uint64_t dseed, float dp) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= N) return;
@@ -208,16 +214,31 @@ __global__ void __launch_bounds__(256) embed_bwd_tok_kernel(const float* __restr
   if (tok < 0 || tok >= V) return;
   float* dst = dwte + (size_t)tok * C;
   const float* src = dout + (size_t)row * C;
-  for (int c = lane; c < C; c += 64) atomicAdd(dst + c, src[c]);
+  if (dp > 0.f) {
+    const float inv = 1.f / (1.f - dp);
+    for (int c = lane; c < C; c += 64)
+      atomicAdd(dst + c, src[c] * dropout_mult(dseed, (size_t)row * C + c, dp, inv));
+  } else {
+    for (int c = lane; c < C; c += 64) atomicAdd(dst + c, src[c]);
+  }
 }
 
 // dwpe[off + t] += Σ_b dout[b*T + t]   (one workgroup per position, no atomics)
 __global__ void __launch_bounds__(256) embed_bwd_pos_kernel(const float* __restrict__ dout, float* __restrict__ dwpe,
-                                                            int B, int T, int C, int off) {
+                                                            int B, int T, int C, int off, uint64_t dseed, float dp) {
   const int t = blockIdx.x;
+  const float inv = dp > 0.f ? 1.f / (1.f - dp) : 1.f;
   for (int c = threadIdx.x * 4; c < C; c += 1024) {
     float4_t s = {0.f, 0.f, 0.f, 0.f};
-    for (int b = 0; b < B; ++b) s += *reinterpret_cast<const float4_t*>(dout + ((size_t)b * T + t) * C + c);
+    for (int b = 0; b < B; ++b) {
+      const size_t e = ((size_t)b * T + t) * C + c;
+      float4_t g = *reinterpret_cast<const float4_t*>(dout + e);
+      if (dp > 0.f) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) g[k] *= dropout_mult(dseed, e + k, dp, inv);
+      }
+      s += g;
+    }
     float4_t* d = reinterpret_cast<float4_t*>(dwpe + (size_t)(off + t) * C + c);
     *d = *d + s;
   }
@@ -460,7 +481,8 @@ std::vector<torch::Tensor> gated_act_bwd(torch::Tensor dy, torch::Tensor g, torc
 }
 
 void embedding_fwd(torch::Tensor idx, torch::Tensor wte, torch::Tensor wpe, int64_t off, torch::Tensor out,
-                   c10::optional<torch::Tensor> off_dev) {
+                   c10::optional<torch::Tensor> off_dev, double dropout_p, int64_t dropout_seed) {
+  TORCH_CHECK(dropout_p >= 0.0 && dropout_p < 1.0, "dropout p must be in [0, 1)");
   TORCH_CHECK(idx.is_cuda() && idx.scalar_type() == torch::kInt64 && idx.dim() == 2);
   const int B = idx.size(0), T = idx.size(1), C = wte.size(1), V = wte.size(0);
   TORCH_CHECK(C % 8 == 0 && wpe.size(1) == C && wte.scalar_type() == wpe.scalar_type());
@@ -478,7 +500,8 @@ void embedding_fwd(torch::Tensor idx, torch::Tensor wte, torch::Tensor wpe, int6
   FOR_FLOAT_TYPES(wte.scalar_type(), TW,
     hipLaunchKernelGGL(embed_fwd_kernel<TW>, dim3((N + 3) / 4), dim3(256), 0, stream, idxc.data_ptr<int64_t>(),
                        reinterpret_cast<const TW*>(wte.data_ptr()), reinterpret_cast<const TW*>(wpe.data_ptr()),
-                       out.data_ptr<float>(), N, T, C, (int)off, V, od, (int)wpe.size(0)))
+                       out.data_ptr<float>(), N, T, C, (int)off, V, od, (int)wpe.size(0), (uint64_t)dropout_seed,
+                       (float)dropout_p))
 }
 
 void transpose_bf16(torch::Tensor in, torch::Tensor out) {
@@ -494,7 +517,9 @@ void transpose_bf16(torch::Tensor in, torch::Tensor out) {
                      reinterpret_cast<const uint16_t*>(in.data_ptr()), reinterpret_cast<uint16_t*>(out.data_ptr()), R, C);
 }
 
-void embedding_bwd(torch::Tensor dout, torch::Tensor idx, torch::Tensor dwte, torch::Tensor dwpe, int64_t off) {
+void embedding_bwd(torch::Tensor dout, torch::Tensor idx, torch::Tensor dwte, torch::Tensor dwpe, int64_t off,
+                   double dropout_p, int64_t dropout_seed) {
+  TORCH_CHECK(dropout_p >= 0.0 && dropout_p < 1.0, "dropout p must be in [0, 1)");
   const int B = idx.size(0), T = idx.size(1), C = dwte.size(1), V = dwte.size(0);
   TORCH_CHECK(dout.scalar_type() == torch::kFloat32 && dwte.scalar_type() == torch::kFloat32 &&
               dwpe.scalar_type() == torch::kFloat32 && C % 4 == 0);
@@ -503,9 +528,10 @@ void embedding_bwd(torch::Tensor dout, torch::Tensor idx, torch::Tensor dwte, to
   const int N = B * T;
   auto stream = at::hip::getCurrentHIPStream();
   hipLaunchKernelGGL(embed_bwd_tok_kernel, dim3((N + 3) / 4), dim3(256), 0, stream, dout.data_ptr<float>(),
-                     idxc.data_ptr<int64_t>(), dwte.data_ptr<float>(), N, C, V);
+                     idxc.data_ptr<int64_t>(), dwte.data_ptr<float>(), N, C, V, (uint64_t)dropout_seed,
+                     (float)dropout_p);
   hipLaunchKernelGGL(embed_bwd_pos_kernel, dim3(T), dim3(256), 0, stream, dout.data_ptr<float>(), dwpe.data_ptr<float>(),
-                     B, T, C, (int)off);
+                     B, T, C, (int)off, (uint64_t)dropout_seed, (float)dropout_p);
 }
 
 torch::Tensor rope_qkv(torch::Tensor qkv, torch::Tensor cosv, torch::Tensor sinv, int64_t H, int64_t Hkv, int64_t D,

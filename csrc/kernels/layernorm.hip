@@ -12,6 +12,11 @@
 // per-column partial sums dγ = Σ dy·x̂, dβ = Σ dy and (optionally) Σ dresid — the bias
 // gradient of the linear that fed this residual — are reduced per workgroup in LDS and
 // finished by a small column-reduction kernel (deterministic, no atomics).
+//
+// Residual dropout (HF GPT-2 resid_pdrop): the fused forward adds drop(delta) =
+// delta·mask/(1-p) to the stream; the backward keeps the fp32 residual gradient unmasked and
+// applies the regenerated mask to the branch gradient it hands on (the bf16 copy for the
+// producing linear's dgrad and that linear's bias-gradient column sum).
 #include "common.h"
 #include "deferred.h"
 #include <torch/extension.h>
@@ -67,11 +72,12 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const TX* __restrict__ x, c
                                                      float* __restrict__ resid_out, const float* __restrict__ w,
                                                      const float* __restrict__ b, TY* __restrict__ y,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                     int N, int C, float eps) {
+                                                     int N, int C, float eps, uint64_t dseed, float dp) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
   if (row >= N) return;
   const size_t base = (size_t)row * C;
+  const float dinv = dp > 0.f ? 1.f / (1.f - dp) : 1.f;
   float v[NCH][4];
   float s = 0.f;
 #pragma unroll
@@ -87,6 +93,10 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const TX* __restrict__ x, c
         V4<float>::ld(dbias + c, e);
 #pragma unroll
         for (int k = 0; k < 4; ++k) d[k] += e[k];
+      }
+      if (dp > 0.f) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d[k] *= dropout_mult(dseed, base + c + k, dp, dinv);
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) v[j][k] += d[k];
@@ -127,11 +137,12 @@ __global__ void __launch_bounds__(256) ln_fwd_loop_kernel(const TX* __restrict__
                                                           float* __restrict__ resid_out, const float* __restrict__ w,
                                                           const float* __restrict__ b, TY* __restrict__ y,
                                                           float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                          int N, int C, float eps) {
+                                                          int N, int C, float eps, uint64_t dseed, float dp) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
   if (row >= N) return;
   const size_t base = (size_t)row * C;
+  const float dinv = dp > 0.f ? 1.f / (1.f - dp) : 1.f;
   float s = 0.f;
   for (int c = 4 * lane; c < C; c += 256) {
     float v[4];
@@ -144,6 +155,10 @@ __global__ void __launch_bounds__(256) ln_fwd_loop_kernel(const TX* __restrict__
         V4<float>::ld(dbias + c, e);
 #pragma unroll
         for (int k = 0; k < 4; ++k) d[k] += e[k];
+      }
+      if (dp > 0.f) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d[k] *= dropout_mult(dseed, base + c + k, dp, dinv);
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) v[k] += d[k];
@@ -183,7 +198,9 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const TDY* __restrict__ dy,
                                                      const float* __restrict__ rstd_in,
                                                      const float* __restrict__ w, float* __restrict__ dresid,
                                                      bf16* __restrict__ dresid_bf, float* __restrict__ part,
-                                                     int N, int C, int accumulate, int want_bias) {
+                                                     int N, int C, int accumulate, int want_bias, uint64_t dseed,
+                                                     float dp) {
+  const float dinv = dp > 0.f ? 1.f / (1.f - dp) : 1.f;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -232,11 +249,14 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const TDY* __restrict__ dy,
       if (accumulate) V4<float>::ld(dresid + base + c, r);
       else r[0] = r[1] = r[2] = r[3] = 0.f;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        r[k] += (g[j][k] * wv[j][k] - c1 - xh[j][k] * c2) * rstd;
-        pz[j][k] += r[k];
-      }
+      for (int k = 0; k < 4; ++k) r[k] += (g[j][k] * wv[j][k] - c1 - xh[j][k] * c2) * rstd;
       V4<float>::st(dresid + base + c, r);
+      if (dp > 0.f) {  // branch gradient = mask ⊙ residual gradient / (1-p)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) r[k] *= dropout_mult(dseed, base + c + k, dp, dinv);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) pz[j][k] += r[k];
       if (dresid_bf != nullptr) V4<bf16>::st(dresid_bf + base + c, r);
     }
   }
@@ -295,7 +315,8 @@ static bool nch_ok(int C) { return nch_pick(C) != 0; }
 template <typename TX, typename TD, typename TY, bool ADD>
 static void launch_fwd(const torch::Tensor& x, const torch::Tensor* delta, torch::Tensor* resid_out,
                        const torch::Tensor& w, const torch::Tensor& b, torch::Tensor& y, torch::Tensor& mean,
-                       torch::Tensor& rstd, double eps, const float* dbias = nullptr) {
+                       torch::Tensor& rstd, double eps, const float* dbias = nullptr, uint64_t dseed = 0,
+                       float drop_p = 0.f) {
   const int N = x.size(0), C = x.size(1);
   if (N == 0) return;
   dim3 grid((N + kRowsPerBlock - 1) / kRowsPerBlock), block(256);
@@ -307,10 +328,11 @@ static void launch_fwd(const torch::Tensor& x, const torch::Tensor* delta, torch
   if (nch_ok(C)) {
     DISPATCH_NCH(C, hipLaunchKernelGGL((ln_fwd_kernel<NCH, TX, TD, TY, ADD>), grid, block, 0, stream, xp, dp, dbias, rp,
                                        w.data_ptr<float>(), b.data_ptr<float>(), yp, mean.data_ptr<float>(),
-                                       rstd.data_ptr<float>(), N, C, (float)eps));
+                                       rstd.data_ptr<float>(), N, C, (float)eps, dseed, drop_p));
   } else {
     hipLaunchKernelGGL((ln_fwd_loop_kernel<TX, TD, TY, ADD>), grid, block, 0, stream, xp, dp, dbias, rp, w.data_ptr<float>(),
-                       b.data_ptr<float>(), yp, mean.data_ptr<float>(), rstd.data_ptr<float>(), N, C, (float)eps);
+                       b.data_ptr<float>(), yp, mean.data_ptr<float>(), rstd.data_ptr<float>(), N, C, (float)eps,
+                       dseed, drop_p);
   }
 }
 
@@ -339,7 +361,8 @@ void layernorm_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor b, double eps
 
 void add_layernorm_fwd(torch::Tensor resid_in, torch::Tensor delta, torch::Tensor resid_out, torch::Tensor w,
                        torch::Tensor b, double eps, torch::Tensor y, torch::Tensor mean, torch::Tensor rstd,
-                       c10::optional<torch::Tensor> delta_bias) {
+                       c10::optional<torch::Tensor> delta_bias, double dropout_p, int64_t dropout_seed) {
+  TORCH_CHECK(dropout_p >= 0.0 && dropout_p < 1.0, "dropout p must be in [0, 1)");
   const int64_t N = resid_in.size(0), C = resid_in.size(1);
   check_rows(resid_in, N, C, "resid_in");
   check_rows(delta, N, C, "delta");
@@ -356,12 +379,15 @@ void add_layernorm_fwd(torch::Tensor resid_in, torch::Tensor delta, torch::Tenso
   FOR_FLOAT_TYPES(resid_in.scalar_type(), TX,
     FOR_FLOAT_TYPES(delta.scalar_type(), TD,
       FOR_FLOAT_TYPES(y.scalar_type(), TY,
-        launch_fwd<TX, TD, TY, true>(resid_in, &delta, &resid_out, w, b, y, mean, rstd, eps, dbp))))
+        launch_fwd<TX, TD, TY, true>(resid_in, &delta, &resid_out, w, b, y, mean, rstd, eps, dbp,
+                                     (uint64_t)dropout_seed, (float)dropout_p))))
 }
 
 void layernorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor mean, torch::Tensor rstd, torch::Tensor w,
                    torch::Tensor dresid, bool accumulate, c10::optional<torch::Tensor> dresid_bf,
-                   torch::Tensor dw, torch::Tensor db, c10::optional<torch::Tensor> dbias_prev) {
+                   torch::Tensor dw, torch::Tensor db, c10::optional<torch::Tensor> dbias_prev, double dropout_p,
+                   int64_t dropout_seed) {
+  TORCH_CHECK(dropout_p >= 0.0 && dropout_p < 1.0, "dropout p must be in [0, 1)");
   const int64_t N = x.size(0), C = x.size(1);
   check_rows(dy, N, C, "dy");
   check_rows(x, N, C, "x");
@@ -388,7 +414,7 @@ void layernorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor mean, torch:
                                          reinterpret_cast<const TX*>(x.data_ptr()), mean.data_ptr<float>(),
                                          rstd.data_ptr<float>(), w.data_ptr<float>(), dresid.data_ptr<float>(), dbf,
                                          part.data_ptr<float>(), (int)N, (int)C, accumulate ? 1 : 0,
-                                         want_bias ? 1 : 0))))
+                                         want_bias ? 1 : 0, (uint64_t)dropout_seed, (float)dropout_p))))
   const int A = want_bias ? 3 : 2;
   float* outs[3] = {dw.data_ptr<float>(), db.data_ptr<float>(), want_bias ? dbias_prev->data_ptr<float>() : nullptr};
   reduce_partials_auto(part, A, grid, (int)C, outs, stream);

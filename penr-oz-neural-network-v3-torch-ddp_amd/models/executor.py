@@ -16,6 +16,17 @@ backward mirrors it: dgrad/wgrad GEMMs (wgrad accumulated in fp32), GELU backwar
   accumulation, its bf16 copy for the next GEMM, and the bias gradient of the preceding
   linear; flash-attention backward; embedding backward (dwte scatter, dwpe reduction).
 
+Dropout (the HF GPT-2 import: embd/resid/attn_pdrop = 0.1, ``mappers.py:140-142`` in the
+reference): attention dropout runs inside the flash kernels; embedding dropout inside the
+embedding kernels; each residual branch's dropout inside the add+LayerNorm kernel that adds it
+to the stream, and the LayerNorm backward applies the regenerated mask to the branch gradient.
+Masks are hashed from (step seed, site, element) and never stored.
+
+bf16-parameter models (``/import/`` loads HF weights in bf16, ``neural_net_model.py:222``) train
+here too: the executor keeps fp32 master copies and makes the module parameters views of the
+bf16 shadow the fused AdamW rewrites every step, so ``state_dict()`` stays bf16 (the checkpoint
+dtype of the reference) while the update itself is fp32.
+
 Parameters, gradients and AdamW moments live in flat fp32 buffers laid out in backward
 completion order (lm_head … wte) so gradient buckets are contiguous slices: the reducer
 launches each bucket's RCCL all-reduce as soon as the layers in it finish, overlapped with
@@ -54,6 +65,8 @@ class _Block:
     fc: nn.Linear
     act: nn.GELU
     fc2: nn.Linear
+    p_attn_res: float = 0.0  # dropout on the attention branch (after proj)
+    p_mlp_res: float = 0.0   # dropout on the MLP branch (after fc2)
 
 
 @dataclass
@@ -70,22 +83,29 @@ class GPTSpec:
     lnf: nn.LayerNorm = None
     head: nn.Linear = None
     gelu_approx: str = "none"
+    p_embd: float = 0.0
+    param_dtype: torch.dtype = torch.float32
 
 
 def _is(m, cls):
     return isinstance(m, cls)
 
 
-def _dropout_zero(m) -> bool:
-    return _is(m, nn.Dropout) and m.p == 0.0
+def _dropout_ok(m) -> bool:
+    return _is(m, nn.Dropout) and 0.0 <= m.p < 1.0
+
+
+# residual-dropout mask streams: one per (step seed, site); attention dropout uses seed + layer
+def _site_seed(seed: int, site: int) -> int:
+    return (seed * 1_000_003 + 7_919 * (site + 1) + 0x5BD1E995) & 0x7FFFFFFFFFFFFFFF
 
 
 class GPTExecutor:
     # ------------------------------------------------------------------ pattern match
     @staticmethod
-    def match(model, require_fp32: bool = True) -> GPTSpec | None:
-        """The GPT-2 block structure (``require_fp32``: the training executor's fp32 masters;
-        the decode program of ``graph_decode.py`` also takes bf16 models)."""
+    def match(model, require_fp32: bool = False) -> GPTSpec | None:
+        """The GPT-2 block structure, with fp32 or bf16 parameters (one dtype for all; the
+        executor keeps fp32 masters either way). ``require_fp32``: fp32 parameters only."""
         ls = list(model.layers)
         if len(ls) < 5:
             return None
@@ -93,7 +113,7 @@ class GPTExecutor:
         if not (_is(emb, L.Summation) and len(emb) == 2 and type(emb[0]) is nn.Embedding
                 and _is(emb[1], L.PositionEmbedding)):
             return None
-        if not _dropout_zero(ls[1]):
+        if not _dropout_ok(ls[1]):
             return None
         tail = ls[-3:] if _is(ls[-1], L.SoftmaxOnLast) else ls[-2:]
         if len(tail) < 2 or not _is(tail[0], nn.LayerNorm) or not _is(tail[1], nn.Linear) or tail[1].bias is not None:
@@ -114,11 +134,11 @@ class GPTExecutor:
             ln1, qkv, att, proj, d1 = a
             ln2, fc, act, fc2, d2 = m
             ok = (_is(ln1, nn.LayerNorm) and _is(qkv, nn.Linear) and _is(att, L.CausalSelfAttention)
-                  and _is(proj, nn.Linear) and _dropout_zero(d1) and _is(ln2, nn.LayerNorm)
-                  and _is(fc, nn.Linear) and _is(act, nn.GELU) and _is(fc2, nn.Linear) and _dropout_zero(d2))
+                  and _is(proj, nn.Linear) and _dropout_ok(d1) and _is(ln2, nn.LayerNorm)
+                  and _is(fc, nn.Linear) and _is(act, nn.GELU) and _is(fc2, nn.Linear) and _dropout_ok(d2))
             if not ok:
                 return None
-            if att.rope_theta is not None or att.num_kv_heads != att.num_heads:
+            if att.rope_theta is not None or att.num_kv_heads != att.num_heads or not 0.0 <= att.dropout < 1.0:
                 return None
             H = att.num_heads
             D = C // H
@@ -134,13 +154,16 @@ class GPTExecutor:
             if act.approximate != approx:
                 return None
             spec.H, spec.D, spec.F = H, D, fc.out_features
-            spec.blocks.append(_Block(ln1, qkv, att, proj, ln2, fc, act, fc2))
+            spec.blocks.append(_Block(ln1, qkv, att, proj, ln2, fc, act, fc2, float(d1.p), float(d2.p)))
         if spec.D not in attn_ops.SUPPORTED_HEAD_DIMS or C % 64 != 0 or spec.F % 64 != 0:
             return None
         if tuple(spec.lnf.normalized_shape) != (C,) or spec.head.in_features != C:
             return None
-        if require_fp32 and any(p.dtype != torch.float32 for p in model.parameters()):
+        dtypes = {p.dtype for p in model.parameters()}
+        if len(dtypes) != 1 or not dtypes <= ({torch.float32} if require_fp32 else {torch.float32, torch.bfloat16}):
             return None
+        spec.param_dtype = dtypes.pop()
+        spec.p_embd = float(ls[1].p)
         spec.gelu_approx = approx
         return spec
 
@@ -186,14 +209,20 @@ class GPTExecutor:
         self.shadow = torch.empty(total, dtype=torch.bfloat16, device=dev)
         self.offsets = {}
         self.segments = []
+        bf16_params = self.spec.param_dtype == torch.bfloat16
         off = 0
         for seg in segs:
             start = off
             for p in seg:
                 n = p.numel()
                 self.flat[off:off + n].copy_(p.data.reshape(-1))
-                p.data = self.flat[off:off + n].view_as(p)
-                p.grad = self.flat_grad[off:off + n].view_as(p)
+                if bf16_params:
+                    # the module sees the bf16 shadow (rewritten by every optimizer step); the
+                    # fp32 masters and gradients stay internal (grad(p) / f32(p))
+                    p.data = self.shadow[off:off + n].view_as(p)
+                else:
+                    p.data = self.flat[off:off + n].view_as(p)
+                    p.grad = self.flat_grad[off:off + n].view_as(p)
                 self.offsets[id(p)] = off
                 off += n
             self.segments.append((start, off))
@@ -265,6 +294,11 @@ class GPTExecutor:
         off = self.offsets[id(p)]
         return self.flat_grad[off:off + p.numel()].view(p.shape)
 
+    def f32(self, p: Tensor) -> Tensor:
+        """The fp32 master of ``p`` (``p`` itself for fp32 models)."""
+        off = self.offsets[id(p)]
+        return self.flat[off:off + p.numel()].view(p.shape)
+
     # ------------------------------------------------------------------ buffers
     def _alloc(self, B: int, T: int):
         if self._acts_shape == (B, T):
@@ -284,7 +318,10 @@ class GPTExecutor:
         self.fcpre = [torch.empty(N, F, dtype=bf, device=dev) for _ in range(self.L)]
         self.fcact = [torch.empty(N, F, dtype=bf, device=dev) for _ in range(self.L)]
         self.lnf_out = torch.empty(N, C, dtype=bf, device=dev)
-        self.logits = torch.empty(N, V, dtype=bf, device=dev)
+        # rows padded to a multiple of 8 elements (16 B): the GEMMs take the row stride, the CE
+        # kernel's 16-B chunks stay inside the row (HF GPT-2: V = 50257 -> stride 50264)
+        self._logits_buf = torch.empty(N, (V + 7) // 8 * 8, dtype=bf, device=dev)
+        self.logits = self._logits_buf[:, :V]
         self.tmp_c = torch.empty(N, C, dtype=bf, device=dev)
         self.dresid = torch.empty(N, C, dtype=f32, device=dev)
         # gradient buffers read by the side-stream weight-gradient GEMMs rotate between two
@@ -296,7 +333,7 @@ class GPTExecutor:
         self._acts_shape = (B, T)
 
     def free_buffers(self):
-        for name in ("resid", "resid_mid", "ln1", "ln2", "qkv", "fcpre", "fcact", "lnf_out", "logits", "tmp_c",
+        for name in ("resid", "resid_mid", "ln1", "ln2", "qkv", "fcpre", "fcact", "lnf_out", "logits", "_logits_buf", "tmp_c",
                      "dresid", "dresid_bf2", "d_f2", "d_c", "dqkv2", "att", "lse", "stats", "statsf"):
             if hasattr(self, name):
                 delattr(self, name)
@@ -310,6 +347,12 @@ class GPTExecutor:
                 torch.addmm(self.bf16(lin.bias), x, w.t())
         return torch.mm(x, w.t(), out=out) if out is not None else torch.mm(x, w.t())
 
+    def _drop(self, training: bool, seed: int, l: int, branch: int) -> tuple[float, int]:
+        """(p, mask seed) of residual-dropout site (layer l, branch 0 = attention / 1 = MLP)."""
+        b = self.spec.blocks[l]
+        p = (b.p_attn_res if branch == 0 else b.p_mlp_res) if training else 0.0
+        return p, _site_seed(seed, 2 * l + branch)
+
     def _forward(self, idx: Tensor, training: bool, dropout_seed: int = 0):
         s = self.spec
         B, T = idx.shape
@@ -317,29 +360,36 @@ class GPTExecutor:
             raise ValueError(f"sequence length {T} exceeds the position table {s.P}")
         self._alloc(B, T)
         H, D, C = s.H, s.D, s.C
-        fused_ops.embedding_fwd(idx, s.wte.weight, s.wpe.weight, s.wpe.position_offset, out=self.resid[0])
+        f = self.f32
+        fused_ops.embedding_fwd(idx, f(s.wte.weight), f(s.wpe.weight), s.wpe.position_offset, out=self.resid[0],
+                                dropout_p=s.p_embd if training else 0.0,
+                                dropout_seed=_site_seed(dropout_seed, -1))
         for l, b in enumerate(s.blocks):
             mean1, rstd1, mean2, rstd2 = self.stats[l]
             if l == 0:
-                norm_ops.ln_fwd(self.resid[0], b.ln1.weight, b.ln1.bias, b.ln1.eps, y=self.ln1[0],
+                norm_ops.ln_fwd(self.resid[0], f(b.ln1.weight), f(b.ln1.bias), b.ln1.eps, y=self.ln1[0],
                                 mean=mean1, rstd=rstd1)
-            else:  # resid[l] = resid_mid[l-1] + fc2(l-1), LN1(l) in the same pass
-                norm_ops.add_ln_fwd(self.resid_mid[l - 1], self.tmp_c, self.resid[l], b.ln1.weight, b.ln1.bias,
-                                    b.ln1.eps, y=self.ln1[l], mean=mean1, rstd=rstd1)
+            else:  # resid[l] = resid_mid[l-1] + drop(fc2(l-1)), LN1(l) in the same pass
+                dp, ds = self._drop(training, dropout_seed, l - 1, 1)
+                norm_ops.add_ln_fwd(self.resid_mid[l - 1], self.tmp_c, self.resid[l], f(b.ln1.weight),
+                                    f(b.ln1.bias), b.ln1.eps, y=self.ln1[l], mean=mean1, rstd=rstd1,
+                                    dropout_p=dp, dropout_seed=ds)
             self._linear(self.ln1[l], b.qkv, out=self.qkv[l])
             p = b.attn.dropout if training else 0.0
             attn_ops.flash_fwd(self.qkv[l].view(B, T, 3 * C), H, H, D, p, dropout_seed + l,
                                out=self.att[l].view(B, T, C), lse=self.lse[l])
             self._linear(self.att[l], b.proj, out=self.tmp_c)
-            norm_ops.add_ln_fwd(self.resid[l], self.tmp_c, self.resid_mid[l], b.ln2.weight, b.ln2.bias, b.ln2.eps,
-                                y=self.ln2[l], mean=mean2, rstd=rstd2)
+            dp, ds = self._drop(training, dropout_seed, l, 0)
+            norm_ops.add_ln_fwd(self.resid[l], self.tmp_c, self.resid_mid[l], f(b.ln2.weight), f(b.ln2.bias),
+                                b.ln2.eps, y=self.ln2[l], mean=mean2, rstd=rstd2, dropout_p=dp, dropout_seed=ds)
             self._linear(self.ln2[l], b.fc, out=self.fcpre[l])
             act_ops.gelu_fwd(self.fcpre[l], s.gelu_approx, out=self.fcact[l])
             self._linear(self.fcact[l], b.fc2, out=self.tmp_c)
         Lc = self.L
         meanf, rstdf = self.statsf
-        norm_ops.add_ln_fwd(self.resid_mid[Lc - 1], self.tmp_c, self.resid[Lc], s.lnf.weight, s.lnf.bias, s.lnf.eps,
-                            y=self.lnf_out, mean=meanf, rstd=rstdf)
+        dp, ds = self._drop(training, dropout_seed, Lc - 1, 1)
+        norm_ops.add_ln_fwd(self.resid_mid[Lc - 1], self.tmp_c, self.resid[Lc], f(s.lnf.weight), f(s.lnf.bias),
+                            s.lnf.eps, y=self.lnf_out, mean=meanf, rstd=rstdf, dropout_p=dp, dropout_seed=ds)
         torch.mm(self.lnf_out, self.bf16(s.head.weight).t(), out=self.logits)
 
     # ------------------------------------------------------------------ public API
@@ -494,9 +544,10 @@ class GPTExecutor:
         mean, rstd = self.statsf
         last = s.blocks[-1]
         rb = 0  # rotating dresid_bf buffer index
-        norm_ops.ln_bwd(self.d_c, self.resid[self.L], mean, rstd, s.lnf.weight, self.dresid, False,
+        dp, ds = self._drop(True, seed, self.L - 1, 1)
+        norm_ops.ln_bwd(self.d_c, self.resid[self.L], mean, rstd, self.f32(s.lnf.weight), self.dresid, False,
                         self._reuse(self.dresid_bf2[rb]), self.grad(s.lnf.weight), self.grad(s.lnf.bias),
-                        self.grad(last.fc2.bias))
+                        self.grad(last.fc2.bias), dropout_p=dp, dropout_seed=ds)
         grads_cap = []
         if cap:
             grads_cap = [self.logits.view(B, T, -1).clone(), self.d_c.view(B, T, C).float().clone(),
@@ -518,8 +569,10 @@ class GPTExecutor:
             _, _, mean, rstd = self.stats[l]
             rb ^= 1
             dres_bf = self._reuse(self.dresid_bf2[rb])
-            norm_ops.ln_bwd(self.d_c, self.resid_mid[l], mean, rstd, b.ln2.weight, self.dresid, True,
-                            dres_bf, self.grad(b.ln2.weight), self.grad(b.ln2.bias), self.grad(b.proj.bias))
+            dp, ds = self._drop(True, seed, l, 0)
+            norm_ops.ln_bwd(self.d_c, self.resid_mid[l], mean, rstd, self.f32(b.ln2.weight), self.dresid, True,
+                            dres_bf, self.grad(b.ln2.weight), self.grad(b.ln2.bias), self.grad(b.proj.bias),
+                            dropout_p=dp, dropout_seed=ds)
             # ---- attention branch
             torch.mm(dres_bf, self._dgrad_w(b.proj.weight), out=self.d_c)
             self._wgrad(dres_bf, self.att[l], b.proj.weight)
@@ -531,15 +584,16 @@ class GPTExecutor:
             mean, rstd, _, _ = self.stats[l]
             prev_bias = self.grad(s.blocks[l - 1].fc2.bias) if l > 0 else None
             rb ^= 1
-            norm_ops.ln_bwd(self.d_c, self.resid[l], mean, rstd, b.ln1.weight, self.dresid, True,
+            dp, ds = self._drop(True, seed, l - 1, 1) if l > 0 else (0.0, 0)
+            norm_ops.ln_bwd(self.d_c, self.resid[l], mean, rstd, self.f32(b.ln1.weight), self.dresid, True,
                             self._reuse(self.dresid_bf2[rb]) if l > 0 else None, self.grad(b.ln1.weight),
-                            self.grad(b.ln1.bias), prev_bias)
+                            self.grad(b.ln1.bias), prev_bias, dropout_p=dp, dropout_seed=ds)
             if cap:
                 grads_cap.append(self.dresid.view(B, T, C).clone())
             self._segment_done(self.L - l, sync)
             layer_range.__exit__(None, None, None)
         fused_ops.embedding_bwd(self.dresid, idx, self.grad(s.wte.weight), self.grad(s.wpe.weight),
-                                s.wpe.position_offset)
+                                s.wpe.position_offset, dropout_p=s.p_embd, dropout_seed=_site_seed(seed, -1))
         self._segment_done(self.L + 1, sync)
         self._defer_reductions(False)
         self._join_side()

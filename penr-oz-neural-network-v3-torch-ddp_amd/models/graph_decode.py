@@ -144,7 +144,7 @@ class GPTDecodeProgram:
         if not DECODE_PROGRAM:
             return None
         from penroz.models.executor import GPTExecutor
-        spec = GPTExecutor.match(model, require_fp32=False)
+        spec = GPTExecutor.match(model)
         if spec is None or any(p.dtype != torch.bfloat16 for p in model.parameters()):
             return None
         return GPTDecodeProgram(model, spec)

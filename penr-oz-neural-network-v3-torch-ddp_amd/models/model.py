@@ -624,20 +624,20 @@ class NeuralNetworkModel(nn.Module):
                 log.info(f"Model {self.model_id}: Training Epoch {epoch + 1}, Cost: {progress_cost:.4f}, "
                          f"Duration: {secs:.2f} secs, Speed: {buffer_size / secs:.2f} tokens/sec")
             if ddp.master_proc() and long_training:
-                self._record_training_overall_progress(runner.captured())
+                self._record_training_overall_progress(runner.captured(), runner.grad_of)
                 self.serialize()
                 last_serialized = time.time()
 
         if ddp.master_proc():
             self.status = _status("Trained", f"Model trained for {epochs} epochs.")
             log.info(f"Model {self.model_id}: Done training for {epochs} epochs.")
-            self._record_training_overall_progress(runner.captured())
+            self._record_training_overall_progress(runner.captured(), runner.grad_of)
             self.serialize()
         runner.close()
         ckpt.wait_flushes()  # the disk copy is complete when training returns
 
     @torch.no_grad()
-    def _record_training_overall_progress(self, captured):
+    def _record_training_overall_progress(self, captured, grad_of=None):
         costs = [p["cost"] for p in self.progress]
         avg_progress_cost = sum(costs) / len(costs) if costs else 0.0
         self.avg_cost = ((self.avg_cost or avg_progress_cost) + avg_progress_cost) / 2.0
@@ -645,7 +645,7 @@ class NeuralNetworkModel(nn.Module):
         if len(self.avg_cost_history) > 100:
             self.avg_cost_history.pop(random.randint(1, 98))
         algos, acts = captured
-        self.stats = diagnostics.training_stats(algos, acts, self._weights)
+        self.stats = diagnostics.training_stats(algos, acts, self._weights, grad_of)
         log.info(f"Model {self.model_id} - Cost: {avg_progress_cost:.4f} Overall Cost: {self.avg_cost:.4f}")
 
 
@@ -709,6 +709,10 @@ class _GenericRunner:
     def step(self):
         self.model.optimizer.step()
 
+    @staticmethod
+    def grad_of(p):
+        return p.grad
+
     def captured(self):
         return self._algos, [(a, a.grad) for a in self._acts]
 
@@ -731,6 +735,9 @@ class _FusedRunner:
 
     def step(self):
         self.exec.optimizer_step()
+
+    def grad_of(self, p):
+        return self.exec.grad(p)
 
     def captured(self):
         return self.exec.captured()

@@ -32,18 +32,21 @@ def reference_embedding_fwd(idx: Tensor, wte: Tensor, wpe: Tensor, pos_offset: i
 
 
 def embedding_fwd(idx: Tensor, wte: Tensor, wpe: Tensor, pos_offset: int = 0, out: Tensor | None = None,
-                  pos_dev: Tensor | None = None) -> Tensor:
-    """idx [B,T] int64 -> fp32 [B*T, C] = wte[idx] + wpe[offset + t]; ``pos_dev`` (device int64
-    [1]) supplies the offset at run time instead (graph-replayed decode; clamped to the table)."""
+                  pos_dev: Tensor | None = None, dropout_p: float = 0.0, dropout_seed: int = 0) -> Tensor:
+    """idx [B,T] int64 -> fp32 [B*T, C] = drop(wte[idx] + wpe[offset + t]); ``pos_dev`` (device
+    int64 [1]) supplies the offset at run time instead (graph-replayed decode; clamped to the
+    table). ``dropout_p``: inverted dropout, mask hashed from (``dropout_seed``, element index)."""
     B, T = idx.shape
     out = torch.empty(B * T, wte.shape[1], dtype=torch.float32, device=idx.device) if out is None else out
-    kernels().embedding_fwd(idx, wte, wpe, int(pos_offset), out, pos_dev)
+    kernels().embedding_fwd(idx, wte, wpe, int(pos_offset), out, pos_dev, float(dropout_p), int(dropout_seed))
     return out
 
 
-def embedding_bwd(dout: Tensor, idx: Tensor, dwte: Tensor, dwpe: Tensor, pos_offset: int = 0):
-    """Accumulate (+=) into fp32 dwte [V, C] and dwpe [P, C] from dout fp32 [B*T, C]."""
-    kernels().embedding_bwd(dout, idx, dwte, dwpe, int(pos_offset))
+def embedding_bwd(dout: Tensor, idx: Tensor, dwte: Tensor, dwpe: Tensor, pos_offset: int = 0,
+                  dropout_p: float = 0.0, dropout_seed: int = 0):
+    """Accumulate (+=) into fp32 dwte [V, C] and dwpe [P, C] from dout fp32 [B*T, C] (times the
+    forward's regenerated dropout mask when ``dropout_p`` > 0)."""
+    kernels().embedding_bwd(dout, idx, dwte, dwpe, int(pos_offset), float(dropout_p), int(dropout_seed))
 
 
 # --------------------------------------------------------------------------- cross entropy

@@ -60,27 +60,32 @@ def ln_fwd(x2d: Tensor, w: Tensor, b: Tensor, eps: float, out_dtype=torch.bfloat
 
 def add_ln_fwd(resid_in: Tensor, delta: Tensor, resid_out: Tensor, w: Tensor, b: Tensor, eps: float,
                y: Tensor | None = None, mean: Tensor | None = None, rstd: Tensor | None = None,
-               delta_bias: Tensor | None = None):
-    """``resid_out = resid_in + delta (+ delta_bias)`` (fp32 stream, bf16 delta, fp32 bias [C])
-    and LayerNorm(resid_out) -> bf16 y."""
+               delta_bias: Tensor | None = None, dropout_p: float = 0.0, dropout_seed: int = 0):
+    """``resid_out = resid_in + drop(delta (+ delta_bias))`` (fp32 stream, bf16 delta, fp32 bias
+    [C]) and LayerNorm(resid_out) -> bf16 y. ``drop`` = inverted dropout with a mask hashed from
+    (``dropout_seed``, element index); ``ln_bwd`` regenerates it."""
     N, C = resid_in.shape
     y = torch.empty(N, C, dtype=torch.bfloat16, device=resid_in.device) if y is None else y
     mean = torch.empty(N, dtype=torch.float32, device=resid_in.device) if mean is None else mean
     rstd = torch.empty(N, dtype=torch.float32, device=resid_in.device) if rstd is None else rstd
-    kernels().add_layernorm_fwd(resid_in, delta, resid_out, w, b, float(eps), y, mean, rstd, delta_bias)
+    kernels().add_layernorm_fwd(resid_in, delta, resid_out, w, b, float(eps), y, mean, rstd, delta_bias,
+                                float(dropout_p), int(dropout_seed))
     return y, mean, rstd
 
 
 def ln_bwd(dy: Tensor, x: Tensor, mean: Tensor, rstd: Tensor, w: Tensor, dresid: Tensor,
            accumulate: bool, dresid_bf16: Tensor | None, dw: Tensor, db: Tensor,
-           dbias_prev: Tensor | None):
+           dbias_prev: Tensor | None, dropout_p: float = 0.0, dropout_seed: int = 0):
     """Fused LayerNorm backward.
 
     ``dresid (+)= dx``; optionally writes ``dresid_bf16`` (the next dgrad GEMM's operand);
     ``dw += Σ dy·x̂``, ``db += Σ dy``; optionally ``dbias_prev += Σ_rows dresid`` (bias grad of
-    the linear that produced the residual branch feeding this norm).
+    the linear that produced the residual branch feeding this norm). With ``dropout_p`` (the
+    branch's dropout in the forward's ``add_ln_fwd``) the bf16 copy and the bias sum carry the
+    regenerated mask; the fp32 residual gradient does not.
     """
-    kernels().layernorm_bwd(dy, x, mean, rstd, w, dresid, accumulate, dresid_bf16, dw, db, dbias_prev)
+    kernels().layernorm_bwd(dy, x, mean, rstd, w, dresid, accumulate, dresid_bf16, dw, db, dbias_prev,
+                            float(dropout_p), int(dropout_seed))
 
 
 # --------------------------------------------------------------------------- autograd front-ends

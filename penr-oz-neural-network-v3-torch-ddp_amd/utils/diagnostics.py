@@ -61,7 +61,9 @@ def _saturation(algo: str, a: Tensor) -> float:
 
 
 @torch.no_grad()
-def training_stats(algos: list[str], acts: list, weights: list) -> dict:
+def training_stats(algos: list[str], acts: list, weights: list, grad_of=None) -> dict:
+    """``grad_of(w)``: the gradient of weight ``w`` when it is not ``w.grad`` (the fused executor
+    keeps bf16-parameter models' fp32 gradients in its flat buffer)."""
     layers = []
     for algo, pair in zip(algos, acts):
         a, g = pair
@@ -80,8 +82,9 @@ def training_stats(algos: list[str], acts: list, weights: list) -> dict:
             continue
         wm, ws = float(w.float().mean()), float(w.float().std())
         grad = {"mean": None, "std": None, "histogram": {"x": [], "y": []}}
-        if w.grad is not None:
-            gm, gs, gx, gy = _hist(w.grad)
+        g = grad_of(w) if grad_of is not None else w.grad
+        if g is not None:
+            gm, gs, gx, gy = _hist(g)
             grad = {"mean": gm, "std": gs, "histogram": {"x": gx, "y": gy}}
         wstats.append({"shape": str(tuple(w.shape)), "data": {"mean": wm, "std": ws}, "gradient": grad})
     return {"layers": layers, "weights": wstats}

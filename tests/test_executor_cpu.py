@@ -21,7 +21,11 @@ def test_hf_style_layouts():
     from transformers import GPT2Config
     from penroz.models import hf
     cfg = GPT2Config(vocab_size=128, n_positions=64, n_embd=128, n_layer=1, n_head=2)
-    assert GPTExecutor.match(_model(hf.gpt2_layers(cfg))) is None  # HF default dropout 0.1 -> generic path
+    spec = GPTExecutor.match(_model(hf.gpt2_layers(cfg)))  # HF default dropout 0.1: fused kernels
+    assert spec is not None and spec.p_embd == 0.1 and spec.blocks[0].p_attn_res == spec.blocks[0].p_mlp_res == 0.1
+    bf = _model(hf.gpt2_layers(cfg)).to(dtype=__import__("torch").bfloat16)  # /import/ loads bf16 weights
+    assert GPTExecutor.match(bf).param_dtype == __import__("torch").bfloat16
+    assert GPTExecutor.match(bf, require_fp32=True) is None
     cfg = GPT2Config(vocab_size=128, n_positions=64, n_embd=128, n_layer=1, n_head=2, resid_pdrop=0.0,
                      embd_pdrop=0.0, attn_pdrop=0.1)
     spec = GPTExecutor.match(_model(hf.gpt2_layers(cfg)))

@@ -90,8 +90,8 @@ def test_decode_program_graph_replay_matches_eager_program(monkeypatch):
     assert all(d.program is not None and isinstance(d.graph, torch.cuda.CUDAGraph) for d in m._graph_decoders.values())
     m.__dict__.pop("_graph_decoders")
 
-    def eager_capture(self, last_tok, cache_len):
-        self._set_state(last_tok, cache_len)
+    def eager_capture(self, last_tok, cache_len, start=0):
+        self._set_state(last_tok, cache_len, start)
         self.graph = _EagerGraph(self)
 
     monkeypatch.setattr(gd.GraphDecoder, "_capture", eager_capture)
@@ -186,8 +186,8 @@ def test_gemma_program_graph_replay_matches_eager_program(monkeypatch):
                for d in m._graph_decoders.values())
     m.__dict__.pop("_graph_decoders")
 
-    def eager_capture(self, last_tok, cache_len):
-        self._set_state(last_tok, cache_len)
+    def eager_capture(self, last_tok, cache_len, start=0):
+        self._set_state(last_tok, cache_len, start)
         self.graph = _EagerGraph(self)
 
     monkeypatch.setattr(gd.GraphDecoder, "_capture", eager_capture)

@@ -148,6 +148,31 @@ def test_cross_entropy(V):
     assert torch.equal(g2, logits), "eval mode must not modify logits"
 
 
+@pytest.mark.parametrize("V", [50257, 1001, 9])
+def test_cross_entropy_any_vocab_padded_rows(V):
+    """HF GPT-2's V = 50257: rows at a padded stride (multiple of 8); pads read as -inf, get 0."""
+    N, ld = 40, (V + 7) // 8 * 8
+    buf = torch.full((N, ld), 7.0, device=DEV, dtype=torch.bfloat16)  # pads hold junk
+    logits = buf[:, :V]
+    logits.copy_((torch.randn(N, V, device=DEV) * 3).to(torch.bfloat16))
+    tgt = torch.randint(0, V, (N,), device=DEV)
+    tgt[0] = V - 1
+    ref_loss = F.cross_entropy(logits.float(), tgt, reduction="none")
+    lf = logits.float().requires_grad_()
+    F.cross_entropy(lf, tgt, reduction="sum").backward()
+    loss = Fu.cross_entropy_fwd_bwd(logits, tgt, 0.25)
+    _close(loss, ref_loss, 2e-3, 1e-4, "loss")
+    _close(logits, 0.25 * lf.grad, 2e-3, 1e-2, "grad")
+    assert torch.all(buf[:, V:] == 0), "pad columns must get a zero gradient"
+    # the lm_head GEMM writes straight into the strided view (no hidden copy)
+    x = torch.randn(N, 64, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(V, 64, device=DEV, dtype=torch.bfloat16)
+    ptr = logits.data_ptr()
+    torch.mm(x, w.t(), out=logits)
+    assert logits.data_ptr() == ptr
+    _close(logits, x.float() @ w.float().t(), 0.1, 0.01)
+
+
 def test_adamw_flat_matches_torch():
     torch.manual_seed(0)
     n = 10007
@@ -591,3 +616,74 @@ def test_sampling_two_stage_wide_vocab(dt):
     freq = torch.stack([(draws == h).float().mean() for h in hot[:3]])
     probs = torch.softmax(torch.tensor([2.0, 1.5, 1.0]), -1)
     assert torch.allclose(freq, probs, atol=0.04), (freq, probs)
+
+
+# ---- residual / embedding dropout (HF GPT-2 resid_pdrop / embd_pdrop in the fused executor) ----
+def _mask_of(C, N, p, seed):
+    """The kernels' mask/(1-p) for element (row, col), read back through add_ln_fwd with
+    resid_in = 0 and delta = 1."""
+    zeros = torch.zeros(N, C, device=DEV)
+    ones = torch.ones(N, C, device=DEV, dtype=torch.bfloat16)
+    w, b = torch.ones(C, device=DEV), torch.zeros(C, device=DEV)
+    m = torch.empty(N, C, device=DEV)
+    Nm.add_ln_fwd(zeros, ones, m, w, b, 1e-5, dropout_p=p, dropout_seed=seed)
+    return m
+
+
+@pytest.mark.parametrize("C", [768, 4100])
+def test_add_layernorm_fwd_dropout(C):
+    torch.manual_seed(2)
+    N, p, seed = 129, 0.1, 1234
+    m = _mask_of(C, N, p, seed)
+    kept = (m != 0).float().mean().item()
+    assert abs(kept - (1 - p)) < 0.02, kept
+    assert torch.allclose(m[m != 0], torch.full_like(m[m != 0], 1 / (1 - p)))
+    assert not torch.equal(m, _mask_of(C, N, p, seed + 1))  # the seed selects the mask
+    x = torch.randn(N, C, device=DEV)
+    d = torch.randn(N, C, device=DEV).to(torch.bfloat16)
+    w, b = torch.randn(C, device=DEV), torch.randn(C, device=DEV)
+    out = torch.empty_like(x)
+    y, _, _ = Nm.add_ln_fwd(x, d, out, w, b, 1e-5, dropout_p=p, dropout_seed=seed)
+    ref = x + d.float() * m
+    _close(out, ref, 1e-5)
+    ry, _, _ = Nm.reference_layer_norm(ref, w, b, 1e-5)
+    _close(y, ry, 0.06, 0.01)
+
+
+def test_layernorm_bwd_dropout():
+    """The fp32 residual gradient is unmasked; the branch gradient (bf16 copy) and the producing
+    linear's bias gradient carry the forward's mask."""
+    torch.manual_seed(3)
+    N, C, p, seed = 512, 768, 0.1, 99
+    m = _mask_of(C, N, p, seed)
+    x = torch.randn(N, C, device=DEV) * 2
+    w, b = torch.randn(C, device=DEV), torch.randn(C, device=DEV)
+    dy = torch.randn(N, C, device=DEV).to(torch.bfloat16)
+    _, mean, rstd = Nm.ln_fwd(x, w, b, 1e-5, torch.float32)
+    base = torch.randn(N, C, device=DEV)
+    dres = base.clone()
+    dres_bf = torch.empty(N, C, device=DEV, dtype=torch.bfloat16)
+    dw, db, dbp = (torch.zeros(C, device=DEV) for _ in range(3))
+    Nm.ln_bwd(dy, x, mean, rstd, w, dres, True, dres_bf, dw, db, dbp, dropout_p=p, dropout_seed=seed)
+    rdx, rdw, rdb = Nm.reference_layer_norm_bwd(dy, x, mean, rstd, w)
+    full = base + rdx
+    _close(dres, full, 2e-3, 1e-4, "dx")
+    _close(dres_bf, full * m, 0.06, 0.01, "branch grad")
+    _close(dbp, (full * m).sum(0), 2e-2, 1e-4, "dbias")
+    _close(dw, rdw, 1e-2, 1e-4, "dw")
+
+
+def test_embedding_dropout():
+    V, P, C, B, T, p, seed = 1000, 64, 768, 3, 50, 0.1, 7
+    wte, wpe = torch.randn(V, C, device=DEV), torch.randn(P, C, device=DEV)
+    idx = torch.randint(0, V, (B, T), device=DEV)
+    m = _mask_of(C, B * T, p, seed)
+    out = Fu.embedding_fwd(idx, wte, wpe, 3, dropout_p=p, dropout_seed=seed)
+    _close(out, Fu.reference_embedding_fwd(idx, wte, wpe, 3) * m, 1e-5)
+    dout = torch.randn(B * T, C, device=DEV)
+    dwte, dwpe = torch.zeros(V, C, device=DEV), torch.zeros(P, C, device=DEV)
+    Fu.embedding_bwd(dout, idx, dwte, dwpe, 3, dropout_p=p, dropout_seed=seed)
+    w1, w2 = wte.clone().requires_grad_(), wpe.clone().requires_grad_()
+    (Fu.reference_embedding_fwd(idx, w1, w2, 3) * m * dout).sum().backward()
+    _close(dwte, w1.grad, 1e-4)
+    _close(dwpe, w2.grad, 1e-4)
