@@ -49,7 +49,7 @@ def main():
     if "fwd" in a.which:
         from penroz.ops._ext import kernels
         k = kernels()
-        variants = [1, 2, 3] + ([99] if os.environ.get('PENROZ_FA_DIAG') else []) if hasattr(k, "flash_fwd_variant") else [0]
+        variants = [1, 3] if (hasattr(k, "flash_fwd_variant") and D == 64) else [0]
         for v in variants:
             if v:
                 prev = k.flash_fwd_variant(v)
@@ -63,7 +63,7 @@ def main():
         k = kernels()
         dout = torch.randn_like(out)
         dq = torch.empty_like(qkv)
-        variants = [1, 2] if hasattr(k, "flash_bwd_variant") else [0]
+        variants = [1, 2] if (hasattr(k, "flash_bwd_variant") and D == 64) else [0]
         for v in variants:
             if v:
                 prev = k.flash_bwd_variant(v)
@@ -72,10 +72,18 @@ def main():
             res.update({f"bwd{sfx}_us": round(t * 1e6, 1), f"bwd{sfx}_TF": round(2.5 * fl / t / 1e12, 1)})
             if v:
                 k.flash_bwd_variant(prev)
-    if a.sdpa and Hkv == H:
-        q, k, v = (x.view(B, T, H, D).transpose(1, 2) for x in qkv.split(H * D, dim=2))
-        t = timeit(lambda: F.scaled_dot_product_attention(q, k, v, is_causal=True), a.iters)
+    if a.sdpa:
+        q, k, v = qkv.split([H * D, Hkv * D, Hkv * D], dim=2)
+        q = q.reshape(B, T, H, D).transpose(1, 2).detach().requires_grad_()
+        k = k.reshape(B, T, Hkv, D).transpose(1, 2).detach().requires_grad_()
+        v = v.reshape(B, T, Hkv, D).transpose(1, 2).detach().requires_grad_()
+        gqa = Hkv != H
+        t = timeit(lambda: F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=gqa), a.iters)
         res.update(sdpa_fwd_us=round(t * 1e6, 1), sdpa_fwd_TF=round(fl / t / 1e12, 1))
+        o = F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=gqa)
+        go = torch.randn_like(o)
+        t = timeit(lambda: torch.autograd.grad(o, (q, k, v), go, retain_graph=True), a.iters)
+        res.update(sdpa_bwd_us=round(t * 1e6, 1), sdpa_bwd_TF=round(2.5 * fl / t / 1e12, 1))
     print(json.dumps(res), flush=True)
 
 

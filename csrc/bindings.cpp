@@ -72,6 +72,12 @@ int64_t flash_fwd_variant(int64_t v);
 int64_t flash_bwd_variant(int64_t v);
 void flash_attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, torch::Tensor dqkv,
                     int64_t H, int64_t Hkv, int64_t D, double scale, double p_drop, int64_t seed);
+// flash_attn_gen.hip (head_dim 128 / 256)
+void flash_attn_gen_fwd(torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int64_t H, int64_t Hkv, int64_t D,
+                        double scale, double p_drop, int64_t seed);
+void flash_attn_gen_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, torch::Tensor lse,
+                        torch::Tensor dqkv, int64_t H, int64_t Hkv, int64_t D, double scale, double p_drop,
+                        int64_t seed);
 
 PYBIND11_MODULE(penroz_kernels, m) {
   m.doc() = "penroz hand-written HIP kernels for MI355X (gfx950)";
@@ -132,4 +138,6 @@ PYBIND11_MODULE(penroz_kernels, m) {
   m.def("flash_fwd_variant", &flash_fwd_variant, pybind11::arg("variant") = 0,
         "select the forward kernel (1 single-stage, 2 tile-pipelined); returns the previous one");
   m.def("flash_attn_bwd", &flash_attn_bwd);
+  m.def("flash_attn_gen_fwd", &flash_attn_gen_fwd, "causal flash attention forward, head_dim 128 / 256");
+  m.def("flash_attn_gen_bwd", &flash_attn_gen_bwd, "causal flash attention backward, head_dim 128 / 256");
 }

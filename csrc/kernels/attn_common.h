@@ -1,0 +1,110 @@
+// Shared device helpers of the flash-attention kernels (flash_attn.hip: head_dim 64, tuned;
+// flash_attn_gen.hip: head_dim 128 / 256). v_mfma_f32_32x32x16_bf16 operand / accumulator
+// maps, the XOR-swizzled LDS tile image, softmax lane exchanges, dropout hash, XCD mapping.
+#pragma once
+#include "common.h"
+
+namespace penroz {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+__device__ __forceinline__ f32x16 mfma32(uint4 a, uint4 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
+                                                 0, 0, 0);
+}
+
+__device__ __forceinline__ int tile_off(int row, int ch) {
+  return row * 128 + ((ch ^ ((((row >> 1) & 1) << 2) | ((row >> 2) & 3))) << 4);
+}
+
+// element j = tile[rbase + (lane&31)][16s + 8·hh + j]
+__device__ __forceinline__ uint4 row_frag(const char* tile, int rbase, int s, int lane) {
+  return *reinterpret_cast<const uint4*>(tile + tile_off(rbase + (lane & 31), 2 * s + (lane >> 5)));
+}
+
+__device__ __forceinline__ uint2 tr_read(const char* tile, int row, int col) {
+  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s16x4*)(tile + tile_off(row, col >> 3) + ((col & 4) << 1)));
+  return __builtin_bit_cast(uint2, v);
+}
+
+// element j = tile[rbase + 8(j>>2) + 4·hh + (j&3)][cbase + (lane&31)]  (transposed read)
+__device__ __forceinline__ uint4 tr_frag(const char* tile, int rbase, int cbase, int lane) {
+  const int hh = lane >> 5, q = (lane & 15) >> 2, p = lane & 3;
+  const int col = cbase + 16 * ((lane >> 4) & 1) + 4 * p;
+  const uint2 a = tr_read(tile, rbase + 4 * hh + q, col);
+  const uint2 b = tr_read(tile, rbase + 8 + 4 * hh + q, col);
+  return uint4{a.x, a.y, b.x, b.y};
+}
+
+// accumulator registers 8ss..8ss+7 -> bf16x8 operand
+__device__ __forceinline__ uint4 acc_frag(const f32x16& a, int ss) {
+  const int o = 8 * ss;
+  return uint4{pack_bf16x2(a[o], a[o + 1]), pack_bf16x2(a[o + 2], a[o + 3]), pack_bf16x2(a[o + 4], a[o + 5]),
+               pack_bf16x2(a[o + 6], a[o + 7])};
+}
+
+__device__ __forceinline__ int acc_row(int i, int lane) { return (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5); }
+
+__device__ __forceinline__ bool dropout_keep(uint64_t seed, int b, int h, int H, int T, int q, int k, float p) {
+  const uint64_t ctr = (((uint64_t)b * H + h) * (uint64_t)T + (uint64_t)q) * (uint64_t)T + (uint64_t)k;
+  return uniform01(seed, ctr) >= p;
+}
+
+__device__ __forceinline__ uint4 zero4() { return uint4{0u, 0u, 0u, 0u}; }
+
+// raw v_exp_f32 (no denormal range fix-up: softmax weights that small are 0 anyway)
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// wave index, provably wave-uniform for the compiler (keeps causal-mask branches scalar)
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
+// Combine a value across the two 32-lane halves (lane l and l^32) with one
+// v_permlane32_swap instead of a ds_bpermute round trip. The swap of (v, v) returns
+// {[lo|lo], [hi|hi]}, so op(r0, r1) is the full-row result in every lane.
+__device__ __forceinline__ float halves_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float halves_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// defer-rescale threshold (log2 units): the running max is only raised when some row's max
+// grows by more than 2^8, so most tiles skip the O rescale (P then stays <= 256: bf16-safe)
+constexpr float kRescaleThr = 8.0f;
+
+// stores 4 consecutive bf16 (8 bytes)
+__device__ __forceinline__ void store4(bf16* p, float a, float b, float c, float d) {
+  *reinterpret_cast<uint2*>(p) = uint2{pack_bf16x2(a, b), pack_bf16x2(c, d)};
+}
+
+// XCD-aware block mapping. Workgroups are dealt to the 8 XCDs round-robin in dispatch order
+// (x fastest), so the plain grid would scatter one head's blocks over all eight L2s. Remap so
+// the gridDim.x blocks of a head share an XCD (its L2 then serves the head's K/V or Q/dO
+// re-reads) with heads dealt to XCDs round-robin; block index order (heaviest first) is kept
+// per XCD. Bijective; a tail of heads that is not a multiple of 8 keeps the plain order.
+__device__ __forceinline__ void xcd_head_block(int& blk, int& head) {
+  const int nblk = gridDim.x, nheads = gridDim.y;
+  const int id = blockIdx.x + nblk * blockIdx.y;
+  const int full = (nheads >> 3) * nblk;  // slots per XCD in the full head groups
+  const int xcd = id & 7, slot = id >> 3;
+  if (slot < full) {
+    head = (slot / nblk) * 8 + xcd;
+    blk = slot - (slot / nblk) * nblk;
+  } else {
+    const int r = id - 8 * full;
+    head = (nheads & ~7) + r / nblk;
+    blk = r - (r / nblk) * nblk;
+  }
+}
+
+
+}  // namespace penroz

@@ -35,113 +35,14 @@
 // Dropout (attn_pdrop) uses a counter-based hash of (b, h, q, k): the backward regenerates
 // the identical mask; the softmax normaliser uses the undropped probabilities (SDPA
 // semantics).
-#include "common.h"
+#include "attn_common.h"
 #include <type_traits>
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 
 namespace penroz {
 
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-
 constexpr int kD = 64;
-constexpr float kLog2e = 1.4426950408889634f;
-constexpr float kLn2 = 0.6931471805599453f;
-
-__device__ __forceinline__ f32x16 mfma32(uint4 a, uint4 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
-                                                 0, 0, 0);
-}
-
-__device__ __forceinline__ int tile_off(int row, int ch) {
-  return row * 128 + ((ch ^ ((((row >> 1) & 1) << 2) | ((row >> 2) & 3))) << 4);
-}
-
-// element j = tile[rbase + (lane&31)][16s + 8·hh + j]
-__device__ __forceinline__ uint4 row_frag(const char* tile, int rbase, int s, int lane) {
-  return *reinterpret_cast<const uint4*>(tile + tile_off(rbase + (lane & 31), 2 * s + (lane >> 5)));
-}
-
-__device__ __forceinline__ uint2 tr_read(const char* tile, int row, int col) {
-  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (lds_s16x4*)(tile + tile_off(row, col >> 3) + ((col & 4) << 1)));
-  return __builtin_bit_cast(uint2, v);
-}
-
-// element j = tile[rbase + 8(j>>2) + 4·hh + (j&3)][cbase + (lane&31)]  (transposed read)
-__device__ __forceinline__ uint4 tr_frag(const char* tile, int rbase, int cbase, int lane) {
-  const int hh = lane >> 5, q = (lane & 15) >> 2, p = lane & 3;
-  const int col = cbase + 16 * ((lane >> 4) & 1) + 4 * p;
-  const uint2 a = tr_read(tile, rbase + 4 * hh + q, col);
-  const uint2 b = tr_read(tile, rbase + 8 + 4 * hh + q, col);
-  return uint4{a.x, a.y, b.x, b.y};
-}
-
-// accumulator registers 8ss..8ss+7 -> bf16x8 operand
-__device__ __forceinline__ uint4 acc_frag(const f32x16& a, int ss) {
-  const int o = 8 * ss;
-  return uint4{pack_bf16x2(a[o], a[o + 1]), pack_bf16x2(a[o + 2], a[o + 3]), pack_bf16x2(a[o + 4], a[o + 5]),
-               pack_bf16x2(a[o + 6], a[o + 7])};
-}
-
-__device__ __forceinline__ int acc_row(int i, int lane) { return (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5); }
-
-__device__ __forceinline__ bool dropout_keep(uint64_t seed, int b, int h, int H, int T, int q, int k, float p) {
-  const uint64_t ctr = (((uint64_t)b * H + h) * (uint64_t)T + (uint64_t)q) * (uint64_t)T + (uint64_t)k;
-  return uniform01(seed, ctr) >= p;
-}
-
-__device__ __forceinline__ uint4 zero4() { return uint4{0u, 0u, 0u, 0u}; }
-
-// raw v_exp_f32 (no denormal range fix-up: softmax weights that small are 0 anyway)
-__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
-
-// wave index, provably wave-uniform for the compiler (keeps causal-mask branches scalar)
-__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
-
-// Combine a value across the two 32-lane halves (lane l and l^32) with one
-// v_permlane32_swap instead of a ds_bpermute round trip. The swap of (v, v) returns
-// {[lo|lo], [hi|hi]}, so op(r0, r1) is the full-row result in every lane.
-__device__ __forceinline__ float halves_max(float v) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
-}
-__device__ __forceinline__ float halves_sum(float v) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-
-// defer-rescale threshold (log2 units): the running max is only raised when some row's max
-// grows by more than 2^8, so most tiles skip the O rescale (P then stays <= 256: bf16-safe)
-constexpr float kRescaleThr = 8.0f;
-
-// stores 4 consecutive bf16 (8 bytes)
-__device__ __forceinline__ void store4(bf16* p, float a, float b, float c, float d) {
-  *reinterpret_cast<uint2*>(p) = uint2{pack_bf16x2(a, b), pack_bf16x2(c, d)};
-}
-
-// XCD-aware block mapping. Workgroups are dealt to the 8 XCDs round-robin in dispatch order
-// (x fastest), so the plain grid would scatter one head's blocks over all eight L2s. Remap so
-// the gridDim.x blocks of a head share an XCD (its L2 then serves the head's K/V or Q/dO
-// re-reads) with heads dealt to XCDs round-robin; block index order (heaviest first) is kept
-// per XCD. Bijective; a tail of heads that is not a multiple of 8 keeps the plain order.
-__device__ __forceinline__ void xcd_head_block(int& blk, int& head) {
-  const int nblk = gridDim.x, nheads = gridDim.y;
-  const int id = blockIdx.x + nblk * blockIdx.y;
-  const int full = (nheads >> 3) * nblk;  // slots per XCD in the full head groups
-  const int xcd = id & 7, slot = id >> 3;
-  if (slot < full) {
-    head = (slot / nblk) * 8 + xcd;
-    blk = slot - (slot / nblk) * nblk;
-  } else {
-    const int r = id - 8 * full;
-    head = (nheads & ~7) + r / nblk;
-    blk = r - (r / nblk) * nblk;
-  }
-}
 
 // ------------------------------------------------------------------------------------------
 // forward
@@ -294,187 +195,13 @@ __global__ void __launch_bounds__(256, 2) fa_fwd_kernel(const bf16* __restrict__
 }
 
 // ------------------------------------------------------------------------------------------
-// forward, software-pipelined across key tiles (default): S_{j+1} = K_{j+1}·Qᵀ is issued
-// before tile j's softmax so the matrix cores run it while the SIMD does tile j's VALU work
-// (an MFMA blocks vector issue for only 8 of its 32 cycles); V_j's transposed fragments are
-// read before the softmax so their LDS latency hides behind it too. K/V live in a 3-stage LDS
-// ring (K_{j+1} and V_j are read while tile j+2 is staged), one barrier per tile.
-template <bool DROPOUT>
-__global__ void __launch_bounds__(256, 2) fa_fwd2_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
-                                                      float* __restrict__ lse, int T, int H, int Hkv, float scale,
-                                                      float p_drop, uint64_t seed) {
-  constexpr int BM = 128, BN = 64, NST = 3;
-  __shared__ __attribute__((aligned(16))) char smem[NST][2][BN * 128];
-  const int nqb = (T + BM - 1) / BM;
-  int qi, bh;
-  xcd_head_block(qi, bh);
-  const int qb = nqb - 1 - qi;
-  const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
-  const int lane = threadIdx.x & 63, w = wave_id(), hh = lane >> 5;
-  const size_t RS = (size_t)(H + 2 * Hkv) * kD;
-  const bf16* qbase = qkv + (size_t)b * T * RS + (size_t)h * kD;
-  const bf16* kbase = qkv + (size_t)b * T * RS + (size_t)(H + hk) * kD;
-  const bf16* vbase = qkv + (size_t)b * T * RS + (size_t)(H + Hkv + hk) * kD;
-  const int q0 = qb * BM + 32 * w;
-  const int qrow = q0 + (lane & 31);
-  const float c = scale * kLog2e;
-  const float inv_keep = DROPOUT ? 1.f / (1.f - p_drop) : 1.f;
-
-  uint4 qf[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s)
-    qf[s] = qrow < T ? *reinterpret_cast<const uint4*>(qbase + (size_t)qrow * RS + 16 * s + 8 * hh) : zero4();
-
-  const int sr = threadIdx.x >> 3, sc = threadIdx.x & 7;
-  uint4 kst[2], vst[2];
-  auto gload = [&](int kt0) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int key = kt0 + sr + 32 * i;
-      kst[i] = key < T ? *reinterpret_cast<const uint4*>(kbase + (size_t)key * RS + 8 * sc) : zero4();
-      vst[i] = key < T ? *reinterpret_cast<const uint4*>(vbase + (size_t)key * RS + 8 * sc) : zero4();
-    }
-  };
-  auto lstore = [&](int stg) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      *reinterpret_cast<uint4*>(smem[stg][0] + tile_off(sr + 32 * i, sc)) = kst[i];
-      *reinterpret_cast<uint4*>(smem[stg][1] + tile_off(sr + 32 * i, sc)) = vst[i];
-    }
-  };
-  auto scores = [&](int stg, f32x16 (&sa)[2]) {
-    const char* Kt = smem[stg][0];
-#pragma unroll
-    for (int kh = 0; kh < 2; ++kh) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) sa[kh][i] = 0.f;
-#pragma unroll
-      for (int st = 0; st < 4; ++st) sa[kh] = mfma32(row_frag(Kt, 32 * kh, st, lane), qf[st], sa[kh]);
-    }
-  };
-
-  const int kend = min(T, qb * BM + BM);
-  const int ntiles = (kend + BN - 1) / BN;
-  const int jlast = min(ntiles - 1, (q0 + 31) / BN);  // this wave's last tile with a visible key
-  f32x16 o[2];
-#pragma unroll
-  for (int dh = 0; dh < 2; ++dh)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) o[dh][i] = 0.f;
-  float m = -1e30f, l = 0.f;
-
-  // one pipelined step: S of tile j+1 into `sn`, softmax + P·V of tile j from `sc`
-  auto step = [&](int j, f32x16 (&scur)[2], f32x16 (&snext)[2]) {
-    const int kt0 = j * BN;
-    if (j + 2 < ntiles) gload(kt0 + 2 * BN);
-    if (j + 1 <= jlast) scores((j + 1) % NST, snext);
-    __builtin_amdgcn_sched_barrier(0);
-    if (j <= jlast) {
-      const char* Vt = smem[j % NST][1];
-      uint4 vfr[2][2][2];
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss)
-#pragma unroll
-          for (int dh = 0; dh < 2; ++dh) vfr[kh][ss][dh] = tr_frag(Vt, 32 * kh + 16 * ss, 32 * dh, lane);
-      auto softmax = [&](auto mask_tag) {
-        constexpr bool MASK = decltype(mask_tag)::value;
-        float tmax = -INFINITY;
-#pragma unroll
-        for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            if constexpr (MASK) {
-              const int key = kt0 + 32 * kh + acc_row(i, lane);
-              scur[kh][i] = (key > qrow || key >= T) ? -INFINITY : scur[kh][i];
-            }
-            tmax = fmaxf(tmax, scur[kh][i]);
-          }
-        tmax = halves_max(tmax) * c;
-        if (!__all(tmax <= m + kRescaleThr)) {
-          const float mnew = fmaxf(m, tmax);
-          const float alpha = fexp2(m - mnew);
-          m = mnew;
-          l *= alpha;
-#pragma unroll
-          for (int dh = 0; dh < 2; ++dh)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) o[dh][i] *= alpha;
-        }
-        const float negm = -m;
-        float2_t lsum = {0.f, 0.f};
-#pragma unroll
-        for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-          for (int i = 0; i < 16; i += 2) {
-            float2_t p = {fexp2(fmaf(scur[kh][i], c, negm)), fexp2(fmaf(scur[kh][i + 1], c, negm))};
-            lsum += p;
-            if constexpr (DROPOUT) {
-              const int key = kt0 + 32 * kh + acc_row(i, lane);
-              p[0] = dropout_keep(seed, b, h, H, T, qrow, key, p_drop) ? p[0] * inv_keep : 0.f;
-              p[1] = dropout_keep(seed, b, h, H, T, qrow, key + 1, p_drop) ? p[1] * inv_keep : 0.f;
-            }
-            scur[kh][i] = p[0];
-            scur[kh][i + 1] = p[1];
-          }
-        l += lsum[0] + lsum[1];
-      };
-      if ((kt0 + BN - 1 > q0) || (kt0 + BN > T))
-        softmax(std::true_type{});
-      else
-        softmax(std::false_type{});
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss) {
-          const uint4 pf = acc_frag(scur[kh], ss);
-#pragma unroll
-          for (int dh = 0; dh < 2; ++dh) o[dh] = mfma32(vfr[kh][ss][dh], pf, o[dh]);
-        }
-    }
-    if (j + 2 < ntiles) lstore((j + 2) % NST);
-    __syncthreads();
-  };
-
-  gload(0);
-  lstore(0);
-  if (ntiles > 1) {
-    gload(BN);
-    lstore(1);
-  }
-  __syncthreads();
-  f32x16 sA[2], sB[2];
-  scores(0, sA);
-  int j = 0;
-  for (; j + 1 < ntiles; j += 2) {
-    step(j, sA, sB);
-    step(j + 1, sB, sA);
-  }
-  if (j < ntiles) step(j, sA, sB);
-
-  l = halves_sum(l);
-  const float inv = l > 0.f ? 1.f / l : 0.f;
-  if (qrow < T) {
-    bf16* orow = out + ((size_t)b * T + qrow) * H * kD + (size_t)h * kD;
-#pragma unroll
-    for (int dh = 0; dh < 2; ++dh)
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        store4(orow + 32 * dh + 8 * g + 4 * hh, o[dh][4 * g] * inv, o[dh][4 * g + 1] * inv, o[dh][4 * g + 2] * inv,
-               o[dh][4 * g + 3] * inv);
-    if (hh == 0) lse[((size_t)b * H + h) * T + qrow] = (m + log2f(l)) * kLn2;
-  }
-}
-
-// ------------------------------------------------------------------------------------------
 // forward, two query blocks per wave (default): a 128-thread workgroup = 2 waves × 64 query
 // rows; each wave holds two independent 32-row blocks A and B. Per 64-key tile the K
 // fragments (row reads) and V fragments (transposed reads) are read from LDS ONCE per wave
 // and used by both blocks, halving LDS traffic per MFMA, and the two blocks' dependency
 // chains interleave: S_B's MFMAs run under softmax_A, P_A·V's under softmax_B. Query blocks
 // of 64 rows are aligned to key tiles, so a wave's only masked tile is its diagonal one.
-template <bool DROPOUT, bool NOSYNC = false>
+template <bool DROPOUT>
 __global__ void __launch_bounds__(128, 2) fa_fwd3_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
                                                       float* __restrict__ lse, int T, int H, int Hkv, float scale,
                                                       float p_drop, uint64_t seed) {
@@ -665,23 +392,17 @@ __global__ void __launch_bounds__(128, 2) fa_fwd3_kernel(const bf16* __restrict_
   for (; j < jlast; ++j) {
     dma((j + 1) * BN, (j + 1) & 1);  // j < jlast <= ntiles-1: buffer freed by the last barrier
     tile(std::false_type{}, j);
-    if constexpr (!NOSYNC) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-  }
-  if (j + 1 < ntiles) dma((j + 1) * BN, (j + 1) & 1);
-  tile(std::true_type{}, j);
-  if constexpr (!NOSYNC) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
+  if (j + 1 < ntiles) dma((j + 1) * BN, (j + 1) & 1);
+  tile(std::true_type{}, j);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   for (++j; j < ntiles; ++j) {
     if (j + 1 < ntiles) dma((j + 1) * BN, (j + 1) & 1);
-    if constexpr (!NOSYNC) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
   }
 
 #pragma unroll
@@ -1432,19 +1153,13 @@ void flash_attn_fwd(torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int
   else if (g_fa_fwd_variant == 1)
     hipLaunchKernelGGL(fa_fwd_kernel<false>, grid, dim3(256), 0, stream, q, o, lse.data_ptr<float>(), T, (int)H,
                        (int)Hkv, (float)scale, 0.f, (uint64_t)seed);
-  else if (g_fa_fwd_variant == 2)
-    hipLaunchKernelGGL(fa_fwd2_kernel<false>, grid, dim3(256), 0, stream, q, o, lse.data_ptr<float>(), T, (int)H,
-                       (int)Hkv, (float)scale, 0.f, (uint64_t)seed);
-  else if (g_fa_fwd_variant == 3)
+  else
     hipLaunchKernelGGL(fa_fwd3_kernel<false>, grid, dim3(128), 0, stream, q, o, lse.data_ptr<float>(), T, (int)H,
                        (int)Hkv, (float)scale, 0.f, (uint64_t)seed);
-  else  // 99: timing diagnostic only (no DMA wait / barrier inside the loop: WRONG results)
-    hipLaunchKernelGGL((fa_fwd3_kernel<false, true>), grid, dim3(128), 0, stream, q, o, lse.data_ptr<float>(), T,
-                       (int)H, (int)Hkv, (float)scale, 0.f, (uint64_t)seed);
 }
 
-// 1 = single-stage forward (fa_fwd_kernel), 2 = tile-pipelined forward (fa_fwd2_kernel),
-// 3 = two query blocks per wave (fa_fwd3_kernel, default)
+// forward: 1 = single-stage (fa_fwd_kernel; also the dropout path), 3 = two query blocks per
+// wave (fa_fwd3_kernel, default). backward:
 // 1 = register-staged dK/dV and dQ kernels, 2 = LDS-DMA pipelined dK/dV and dQ kernels (default)
 int64_t flash_bwd_variant(int64_t v) {
   const int64_t prev = g_fa_bwd_variant;

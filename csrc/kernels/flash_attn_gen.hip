@@ -1,0 +1,587 @@
+// Causal flash attention for head_dim 128 and 256 (Gemma-family training / prefill; the tuned
+// head_dim-64 kernels live in flash_attn.hip). bf16 in/out, fp32 accumulate, GQA by index math.
+//
+// Same algebra and operand maps as the head_dim-64 kernels (v_mfma_f32_32x32x16_bf16 with the
+// key on the MFMA lane or row so softmax rows never cross LDS; see flash_attn.hip), generalised
+// over D by storing every LDS tile as D/64 "panels" of 64 columns: panel p holds columns
+// 64p..64p+63 of all the tile's rows in the head_dim-64 image (128-B rows, XOR-swizzled chunk
+// order tile_off), so the bank-conflict-free row reads (ds_read_b128) and transposed reads
+// (ds_read_b64_tr_b16) carry over unchanged. Tiles arrive by LDS-DMA (global_load_lds_dwordx4,
+// swizzle applied on the per-lane SOURCE address, the LDS image stays lane-linear), double
+// buffered: tile j+1 is in flight while tile j computes.
+//
+//   forward   — workgroup = 2 (D = 128) or 4 (D = 256) waves × 32 query rows; 32-key tiles; Sᵀ = K·Qᵀ (Q in D/16
+//               registers), online softmax per lane (one query row per lane), Oᵀ += Vᵀ·Pᵀ
+//               with Oᵀ in D/32 accumulators; heaviest query blocks first; writes O head-merged
+//               and the row log-sum-exp (natural log), like the head_dim-64 kernel.
+//   backward  — δ = rowsum(dO·O); dK/dV kernel: a wave keeps 32 keys' K, V fragments and
+//               dKᵀ, dVᵀ accumulators in registers while sweeping 32-row query slices of every
+//               query head of its KV group (no cross-workgroup sum, deterministic); dQ kernel:
+//               forward-shaped, a wave keeps 32 query rows' Q, dO and dQᵀ in registers.
+// At D = 256 the register-resident operands exceed 256 VGPRs: those kernels run one wave per
+// SIMD with the accumulators in the AGPR half of the unified 512-entry register file.
+#include "attn_common.h"
+#include <type_traits>
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+
+namespace penroz {
+
+// At D = 256 hipcc would hoist every LDS fragment read of a fully unrolled MFMA chain ahead of
+// the chain (~128 extra VGPRs beside 128–256 accumulators) and spill; a scheduling fence per
+// group keeps at most a few fragments in flight.
+template <int D>
+__device__ __forceinline__ void d_fence() {
+  if constexpr (D >= 256) __builtin_amdgcn_sched_barrier(0);
+}
+
+// panel p of an LDS tile with R rows (R·128 bytes per panel)
+__device__ __forceinline__ const char* panel(const char* tile, int R, int p) { return tile + p * R * 128; }
+
+// swizzle of the LDS image for row r (depends on r & 15): physical chunk = logical ^ swz(r)
+__device__ __forceinline__ int swz(int r) { return (((r >> 1) & 1) << 2) | ((r >> 2) & 3); }
+
+// DMA R rows × D columns of a row-major bf16 matrix (row stride RS elements) into the paneled
+// tile image (PR rows per panel) at LDS byte address `dst`: NP·R/8 pieces (8 rows × 128 B each)
+// issued by this wave. Rows past T are clamped to T-1 (finite data the mask / P = 0 cancels).
+template <int NP, int R = 32, int PR = R>
+__device__ __forceinline__ void dma_rows(const bf16* base, size_t RS, int r0, int T, unsigned dst, int lane) {
+  const int rr = lane >> 3;
+#pragma unroll
+  for (int p = 0; p < NP; ++p)
+#pragma unroll
+    for (int r8 = 0; r8 < R / 8; ++r8) {
+      const int lc = (lane & 7) ^ swz(8 * (r8 & 1) + rr);  // the image row is 8·r8 + rr (PR, R % 16 == 0)
+      const int row = min(r0 + 8 * r8 + rr, T - 1);
+      glds16(base + (size_t)row * RS + 64 * p + 8 * lc, dst + (p * PR + 8 * r8) * 128);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// forward
+// D = 256 runs 4 waves per workgroup (128 query rows): its LDS (K/V double buffer + the Q image,
+// 128 KB) admits one workgroup per CU, and 4 waves then occupy all four SIMDs.
+template <int D> constexpr int fwd_waves() { return D >= 256 ? 4 : 2; }
+
+template <int D, bool DROPOUT>
+__global__ void __launch_bounds__(64 * fwd_waves<D>(), (D >= 256 ? 1 : 2))
+    fa_gen_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out, float* __restrict__ lse, int T, int H,
+                      int Hkv, float scale, float p_drop, uint64_t seed) {
+  constexpr int NP = D / 64, NS = D / 16, ND = D / 32, NW = fwd_waves<D>();
+  constexpr int BM = 32 * NW, BN = 32, TILE = BN * 128 * NP;
+  // D = 256: the 32 Q fragments would not fit beside Oᵀ (128 accumulators) in registers; the
+  // workgroup's query rows sit in LDS instead (read as B-operand row fragments per tile)
+  constexpr bool QLDS = D >= 256;
+  constexpr int QTILE = QLDS ? BM * 128 * NP : 16;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE + QTILE];
+  const int nqb = (T + BM - 1) / BM;
+  int qi, bh;
+  xcd_head_block(qi, bh);
+  const int qb = nqb - 1 - qi;
+  const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
+  const int lane = threadIdx.x & 63, w = wave_id(), hh = lane >> 5;
+  const size_t RS = (size_t)(H + 2 * Hkv) * D;
+  const bf16* qbase = qkv + (size_t)b * T * RS + (size_t)h * D;
+  const bf16* kbase = qkv + (size_t)b * T * RS + (size_t)(H + hk) * D;
+  const bf16* vbase = qkv + (size_t)b * T * RS + (size_t)(H + Hkv + hk) * D;
+  const int q0 = qb * BM + 32 * w;
+  const int qrow = q0 + (lane & 31);
+  const float c = scale * kLog2e;
+  const float inv_keep = DROPOUT ? 1.f / (1.f - p_drop) : 1.f;
+  const char* Qs = smem + 4 * TILE;
+
+  uint4 qf[QLDS ? 1 : NS];
+  if constexpr (QLDS) {
+    // both waves' rows, 32 per wave, into one 64-row paneled image
+    dma_rows<NP, 32, BM>(qbase, RS, qb * BM + 32 * w, T,
+                         __builtin_amdgcn_readfirstlane(lds_addr_of(smem + 4 * TILE)) + w * 32 * 128, lane);
+  } else {
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      qf[s] = qrow < T ? *reinterpret_cast<const uint4*>(qbase + (size_t)qrow * RS + 16 * s + 8 * hh) : zero4();
+#pragma unroll
+    for (int s = 0; s < NS; ++s) launder(qf[s]);
+  }
+  // B fragment s of Qᵀ: element j = Q[qrow][16s + 8hh + j]
+  auto qfrag = [&](int s) -> uint4 {
+    if constexpr (QLDS) return row_frag(panel(Qs, BM, s >> 2), 32 * w, s & 3, lane);
+    else return qf[s];
+  };
+
+  const int kend = min(T, qb * BM + BM);
+  const int ntiles = (kend + BN - 1) / BN;
+  f32x16 o[ND];
+#pragma unroll
+  for (int dh = 0; dh < ND; ++dh)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[dh][i] = 0.f;
+  float m = -1e30f, l = 0.f;
+
+  auto dma = [&](int j) {  // even waves: K tile, odd waves: V tile (NW = 4: half the panels each)
+    constexpr int NPW = NP * 2 / NW;
+    const int p0 = (w >> 1) * NPW;
+    const unsigned dst = __builtin_amdgcn_readfirstlane(lds_addr_of(smem + ((j & 1) * 2 + (w & 1)) * TILE)) +
+                         p0 * BN * 128;
+    dma_rows<NPW>(((w & 1) == 0 ? kbase : vbase) + 64 * p0, RS, j * BN, T, dst, lane);
+  };
+
+  dma(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int j = 0; j < ntiles; ++j) {
+    const int kt0 = j * BN;
+    if (j + 1 < ntiles) dma(j + 1);  // buffer (j+1)&1 was released by the previous barrier
+    const char* Kt = smem + (j & 1) * 2 * TILE;
+    const char* Vt = Kt + TILE;
+    if (kt0 <= q0 + 31 && q0 < T) {
+      f32x16 st;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) st[i] = 0.f;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        st = mfma32(row_frag(panel(Kt, BN, s >> 2), 0, s & 3, lane), qfrag(s), st);
+        if ((s & 3) == 3) d_fence<D>();
+      }
+      auto softmax = [&](auto mask_tag) {
+        constexpr bool MASK = decltype(mask_tag)::value;
+        float tmax = -INFINITY;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          if constexpr (MASK) {
+            const int key = kt0 + acc_row(i, lane);
+            st[i] = (key > qrow || key >= T) ? -INFINITY : st[i];
+          }
+          tmax = fmaxf(tmax, st[i]);
+        }
+        tmax = halves_max(tmax) * c;
+        if (!__all(tmax <= m + kRescaleThr)) {
+          const float mnew = fmaxf(m, tmax);
+          const float alpha = fexp2(m - mnew);
+          m = mnew;
+          l *= alpha;
+#pragma unroll
+          for (int dh = 0; dh < ND; ++dh)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) o[dh][i] *= alpha;
+        }
+        const float negm = -m;
+        float lsum = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float p = fexp2(fmaf(st[i], c, negm));
+          lsum += p;
+          if constexpr (DROPOUT) {
+            const int key = kt0 + acc_row(i, lane);
+            p = dropout_keep(seed, b, h, H, T, qrow, key, p_drop) ? p * inv_keep : 0.f;
+          }
+          st[i] = p;
+        }
+        l += lsum;
+      };
+      if (kt0 + BN - 1 > q0 || kt0 + BN > T)
+        softmax(std::true_type{});
+      else
+        softmax(std::false_type{});
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const uint4 pf = acc_frag(st, ss);
+#pragma unroll
+        for (int dh = 0; dh < ND; ++dh) {
+          o[dh] = mfma32(tr_frag(panel(Vt, BN, dh >> 1), 16 * ss, 32 * (dh & 1), lane), pf, o[dh]);
+          if (dh & 1) d_fence<D>();
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  l = halves_sum(l);
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  if (qrow < T) {
+    bf16* orow = out + ((size_t)b * T + qrow) * H * D + (size_t)h * D;
+#pragma unroll
+    for (int dh = 0; dh < ND; ++dh)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        store4(orow + 32 * dh + 8 * g + 4 * hh, o[dh][4 * g] * inv, o[dh][4 * g + 1] * inv, o[dh][4 * g + 2] * inv,
+               o[dh][4 * g + 3] * inv);
+    if (hh == 0) lse[((size_t)b * H + h) * T + qrow] = (m + log2f(l)) * kLn2;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// backward preprocessing: delta[b, h, q] = Σ_d dO·O  (D/8 lanes per row, 16-B loads)
+template <int D>
+__global__ void __launch_bounds__(256) fa_gen_bwd_pre_kernel(const bf16* __restrict__ dout,
+                                                             const bf16* __restrict__ out, float* __restrict__ delta,
+                                                             int B, int T, int H) {
+  constexpr int LPR = D / 8;  // lanes per row (16 or 32; divides 64)
+  const int gid = blockIdx.x * 256 + threadIdx.x;
+  const int row = gid / LPR, part = gid % LPR;  // row over B*T*H in [b][t][h] order
+  const bool ok = row < B * T * H;
+  float s = 0.f;
+  if (ok) {
+    float a[8], o[8];
+    Vec8<bf16>::load(dout + (size_t)row * D + 8 * part, a);
+    Vec8<bf16>::load(out + (size_t)row * D + 8 * part, o);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += a[k] * o[k];
+  }
+#pragma unroll
+  for (int off = 1; off < LPR; off <<= 1) s += __shfl_xor(s, off, 64);
+  if (ok && part == 0) {
+    const int h = row % H, t = (row / H) % T, b = row / (H * T);
+    delta[((size_t)b * H + h) * T + t] = s;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// dK / dV: grid (ceil(T/64) key blocks, B*Hkv); wave w owns keys kb*64 + 32w + (lane&31) and
+// sweeps 32-row query slices (every query head of its KV group) staged in LDS: Q | dO | LSE | δ.
+template <int D, bool DROPOUT>
+__global__ void __launch_bounds__(128, 1)
+    fa_gen_bwd_dkdv_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
+                           const float* __restrict__ delta, bf16* __restrict__ dqkv, int T, int H, int Hkv,
+                           float scale, float p_drop, uint64_t seed) {
+  constexpr int NP = D / 64, NS = D / 16, ND = D / 32;
+  constexpr int BK = 64, QS = 32;
+  constexpr int TILE = QS * 128 * NP;          // one 32-row slice of Q (or dO)
+  constexpr int STAGE = 2 * TILE + 2 * 256;    // Q | dO | LSE[64] | δ[64] (64-lane DMA pieces)
+  // D = 256: K and V fragments (128 registers) would not fit beside the dKᵀ / dVᵀ accumulators
+  // (256): the workgroup's 64 keys of K and V sit in LDS and are read per slice instead
+  constexpr bool KVLDS = D >= 256;
+  constexpr int KVT = BK * 128 * NP;           // 64 key rows
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + (KVLDS ? 2 * KVT : 16)];
+  int kb, bh;
+  xcd_head_block(kb, bh);  // key block kb ascending = heaviest first (causal)
+  const int b = bh / Hkv, hk = bh % Hkv;
+  const int G = H / Hkv;
+  const int lane = threadIdx.x & 63, w = wave_id(), hh = lane >> 5;
+  const size_t RS = (size_t)(H + 2 * Hkv) * D;
+  const size_t ORS = (size_t)H * D;
+  const int kw0 = kb * BK + 32 * w;
+  const int key = kw0 + (lane & 31);
+  const float c = scale * kLog2e;
+  const float inv_keep = DROPOUT ? 1.f / (1.f - p_drop) : 1.f;
+
+  const bf16* kbase = qkv + (size_t)b * T * RS + (size_t)(H + hk) * D;
+  const bf16* vbase = qkv + (size_t)b * T * RS + (size_t)(H + Hkv + hk) * D;
+  const char* KVs = smem + 2 * STAGE;  // [K 64 rows | V 64 rows] paneled images (KVLDS)
+  uint4 kf[KVLDS ? 1 : NS], vf[KVLDS ? 1 : NS];
+  if constexpr (KVLDS) {
+    dma_rows<NP, BK>(w == 0 ? kbase : vbase, RS, kb * BK, T,
+                     __builtin_amdgcn_readfirstlane(lds_addr_of(smem + 2 * STAGE)) + w * KVT, lane);
+  } else {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      kf[s] = key < T ? *reinterpret_cast<const uint4*>(kbase + (size_t)key * RS + 16 * s + 8 * hh) : zero4();
+      vf[s] = key < T ? *reinterpret_cast<const uint4*>(vbase + (size_t)key * RS + 16 * s + 8 * hh) : zero4();
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      launder(kf[s]);
+      launder(vf[s]);
+    }
+  }
+  // B fragment s of Kᵀ (Vᵀ): element j = K[key][16s + 8hh + j]
+  auto kfrag = [&](int s) -> uint4 {
+    if constexpr (KVLDS) return row_frag(panel(KVs, BK, s >> 2), 32 * w, s & 3, lane);
+    else return kf[s];
+  };
+  auto vfrag = [&](int s) -> uint4 {
+    if constexpr (KVLDS) return row_frag(panel(KVs + KVT, BK, s >> 2), 32 * w, s & 3, lane);
+    else return vf[s];
+  };
+  f32x16 dk[ND], dv[ND];
+#pragma unroll
+  for (int dh = 0; dh < ND; ++dh)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dk[dh][i] = dv[dh][i] = 0.f;
+
+  const int s_first = (kb * BK) / QS;
+  const int nslices = (T + QS - 1) / QS;
+  const int per_head = nslices - s_first;
+  const int total = G * per_head;
+
+  auto dma = [&](int it) {  // wave 0: Q slice + LSE rows, wave 1: dO slice + δ rows
+    const int hq = hk * G + it / per_head;
+    const int qs0 = (s_first + it % per_head) * QS;
+    const unsigned st = __builtin_amdgcn_readfirstlane(lds_addr_of(smem + (it & 1) * STAGE));
+    if (w == 0)
+      dma_rows<NP>(qkv + (size_t)b * T * RS + (size_t)hq * D, RS, qs0, T, st, lane);
+    else
+      dma_rows<NP>(dout + (size_t)b * T * ORS + (size_t)hq * D, ORS, qs0, T, st + TILE, lane);
+    const float* sp = (w == 0 ? lse : delta) + ((size_t)b * H + hq) * T + min(qs0 + lane, T - 1);
+    glds4(sp, st + 2 * TILE + 256 * w);
+  };
+
+  if (total > 0) dma(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int it = 0; it < total; ++it) {
+    if (it + 1 < total) dma(it + 1);  // the other stage, released by the previous barrier
+    const char* stg = smem + (it & 1) * STAGE;
+    const char* Qt = stg;
+    const char* Dt = stg + TILE;
+    const float* lse_s = reinterpret_cast<const float*>(stg + 2 * TILE);
+    const float* del_s = lse_s + 64;
+    const int hq = hk * G + it / per_head;
+    const int qs0 = (s_first + it % per_head) * QS;
+    if (qs0 + QS - 1 >= kw0 && kw0 < T && qs0 < T) {
+      f32x16 sp, dp;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4_t dl = *reinterpret_cast<const float4_t*>(&del_s[8 * g + 4 * hh]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          sp[4 * g + k] = 0.f;
+          dp[4 * g + k] = DROPOUT ? 0.f : -dl[k];
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        sp = mfma32(row_frag(panel(Qt, QS, s >> 2), 0, s & 3, lane), kfrag(s), sp);
+        dp = mfma32(row_frag(panel(Dt, QS, s >> 2), 0, s & 3, lane), vfrag(s), dp);
+        if (s & 1) d_fence<D>();
+      }
+      auto grads = [&](auto mask_tag) {
+        constexpr bool MASK = decltype(mask_tag)::value;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int r0 = 8 * g + 4 * hh;
+          const float4_t l2 = *reinterpret_cast<const float4_t*>(&lse_s[r0]) * kLog2e;
+          float4_t dl = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (DROPOUT) dl = *reinterpret_cast<const float4_t*>(&del_s[r0]);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int i = 4 * g + k;
+            const int q = qs0 + r0 + k;
+            float p = fexp2(fmaf(sp[i], c, -l2[k]));
+            if constexpr (MASK) p = (key > q || q >= T || key >= T) ? 0.f : p;
+            if constexpr (DROPOUT) {
+              const bool keep = dropout_keep(seed, b, hq, H, T, q, key, p_drop);
+              sp[i] = keep ? p * inv_keep : 0.f;
+              dp[i] = p * ((keep ? dp[i] * inv_keep : 0.f) - dl[k]);
+            } else {
+              sp[i] = p;
+              dp[i] = p * dp[i];
+            }
+          }
+        }
+      };
+      if (kw0 + 31 > qs0 || qs0 + QS > T || kw0 + 32 > T)
+        grads(std::true_type{});
+      else
+        grads(std::false_type{});
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const uint4 pf = acc_frag(sp, ss), sf = acc_frag(dp, ss);
+#pragma unroll
+        for (int dh = 0; dh < ND; ++dh) {
+          dv[dh] = mfma32(tr_frag(panel(Dt, QS, dh >> 1), 16 * ss, 32 * (dh & 1), lane), pf, dv[dh]);
+          dk[dh] = mfma32(tr_frag(panel(Qt, QS, dh >> 1), 16 * ss, 32 * (dh & 1), lane), sf, dk[dh]);
+          if (dh & 1) d_fence<D>();
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (key < T) {
+    bf16* dkrow = dqkv + ((size_t)b * T + key) * RS + (size_t)(H + hk) * D;
+    bf16* dvrow = dqkv + ((size_t)b * T + key) * RS + (size_t)(H + Hkv + hk) * D;
+#pragma unroll
+    for (int dh = 0; dh < ND; ++dh)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = 32 * dh + 8 * g + 4 * hh;
+        store4(dkrow + d, dk[dh][4 * g] * scale, dk[dh][4 * g + 1] * scale, dk[dh][4 * g + 2] * scale,
+               dk[dh][4 * g + 3] * scale);
+        store4(dvrow + d, dv[dh][4 * g], dv[dh][4 * g + 1], dv[dh][4 * g + 2], dv[dh][4 * g + 3]);
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// dQ: grid (ceil(T/64) query blocks, heaviest first, B*H); forward-shaped: a wave keeps 32
+// query rows' Q, dO, LSE, δ and dQᵀ in registers while sweeping 32-key K/V tiles.
+template <int D, bool DROPOUT>
+__global__ void __launch_bounds__(128, (D >= 256 ? 1 : 2))
+    fa_gen_bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
+                         const float* __restrict__ delta, bf16* __restrict__ dqkv, int T, int H, int Hkv, float scale,
+                         float p_drop, uint64_t seed) {
+  constexpr int NP = D / 64, NS = D / 16, ND = D / 32;
+  constexpr int BM = 64, BN = 32, TILE = BN * 128 * NP;
+  __shared__ __attribute__((aligned(16))) char smem[2][2][TILE];
+  const int nqb = (T + BM - 1) / BM;
+  int qi, bh;
+  xcd_head_block(qi, bh);
+  const int qb = nqb - 1 - qi;
+  const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
+  const int lane = threadIdx.x & 63, w = wave_id(), hh = lane >> 5;
+  const size_t RS = (size_t)(H + 2 * Hkv) * D;
+  const size_t ORS = (size_t)H * D;
+  const bf16* kbase = qkv + (size_t)b * T * RS + (size_t)(H + hk) * D;
+  const bf16* vbase = qkv + (size_t)b * T * RS + (size_t)(H + Hkv + hk) * D;
+  const int q0 = qb * BM + 32 * w;
+  const int qrow = q0 + (lane & 31);
+  const bool qok = qrow < T;
+  const float c = scale * kLog2e;
+  const float inv_keep = DROPOUT ? 1.f / (1.f - p_drop) : 1.f;
+
+  uint4 qf[NS], dof[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    qf[s] = qok ? *reinterpret_cast<const uint4*>(qkv + (size_t)b * T * RS + (size_t)h * D + (size_t)qrow * RS +
+                                                  16 * s + 8 * hh)
+                : zero4();
+    dof[s] = qok ? *reinterpret_cast<const uint4*>(dout + (size_t)b * T * ORS + (size_t)h * D + (size_t)qrow * ORS +
+                                                   16 * s + 8 * hh)
+                 : zero4();
+  }
+  const size_t rr = ((size_t)b * H + h) * T + qrow;
+  float l2 = qok ? lse[rr] * kLog2e : 0.f;
+  float dl = qok ? delta[rr] : 0.f;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    launder(qf[s]);
+    launder(dof[s]);
+  }
+  asm volatile("" : "+v"(l2), "+v"(dl));
+
+  const int kend = min(T, qb * BM + BM);
+  const int ntiles = (kend + BN - 1) / BN;
+  f32x16 dq[ND];
+#pragma unroll
+  for (int dh = 0; dh < ND; ++dh)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dq[dh][i] = 0.f;
+
+  auto dma = [&](int j) {  // wave 0: K tile, wave 1: V tile
+    const unsigned dst = __builtin_amdgcn_readfirstlane(lds_addr_of(smem[j & 1][w]));
+    dma_rows<NP>(w == 0 ? kbase : vbase, RS, j * BN, T, dst, lane);
+  };
+  dma(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int j = 0; j < ntiles; ++j) {
+    const int kt0 = j * BN;
+    if (j + 1 < ntiles) dma(j + 1);
+    const char* Kt = smem[j & 1][0];
+    const char* Vt = smem[j & 1][1];
+    if (kt0 <= q0 + 31 && q0 < T) {
+      f32x16 st, dp;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        st[i] = 0.f;
+        dp[i] = DROPOUT ? 0.f : -dl;
+      }
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        st = mfma32(row_frag(panel(Kt, BN, s >> 2), 0, s & 3, lane), qf[s], st);
+        dp = mfma32(row_frag(panel(Vt, BN, s >> 2), 0, s & 3, lane), dof[s], dp);
+        if (s & 1) d_fence<D>();
+      }
+      auto grads = [&](auto mask_tag) {
+        constexpr bool MASK = decltype(mask_tag)::value;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int k = kt0 + acc_row(i, lane);
+          float p = fexp2(fmaf(st[i], c, -l2));
+          if constexpr (MASK) p = (k > qrow || k >= T || !qok) ? 0.f : p;
+          if constexpr (DROPOUT) {
+            const bool keep = dropout_keep(seed, b, h, H, T, qrow, k, p_drop);
+            st[i] = p * ((keep ? dp[i] * inv_keep : 0.f) - dl);
+          } else {
+            st[i] = p * dp[i];
+          }
+        }
+      };
+      if (kt0 + BN - 1 > q0 || kt0 + BN > T || q0 + 32 > T)
+        grads(std::true_type{});
+      else
+        grads(std::false_type{});
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const uint4 sf = acc_frag(st, ss);
+#pragma unroll
+        for (int dh = 0; dh < ND; ++dh) {
+          dq[dh] = mfma32(tr_frag(panel(Kt, BN, dh >> 1), 16 * ss, 32 * (dh & 1), lane), sf, dq[dh]);
+          if (dh & 1) d_fence<D>();
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (qok) {
+    bf16* dqrow = dqkv + ((size_t)b * T + qrow) * RS + (size_t)h * D;
+#pragma unroll
+    for (int dh = 0; dh < ND; ++dh)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        store4(dqrow + 32 * dh + 8 * g + 4 * hh, dq[dh][4 * g] * scale, dq[dh][4 * g + 1] * scale,
+               dq[dh][4 * g + 2] * scale, dq[dh][4 * g + 3] * scale);
+  }
+}
+
+}  // namespace penroz
+
+// ============================================================================ host side
+using namespace penroz;
+
+#define FA_GEN_DISPATCH(D, DROP, ...)                                                         \
+  if ((D) == 128 && (DROP)) { constexpr int DD = 128; constexpr bool DR = true; __VA_ARGS__; }   \
+  else if ((D) == 128) { constexpr int DD = 128; constexpr bool DR = false; __VA_ARGS__; }       \
+  else if ((D) == 256 && (DROP)) { constexpr int DD = 256; constexpr bool DR = true; __VA_ARGS__; } \
+  else if ((D) == 256) { constexpr int DD = 256; constexpr bool DR = false; __VA_ARGS__; }       \
+  else TORCH_CHECK(false, "generic flash attention supports head_dim 128 and 256, got ", (D));
+
+void flash_attn_gen_fwd(torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int64_t H, int64_t Hkv, int64_t D,
+                        double scale, double p_drop, int64_t seed) {
+  TORCH_CHECK(qkv.is_cuda() && qkv.is_contiguous() && qkv.dim() == 3 && qkv.scalar_type() == torch::kBFloat16,
+              "qkv must be a contiguous bf16 [B, T, W] GPU tensor");
+  TORCH_CHECK(H > 0 && Hkv > 0 && H % Hkv == 0 && qkv.size(2) == (H + 2 * Hkv) * D, "qkv width must be (H+2Hkv)*D");
+  const int B = qkv.size(0), T = qkv.size(1);
+  TORCH_CHECK(out.is_contiguous() && out.scalar_type() == torch::kBFloat16 && out.numel() == (int64_t)B * T * H * D);
+  TORCH_CHECK(lse.is_contiguous() && lse.scalar_type() == torch::kFloat32 && lse.numel() == (int64_t)B * H * T);
+  if (B == 0 || T == 0) return;
+  auto stream = at::hip::getCurrentHIPStream();
+  const bf16* q = reinterpret_cast<const bf16*>(qkv.data_ptr());
+  bf16* o = reinterpret_cast<bf16*>(out.data_ptr());
+  FA_GEN_DISPATCH(D, p_drop > 0.0, {
+    constexpr int NW = fwd_waves<DD>();
+    dim3 g((T + 32 * NW - 1) / (32 * NW), B * H);
+    hipLaunchKernelGGL((fa_gen_fwd_kernel<DD, DR>), g, dim3(64 * NW), 0, stream, q, o, lse.data_ptr<float>(), T,
+                       (int)H, (int)Hkv, (float)scale, (float)p_drop, (uint64_t)seed);
+  })
+}
+
+void flash_attn_gen_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, torch::Tensor lse,
+                        torch::Tensor dqkv, int64_t H, int64_t Hkv, int64_t D, double scale, double p_drop,
+                        int64_t seed) {
+  TORCH_CHECK(qkv.is_cuda() && qkv.is_contiguous() && qkv.dim() == 3 && qkv.scalar_type() == torch::kBFloat16);
+  TORCH_CHECK(H > 0 && Hkv > 0 && H % Hkv == 0 && qkv.size(2) == (H + 2 * Hkv) * D, "qkv width must be (H+2Hkv)*D");
+  const int B = qkv.size(0), T = qkv.size(1);
+  TORCH_CHECK(dout.is_contiguous() && dout.scalar_type() == torch::kBFloat16 && dout.numel() == (int64_t)B * T * H * D);
+  TORCH_CHECK(out.is_contiguous() && out.numel() == dout.numel() && lse.numel() == (int64_t)B * H * T);
+  TORCH_CHECK(dqkv.is_contiguous() && dqkv.scalar_type() == torch::kBFloat16 && dqkv.numel() == qkv.numel());
+  if (B == 0 || T == 0) return;
+  auto delta = torch::empty({B, H, T}, qkv.options().dtype(torch::kFloat32));
+  auto stream = at::hip::getCurrentHIPStream();
+  const int rows = B * T * H;
+  const bf16* q = reinterpret_cast<const bf16*>(qkv.data_ptr());
+  const bf16* d = reinterpret_cast<const bf16*>(dout.data_ptr());
+  bf16* g = reinterpret_cast<bf16*>(dqkv.data_ptr());
+  dim3 gkv((T + 63) / 64, B * Hkv), gq((T + 63) / 64, B * H);
+  FA_GEN_DISPATCH(D, p_drop > 0.0, {
+    hipLaunchKernelGGL((fa_gen_bwd_pre_kernel<DD>), dim3(((int64_t)rows * (DD / 8) + 255) / 256), dim3(256), 0,
+                       stream, d, reinterpret_cast<const bf16*>(out.data_ptr()), delta.data_ptr<float>(), B, T,
+                       (int)H);
+    hipLaunchKernelGGL((fa_gen_bwd_dkdv_kernel<DD, DR>), gkv, dim3(128), 0, stream, q, d, lse.data_ptr<float>(),
+                       delta.data_ptr<float>(), g, T, (int)H, (int)Hkv, (float)scale, (float)p_drop,
+                       (uint64_t)seed);
+    hipLaunchKernelGGL((fa_gen_bwd_dq_kernel<DD, DR>), gq, dim3(128), 0, stream, q, d, lse.data_ptr<float>(),
+                       delta.data_ptr<float>(), g, T, (int)H, (int)Hkv, (float)scale, (float)p_drop, (uint64_t)seed);
+  })
+}

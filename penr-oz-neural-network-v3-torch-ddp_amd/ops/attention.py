@@ -1,6 +1,8 @@
 """Causal self-attention over a fused QKV tensor, and KV-cache (decode) attention.
 
-GPU: hand-written CDNA4 flash attention (``csrc/kernels/flash_attn.hip``):
+GPU: hand-written CDNA4 flash attention — ``csrc/kernels/flash_attn.hip`` (head_dim 64, GPT-2)
+and ``csrc/kernels/flash_attn_gen.hip`` (head_dim 128 / 256, Gemma; the same algebra over
+64-column LDS panels):
   * forward reads Q/K/V straight out of the fused ``[B, T, (H + 2·Hkv)·D]`` projection (no
     split/transpose copies), keeps Q in registers, stages K/V tiles through XOR-swizzled LDS,
     computes Sᵀ = K·Qᵀ with ``v_mfma_f32_32x32x16_bf16`` so each lane owns one query row's
@@ -8,7 +10,8 @@ GPU: hand-written CDNA4 flash attention (``csrc/kernels/flash_attn.hip``):
     accumulators into Oᵀ = Vᵀ·Pᵀ (V read with ``ds_read_b64_tr_b16``), and writes O already
     head-merged ``[B, T, H·D]`` plus the row log-sum-exp;
   * backward keeps each wave's 32 keys (K, V, dKᵀ, dVᵀ) in registers while sweeping the query
-    blocks; dQ is accumulated with fp32 atomics and converted once.
+    slices of every query head of its KV group; a second, forward-shaped kernel keeps 32 query
+    rows (Q, dO, dQᵀ) in registers while sweeping the key tiles — deterministic, no atomics.
   GQA is handled by index math (kv head = q head // group) — K/V are never expanded.
   Dropout (``attn_pdrop``) uses a counter-based hash RNG regenerated in the backward pass.
 CPU: ``torch.nn.functional.scaled_dot_product_attention`` (math) with GQA expansion.
@@ -25,10 +28,10 @@ import torch.nn.functional as F
 
 from penroz.ops._ext import use_kernels, kernels
 
-# head dims with a native kernel: prefill / training flash attention (csrc/kernels/flash_attn.hip)
-# and decode attention (csrc/kernels/decode_attn.hip). Other head dims (e.g. Gemma's 256) run
-# torch SDPA on the GPU.
-SUPPORTED_HEAD_DIMS = (64,)
+# head dims with a native kernel: prefill / training flash attention (flash_attn.hip: 64;
+# flash_attn_gen.hip: 128, 256) and decode attention (csrc/kernels/decode_attn.hip). Other head
+# dims run torch SDPA on the GPU.
+SUPPORTED_HEAD_DIMS = (64, 128, 256)
 DECODE_HEAD_DIMS = (64, 128, 256)
 
 
@@ -68,7 +71,8 @@ def flash_fwd(qkv: Tensor, H: int, Hkv: int, D: int, dropout_p: float = 0.0, see
     B, T, _ = qkv.shape
     out = torch.empty(B, T, H * D, dtype=torch.bfloat16, device=qkv.device) if out is None else out
     lse = torch.empty(B, H, T, dtype=torch.float32, device=qkv.device) if lse is None else lse
-    kernels().flash_attn_fwd(qkv, out, lse, H, Hkv, D, 1.0 / math.sqrt(D), float(dropout_p), int(seed))
+    fn = kernels().flash_attn_fwd if D == 64 else kernels().flash_attn_gen_fwd
+    fn(qkv, out, lse, H, Hkv, D, 1.0 / math.sqrt(D), float(dropout_p), int(seed))
     return out, lse
 
 
@@ -76,7 +80,8 @@ def flash_bwd(dout: Tensor, qkv: Tensor, out: Tensor, lse: Tensor, H: int, Hkv: 
               dropout_p: float = 0.0, seed: int = 0, dqkv: Tensor | None = None) -> Tensor:
     """-> dqkv bf16 [B,T,(H+2Hkv)D] (written into ``dqkv`` when given)."""
     dqkv = torch.empty_like(qkv) if dqkv is None else dqkv
-    kernels().flash_attn_bwd(dout, qkv, out, lse, dqkv, H, Hkv, D, 1.0 / math.sqrt(D), float(dropout_p), int(seed))
+    fn = kernels().flash_attn_bwd if D == 64 else kernels().flash_attn_gen_bwd
+    fn(dout, qkv, out, lse, dqkv, H, Hkv, D, 1.0 / math.sqrt(D), float(dropout_p), int(seed))
     return dqkv
 
 
