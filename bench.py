@@ -129,8 +129,9 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def launch_ranks(args, argv: list[str], poll_s: float = 0.2) -> int:
-    """Spawn ``args.gpus`` child ranks of this script and supervise them (parent: no GPU use)."""
+def launch_ranks(args, argv: list[str], poll_s: float = 0.2, script: str | None = None) -> int:
+    """Spawn ``args.gpus`` child ranks of ``script`` (default: this file) and supervise them
+    (parent: no GPU use)."""
     n = args.gpus
     if args.device == "cuda":
         visible = torch.cuda.device_count()  # does not initialise HIP on this image
@@ -148,7 +149,7 @@ def launch_ranks(args, argv: list[str], poll_s: float = 0.2) -> int:
                     "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
         if args.device == "cpu":
             env.setdefault("OMP_NUM_THREADS", str(threads))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + argv, env=env))
     rc = 0
     try:
         live = list(procs)

@@ -4,8 +4,10 @@
 // through the torch.distributed TCPStore, and a dedicated high-priority non-blocking HIP
 // stream. all_reduce_avg_async() fences the comm stream behind the producer's current stream
 // with an event (so a bucket's all-reduce starts as soon as the kernels that wrote it finish,
-// while the compute stream runs on) and launches ncclAllReduce(ncclAvg) in place; wait_all()
-// makes the compute stream wait for everything launched so far (before the optimizer step).
+// while the compute stream runs on) and launches ncclAllReduce(ncclAvg) in place, then records a
+// completion event and returns its handle: wait(handle) makes the compute stream wait for that
+// one collective (the optimizer updates bucket i as soon as bucket i has landed), wait_all()
+// for everything launched so far.
 // This replaces the reference's implicit C++ DDP Reducer + ProcessGroupNCCL
 // (``neural_net_model.py:609``) with an explicit, bucket-granular, stream-ordered design.
 #include <torch/extension.h>
@@ -56,6 +58,7 @@ class RcclComm {
   ~RcclComm() {
     if (comm_) ncclCommDestroy(comm_);
     for (auto e : events_) hipEventDestroy(e);
+    for (auto e : done_) hipEventDestroy(e);
     if (stream_) hipStreamDestroy(stream_);
   }
 
@@ -65,20 +68,32 @@ class RcclComm {
     return std::string(reinterpret_cast<const char*>(&id), sizeof(id));
   }
 
-  // in-place average of `t` across ranks, ordered after the current torch stream's work
-  void all_reduce_avg_async(torch::Tensor t) {
+  // in-place average of `t` across ranks, ordered after the current torch stream's work;
+  // returns the handle of its completion event (valid until wait_all() / reset_handles())
+  int64_t all_reduce_avg_async(torch::Tensor t) {
     TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "RCCL all-reduce needs a contiguous GPU tensor");
     fence_from_current();
     NCCL_OK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), ncclAvg, comm_, stream_));
     ++pending_;
+    return record_done();
   }
 
-  void all_reduce_sum_async(torch::Tensor t) {
+  int64_t all_reduce_sum_async(torch::Tensor t) {
     TORCH_CHECK(t.is_cuda() && t.is_contiguous());
     fence_from_current();
     NCCL_OK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), ncclSum, comm_, stream_));
     ++pending_;
+    return record_done();
   }
+
+  // the current torch stream waits for the collective with this handle only
+  void wait(int64_t handle) {
+    TORCH_CHECK(handle >= 0 && handle < n_done_, "unknown collective handle ", handle);
+    HIP_OK(hipStreamWaitEvent(at::hip::getCurrentHIPStream().stream(), done_[handle], 0));
+  }
+
+  // forget the handles (their events are re-recorded by later collectives)
+  void reset_handles() { n_done_ = 0; }
 
   void broadcast(torch::Tensor t, int root) {
     TORCH_CHECK(t.is_cuda() && t.is_contiguous());
@@ -95,6 +110,7 @@ class RcclComm {
     HIP_OK(hipEventRecord(e, stream_));
     HIP_OK(hipStreamWaitEvent(at::hip::getCurrentHIPStream().stream(), e, 0));
     pending_ = 0;
+    n_done_ = 0;
   }
 
   void synchronize() { HIP_OK(hipStreamSynchronize(stream_)); }
@@ -106,6 +122,17 @@ class RcclComm {
     hipEvent_t e = next_event();
     HIP_OK(hipEventRecord(e, at::hip::getCurrentHIPStream().stream()));
     HIP_OK(hipStreamWaitEvent(stream_, e, 0));
+  }
+
+  // one completion event per collective since the last reset (a bucket plan has tens)
+  int64_t record_done() {
+    if (n_done_ == (int64_t)done_.size()) {
+      hipEvent_t e;
+      HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      done_.push_back(e);
+    }
+    HIP_OK(hipEventRecord(done_[n_done_], stream_));
+    return n_done_++;
   }
 
   hipEvent_t next_event() {
@@ -124,6 +151,8 @@ class RcclComm {
   ncclComm_t comm_ = nullptr;
   hipStream_t stream_ = nullptr;
   std::vector<hipEvent_t> events_;
+  std::vector<hipEvent_t> done_;
+  int64_t n_done_ = 0;
   size_t ring_ = 0;
   int pending_ = 0;
 };
@@ -136,6 +165,8 @@ PYBIND11_MODULE(penroz_comm, m) {
       .def("all_reduce_avg_async", &RcclComm::all_reduce_avg_async)
       .def("all_reduce_sum_async", &RcclComm::all_reduce_sum_async)
       .def("broadcast", &RcclComm::broadcast)
+      .def("wait", &RcclComm::wait)
+      .def("reset_handles", &RcclComm::reset_handles)
       .def("wait_all", &RcclComm::wait_all)
       .def("synchronize", &RcclComm::synchronize)
       .def_property_readonly("rank", &RcclComm::rank)

@@ -43,8 +43,16 @@ class NativeComm:
             cls._instances[k] = NativeComm(group)
         return cls._instances[k]
 
-    def all_reduce_avg_async(self, t: torch.Tensor):
-        self.comm.all_reduce_avg_async(t)
+    def all_reduce_avg_async(self, t: torch.Tensor) -> int:
+        """Launch; returns the handle :meth:`wait` takes."""
+        return self.comm.all_reduce_avg_async(t)
+
+    def wait(self, handle: int):
+        """The current stream waits for that one collective."""
+        self.comm.wait(handle)
+
+    def reset_handles(self):
+        self.comm.reset_handles()
 
     def wait_all(self):
         self.comm.wait_all()

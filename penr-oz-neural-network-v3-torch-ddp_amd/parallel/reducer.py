@@ -100,7 +100,7 @@ class GradReducer:
             view = self._wire[s:e]
         self._launched[i] = True
         if self._native is not None:
-            self._native.all_reduce_avg_async(view)
+            self._works.append(("native", self._native.all_reduce_avg_async(view)))
         elif self.backend == "nccl":
             self._works.append(dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.group, async_op=True))
         else:
@@ -113,14 +113,17 @@ class GradReducer:
                 self.bucket_ready(i)
 
     def per_bucket_waits(self) -> bool:
-        """True when :meth:`wait_bucket` can wait for one bucket at a time (c10d transport)."""
-        return self._native is None and len(self._works) == len(self.buckets)
+        """True when :meth:`wait_bucket` can wait for one bucket at a time (every bucket launched,
+        in bucket order; c10d work objects or native RCCL completion events)."""
+        return len(self._works) == len(self.buckets)
 
     def wait_bucket(self, i: int) -> tuple[int, int]:
         """Current stream waits for bucket ``i``'s all-reduce (launch order = bucket order);
         returns its element range, now holding the averaged gradient."""
         w = self._works[i]
-        if isinstance(w, tuple):
+        if isinstance(w, tuple) and w[0] == "native":
+            self._native.wait(w[1])
+        elif isinstance(w, tuple):
             w[0].wait()
             w[1].div_(self.world)
         else:
@@ -133,6 +136,8 @@ class GradReducer:
     def reset(self):
         self._works.clear()
         self._launched = [False] * len(self.buckets)
+        if self._native is not None:
+            self._native.reset_handles()
 
     def finish(self):
         """Launch any bucket not yet launched, then wait for all of them."""
@@ -142,6 +147,8 @@ class GradReducer:
         if self._native is not None:
             self._native.wait_all()
         for w in self._works:
+            if isinstance(w, tuple) and w[0] == "native":
+                continue
             if isinstance(w, tuple):
                 w[0].wait()
                 w[1].div_(self.world)

@@ -216,3 +216,40 @@ def test_fault_injection_disabled_by_default(clean_env):
     with mock.patch.object(LA.os, "_exit") as ex:
         LA.maybe_inject_fault(0)
         ex.assert_not_called()
+
+
+def test_bucket_plan_gpt2_xl_gradients():
+    """6.55 GB of XL fp32 gradients: contiguous buckets covering every element once, each at
+    least the target (except the tail) and never splitting a layer."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench"))
+    import allreduce_bench as ab
+    from penroz.parallel.reducer import plan_buckets
+    segs = ab.gpt2_segments(1600, 48)
+    total = segs[-1][1]
+    assert abs(total * 4 / 1e9 - 6.55) < 0.05
+    for mb in (25, 64, 128, 256):
+        b = plan_buckets(segs, mb * 2**20)
+        assert b[0][0] == 0 and b[-1][1] == total
+        assert all(b[i][1] == b[i + 1][0] for i in range(len(b) - 1))
+        bounds = {s for s, _ in segs} | {total}
+        assert all(s in bounds and e in bounds for s, e in b)  # layer boundaries only
+        assert all((e - s) * 4 >= mb * 2**20 for s, e in b[:-1])
+    plan = ab.plan_summary(64)
+    assert plan["gpt2-xl"]["buckets"] < plan["gpt2-xl"]["grad_mb"] / 64 + 2
+
+
+@pytest.mark.slow
+def test_allreduce_bench_cpu_rehearsal():
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench", "allreduce_bench.py"), "--gpus", "2", "--device", "cpu",
+                        "--sizes-mb", "1", "--wires", "fp32,bf16", "--iters", "2", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 3 and lines[-1]["summary"] and lines[-1]["n_ranks"] == 2
+    assert {l["wire"] for l in lines[:2]} == {"fp32", "bf16"} and lines[1]["wire_mb"] == 0.5

@@ -115,6 +115,18 @@ def test_native_rccl_world_size_one():
         torch.cuda.synchronize()
         assert torch.equal(t, torch.arange(1024, device="cuda", dtype=torch.float32))
         c.broadcast(t, 0)
+        # per-collective completion handles: the optimizer waits bucket by bucket
+        bufs = [torch.full((n,), float(i), device="cuda") for i, n in enumerate((4096, 1 << 20, 333))]
+        hs = [c.all_reduce_avg_async(b) for b in bufs]
+        assert hs == [0, 1, 2]
+        for h, b in zip(hs, bufs):
+            c.wait(h)
+            b.add_(1)  # ordered after that bucket's collective on the current stream
+        torch.cuda.synchronize()
+        assert all(torch.all(b == i + 1) for i, b in enumerate(bufs))
+        c.reset_handles()
+        assert c.all_reduce_avg_async(bufs[0]) == 0
+        c.wait_all()
     finally:
         dist.destroy_process_group()
 
