@@ -173,6 +173,8 @@ class GPTExecutor:
         if spec is None:
             raise ValueError("model does not match the GPT-2 pattern")
         _ext.kernels()  # hard requirement on GPU
+        if device.type == "cuda":
+            gemm_ops.load_tuned_gemms()
         self.model = model
         self.spec = spec
         self.device = device
