@@ -52,9 +52,27 @@ __device__ __forceinline__ uint4 acc_frag(const f32x16& a, int ss) {
 
 __device__ __forceinline__ int acc_row(int i, int lane) { return (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5); }
 
+// Attention-dropout mask, regenerated identically by every forward / backward kernel.
+// Element (q, k) of head row-block bh (= b·H + h) is kept iff the 16-bit half (k & 1) of
+// H = fmix32(rowkey(seed, bh·T + q) ^ (k >> 1)·0x85EBCA6B) is ≥ p·65536 (p quantised to 2⁻¹⁶).
+// 32-bit arithmetic only (two v_mul_lo_u32 per hash) and one hash per key PAIR: the
+// kernels that hold consecutive keys of one query row in consecutive registers (forward, dQ)
+// get both halves from one hash; the dK/dV kernel (key on the lane) pays one per element.
+__device__ __forceinline__ uint32_t fmix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x85EBCA6Bu;
+  x ^= x >> 13;
+  x *= 0xC2B2AE35u;
+  x ^= x >> 16;
+  return x;
+}
+
 __device__ __forceinline__ bool dropout_keep(uint64_t seed, int b, int h, int H, int T, int q, int k, float p) {
-  const uint64_t ctr = (((uint64_t)b * H + h) * (uint64_t)T + (uint64_t)q) * (uint64_t)T + (uint64_t)k;
-  return uniform01(seed, ctr) >= p;
+  const uint32_t row = (uint32_t)((b * H + h) * T + q);
+  const uint32_t rowkey = ((uint32_t)seed ^ ((uint32_t)(seed >> 32) * 0x27D4EB2Fu)) ^ (row * 0x9E3779B1u);
+  const uint32_t hsh = fmix32(rowkey ^ ((uint32_t)(k >> 1) * 0x85EBCA6Bu));
+  const uint32_t u16 = (k & 1) ? (hsh >> 16) : (hsh & 0xFFFFu);
+  return u16 >= (uint32_t)(p * 65536.f);
 }
 
 __device__ __forceinline__ uint4 zero4() { return uint4{0u, 0u, 0u, 0u}; }

@@ -201,7 +201,7 @@ __global__ void __launch_bounds__(256, 2) fa_fwd_kernel(const bf16* __restrict__
 // and used by both blocks, halving LDS traffic per MFMA, and the two blocks' dependency
 // chains interleave: S_B's MFMAs run under softmax_A, P_A·V's under softmax_B. Query blocks
 // of 64 rows are aligned to key tiles, so a wave's only masked tile is its diagonal one.
-template <bool DROPOUT>
+template <bool DROPOUT>  // instantiated without dropout only (see flash_attn_fwd)
 __global__ void __launch_bounds__(128, 2) fa_fwd3_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
                                                       float* __restrict__ lse, int T, int H, int Hkv, float scale,
                                                       float p_drop, uint64_t seed) {
@@ -1145,8 +1145,8 @@ void flash_attn_fwd(torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int
   auto stream = at::hip::getCurrentHIPStream();
   const bf16* q = reinterpret_cast<const bf16*>(qkv.data_ptr());
   bf16* o = reinterpret_cast<bf16*>(out.data_ptr());
-  // dropout always takes the single-stage kernel (the pipelined one would spill with the
-  // mask hashing live across the tile loop)
+  // dropout takes the single-stage kernel: the two-block kernel spills with the mask hashing of
+  // both query blocks live (159 VGPRs to scratch)
   if (p_drop > 0.0)
     hipLaunchKernelGGL(fa_fwd_kernel<true>, grid, dim3(256), 0, stream, q, o, lse.data_ptr<float>(), T, (int)H,
                        (int)Hkv, (float)scale, (float)p_drop, (uint64_t)seed);
@@ -1191,10 +1191,15 @@ void flash_attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, to
   const bf16* d = reinterpret_cast<const bf16*>(dout.data_ptr());
   bf16* g = reinterpret_cast<bf16*>(dqkv.data_ptr());
   dim3 gkv((T + 127) / 128, B * Hkv), gq((T + 127) / 128, B * H);
-  if (p_drop > 0.0) {
+  if (p_drop > 0.0 && g_fa_bwd_variant == 1) {
     hipLaunchKernelGGL(fa_bwd_dkdv_kernel<true>, gkv, dim3(256), 0, stream, q, d, lse.data_ptr<float>(),
                        delta.data_ptr<float>(), g, T, (int)H, (int)Hkv, (float)scale, (float)p_drop, (uint64_t)seed);
     hipLaunchKernelGGL(fa_bwd_dq_kernel<true>, gq, dim3(256), 0, stream, q, d, lse.data_ptr<float>(),
+                       delta.data_ptr<float>(), g, T, (int)H, (int)Hkv, (float)scale, (float)p_drop, (uint64_t)seed);
+  } else if (p_drop > 0.0) {
+    hipLaunchKernelGGL(fa_bwd_dkdv2_kernel<true>, gkv, dim3(256), 0, stream, q, d, lse.data_ptr<float>(),
+                       delta.data_ptr<float>(), g, T, (int)H, (int)Hkv, (float)scale, (float)p_drop, (uint64_t)seed);
+    hipLaunchKernelGGL(fa_bwd_dq3_kernel<true>, gq, dim3(256), 0, stream, q, d, lse.data_ptr<float>(),
                        delta.data_ptr<float>(), g, T, (int)H, (int)Hkv, (float)scale, (float)p_drop, (uint64_t)seed);
   } else {
     if (g_fa_bwd_variant == 1)
