@@ -571,8 +571,16 @@ void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad, int64_t t
   TORCH_CHECK(dy.stride(1) == 1 && x.stride(1) == 1 && grad.is_contiguous());
   const int K = dy.size(0), M = dy.size(1), N = x.size(1);
   TORCH_CHECK(grad.size(0) == M && grad.size(1) == N, "wgrad: gradient shape mismatch");
-  TORCH_CHECK(M % 8 == 0 && N % 8 == 0 && dy.stride(0) % 8 == 0 && x.stride(0) % 8 == 0,
-              "wgrad: widths and row strides must be multiples of 8");
+  // the kernels load 8-column (16-B) chunks: a width that is not a multiple of 8 is fine when
+  // the rows are padded (row stride >= the width rounded up to 8, e.g. the executor's logits
+  // rows for V = 50257), the tail chunk then reads pad columns of the same row (their products
+  // only reach output rows >= M, which are never stored)
+  const int Mp = (M + 7) & ~7;
+  TORCH_CHECK(N % 8 == 0 && dy.stride(0) % 8 == 0 && x.stride(0) % 8 == 0 && (M % 8 == 0 || dy.stride(0) >= Mp),
+              "wgrad: N and row strides must be multiples of 8, and M too unless dy's rows are padded to it");
+  TORCH_CHECK(M % 8 == 0 || dy.storage().nbytes() >= (size_t)(dy.storage_offset() + (int64_t)(K - 1) * dy.stride(0) +
+                                                             Mp) * 2,
+              "wgrad: dy's last row padding must be allocated");
   TORCH_CHECK(tile == 128 || tile == 256, "wgrad: tile must be 128 or 256");
   if (K == 0) return;
   const int T = (int)tile;

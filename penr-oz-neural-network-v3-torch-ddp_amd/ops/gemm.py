@@ -22,8 +22,9 @@ from penroz.ops._ext import use_kernels, kernels
 NATIVE_WGRAD = os.environ.get("PENROZ_NATIVE_WGRAD", "auto")
 
 
-def _native_ok(m: int, n: int) -> bool:
-    return NATIVE_WGRAD != "0" and m % 8 == 0 and n % 8 == 0
+def _native_ok(m: int, n: int, lda: int | None = None) -> bool:
+    """m need not be a multiple of 8 when dy's rows are padded to it (lda >= round_up(m, 8))."""
+    return NATIVE_WGRAD != "0" and n % 8 == 0 and (m % 8 == 0 or (lda is not None and lda >= (m + 7) // 8 * 8))
 
 
 def reference_wgrad(dy: Tensor, x: Tensor, grad: Tensor) -> None:
@@ -31,7 +32,7 @@ def reference_wgrad(dy: Tensor, x: Tensor, grad: Tensor) -> None:
 
 
 def wgrad(dy: Tensor, x: Tensor, grad: Tensor) -> None:
-    if (use_kernels(dy) and _native_ok(dy.shape[1], x.shape[1]) and dy.dtype == torch.bfloat16
+    if (use_kernels(dy) and _native_ok(dy.shape[1], x.shape[1], dy.stride(0)) and dy.dtype == torch.bfloat16
             and x.dtype == torch.bfloat16 and dy.stride(0) % 8 == 0 and x.stride(0) % 8 == 0):
         kernels().wgrad_gemm(dy, x, grad)
     elif dy.is_cuda:

@@ -757,3 +757,24 @@ def test_embedding_dropout():
     (Fu.reference_embedding_fwd(idx, w1, w2, 3) * m * dout).sum().backward()
     _close(dwte, w1.grad, 1e-4)
     _close(dwpe, w2.grad, 1e-4)
+
+
+@pytest.mark.parametrize("tile,variant", [(128, 0), (256, 4)])
+@pytest.mark.parametrize("M", [50257, 1001])
+def test_wgrad_gemm_padded_rows(M, tile, variant):
+    """HF GPT-2 vocab (V = 50257): dlogits rows padded to a multiple of 8 (zero pad columns, as the
+    CE kernel leaves them); only the first M gradient rows are touched."""
+    torch.manual_seed(0)
+    K, N = 2048, 768
+    Mp = (M + 7) // 8 * 8
+    buf = torch.zeros(K, Mp, device=DEV, dtype=torch.bfloat16)
+    dy = buf[:, :M]
+    dy.copy_(torch.randn(K, M, device=DEV).to(torch.bfloat16))
+    x = torch.randn(K, N, device=DEV).to(torch.bfloat16)
+    flat = torch.randn(M * N + 4096, device=DEV)
+    grad = flat[:M * N].view(M, N)
+    tail = flat[M * N:].clone()
+    ref = grad + dy.float().t() @ x.float()
+    _ext.kernels().wgrad_gemm(dy, x, grad, tile, variant)
+    assert (grad - ref).norm() / ref.norm() < 1e-4
+    assert torch.equal(flat[M * N:], tail), "wrote past the gradient's M rows"
