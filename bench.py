@@ -108,6 +108,9 @@ def parse_args(argv=None):
                          "(1 GPU, gpt2-124m only; 0 = skip)")
     ap.add_argument("--nocomm-steps", type=int, default=4,
                     help="steps without the gradient all-reduce, for allreduce_exposed_ms (world > 1; 0 = skip)")
+    ap.add_argument("--via-runtime", action="store_true",
+                    help="also time the same config through NeuralNetworkModel.train_model (Loader over synthetic "
+                         "shards, per-epoch diagnostics, checkpoints) and report its tokensPerSec progress figure")
     ap.add_argument("--profile", default=None, metavar="DIR",
                     help="after the timed steps, profile 3 more under torch.profiler into DIR "
                          "(Chrome trace + per-kernel table); set PENROZ_ROCTX=1 for roctx phase ranges")
@@ -272,6 +275,56 @@ def _reference_eager_tok_s(args, cfg, device, pool) -> float | None:
         torch.cuda.empty_cache()
 
 
+def _via_runtime(args, cfg, device, world, rank) -> dict:
+    """``PUT /train/``'s worker path (``train_model``) on the same config: synthetic token shards on
+    disk, the rank-strided Loader, per-epoch weight-update ratios and cost sync, checkpoints in a
+    scratch directory. Returns the mean ``tokensPerSec`` of the timed epochs (the last epoch, which
+    also captures stats, is excluded) — the runtime's own throughput figure."""
+    import tempfile
+    import numpy as np
+    from penroz.models import model as model_mod
+    from penroz.models.mapper import Mapper
+    from penroz.models.model import NeuralNetworkModel
+    from penroz.utils import checkpoint as ckpt
+    from penroz.utils import loaders
+    B, T = args.batch, args.seq
+    epochs = args.warmup + args.steps + 1
+    tmp = tempfile.mkdtemp(prefix="penroz_runtime_bench_")
+    saved = (loaders.DATA_FOLDER, NeuralNetworkModel.SHM_PATH, model_mod.MODELS_FOLDER)
+    loaders.DATA_FOLDER = os.path.join(tmp, "data")
+    NeuralNetworkModel.SHM_PATH = os.path.join(tmp, "shm")
+    model_mod.MODELS_FOLDER = os.path.join(tmp, "models")
+    try:
+        if rank == 0:
+            rng = np.random.default_rng(0)
+            loaders.save_shard("bench", 0, rng.integers(0, cfg["V"], epochs * B * T * world + 1), cfg["V"])
+        if world > 1:
+            dist.barrier()
+        torch.manual_seed(1234)
+        dims = {k: cfg[k] for k in ("V", "C", "L", "H", "P")}
+        layers = hf_gpt2_layers(**dims) if cfg.get("hf") else gpt2_layers(**dims)
+        m = NeuralNetworkModel("bench", Mapper(layers, {"adamw": {"lr": 6e-4, "betas": [0.9, 0.95], "eps": 1e-8}}))
+        m.to(device)
+        if cfg.get("hf"):
+            m.to(dtype=torch.bfloat16)
+        os.environ["PENROZ_ENGINE"] = args.engine
+        m.train_model("bench", 0, epochs, B, T, B)
+        prog = m.progress[args.warmup:epochs - 1]
+        tps = [p["tokensPerSec"] for p in prog]
+        out = {"epochs_timed": len(tps), "tokensPerSec_mean": sum(tps) / len(tps) if tps else None,
+               "tokensPerSec_median": sorted(tps)[len(tps) // 2] if tps else None,
+               "speedPerSec_mean": sum(p["speedPerSec"] for p in prog) / len(prog) if prog else None}
+        del m
+        torch.cuda.empty_cache() if device.type == "cuda" else None
+        return out
+    finally:
+        ckpt.wait_flushes()
+        loaders.DATA_FOLDER, NeuralNetworkModel.SHM_PATH, model_mod.MODELS_FOLDER = saved
+        if rank == 0:
+            import shutil
+            shutil.rmtree(tmp, ignore_errors=True)
+
+
 def run_rank(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -327,14 +380,27 @@ def run_rank(args):
             print(table, file=sys.stderr)
 
     n_params = sum(p.numel() for p in model.parameters())
+    runtime = None
+    if args.via_runtime:
+        ex = getattr(runner, "exec", None)
+        if ex is not None:
+            ex.end_training()
+            ex.free_buffers()
+        del runner, model
+        if device.type == "cuda":
+            torch.cuda.empty_cache()
+        runtime = _via_runtime(args, cfg, device, world, rank)
+        if runtime.get("tokensPerSec_mean"):
+            runtime["ratio_vs_executor"] = runtime["tokensPerSec_mean"] / tok_s
     ref_tok_s = None
     if (world == 1 and device.type == "cuda" and args.engine == "fused" and args.ref_steps > 0
             and args.model == "gpt2-124m"):
-        ex = getattr(runner, "exec", None)
-        if ex is not None:
-            ex.free_buffers()
-        del runner, model
-        torch.cuda.empty_cache()
+        if not args.via_runtime:
+            ex = getattr(runner, "exec", None)
+            if ex is not None:
+                ex.free_buffers()
+            del runner, model
+            torch.cuda.empty_cache()
         ref_tok_s = _reference_eager_tok_s(args, cfg, device, pool)
 
     if rank == 0:
@@ -350,6 +416,7 @@ def run_rank(args):
             "dtype": "bf16" if device.type == "cuda" else "fp32",
             "data": "synthetic uniform tokens, random-init weights",
             "comm": comm,
+            **({"via_runtime": runtime} if runtime is not None else {}),
             "config": {"model": args.model, "global_batch": world * B, "seq_len": T, "micro_batch_per_gpu": B,
                        "tokens_per_step": world * B * T, "parallelism": f"dp{world}"},
         }), flush=True)
