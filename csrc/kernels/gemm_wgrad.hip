@@ -20,6 +20,7 @@
 // wgrad_kernel (128×128, 4 waves, register staging) and wgrad256_kernel (double-buffered)
 // are kept as selectable variants for A/B measurement.
 #include "common.h"
+#include "host_plan.h"
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 
@@ -586,28 +587,14 @@ void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad, int64_t t
   const int T = (int)tile;
   const int tiles_m = (M + T - 1) / T, tiles_n = (N + T - 1) / T;
   const int ntiles = tiles_m * tiles_n;
-  // Split-K count from a wave-quantisation cost model: the launch runs ceil(ntiles·s / slots)
-  // waves of workgroups, each 1/s of the K loop long, plus the slab round trip (s slabs written
-  // and read once) priced against the per-workgroup MFMA time. slots = resident workgroups:
-  // 1 (256-tile, 128 KiB LDS) or 2 (128-tile) per CU.
   static int n_cu = 0;
   if (n_cu == 0) {
     hipDeviceProp_t prop;
     n_cu = hipGetDeviceProperties(&prop, grad.get_device()) == hipSuccess ? prop.multiProcessorCount : 256;
   }
-  const int slots = T == 256 ? n_cu : 2 * n_cu;
-  const double wg_full_k = (double)T * T * 2.0 * K / (T == 256 ? 2.3e12 : 1.1e12);  // seconds, one workgroup
-  int splits = 1;
-  double best = 1e30;
-  for (int s = 1; s <= std::max(1, K / 512) && s <= 64; ++s) {
-    const double waves = (double)((ntiles * (int64_t)s + slots - 1) / slots);
-    const double slab = s > 1 ? (double)s * M * N * 8.0 / 4.0e12 : 0.0;
-    const double cost = waves * wg_full_k / s + slab;
-    if (cost < best * 0.995) best = cost, splits = s;
-  }
-  const int bk = T == 256 ? BK2 : BK;
-  int klen = ((K + splits - 1) / splits + bk - 1) / bk * bk;
-  splits = (K + klen - 1) / klen;
+  // split-K from the wave-quantisation cost model (host_plan.h, sanitizer-tested on the host)
+  const SplitK plan = plan_wgrad_splits(M, N, K, T, n_cu, T == 256 ? BK2 : BK);
+  const int splits = plan.splits, klen = plan.klen;
   auto stream = at::hip::getCurrentHIPStream();
   const int nwg = ntiles * splits;
   const bf16* a = reinterpret_cast<const bf16*>(dy.data_ptr());

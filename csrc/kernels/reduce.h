@@ -6,6 +6,7 @@
 // S slice sums in slice order. Fixed summation order => bitwise reproducible.
 #pragma once
 #include <hip/hip_runtime.h>
+#include "host_plan.h"
 
 namespace penroz {
 namespace {  // internal linkage: every including translation unit gets its own copy
@@ -44,12 +45,6 @@ inline void reduce_partials_add(const float* part, int A, int G, int C, float* c
   dim3 g1((C + 255) / 256, S, A), g2((C + 255) / 256, A);
   hipLaunchKernelGGL(reduce_stage1_kernel, g1, dim3(256), 0, stream, part, G, C, S, mid);
   hipLaunchKernelGGL(reduce_stage2_kernel, g2, dim3(256), 0, stream, mid, C, S, o);
-}
-
-inline int reduce_slices(int G) {
-  int s = 1;
-  while (s * s < G) ++s;  // ~sqrt(G): balances the two stages
-  return s;
 }
 
 }  // namespace
