@@ -251,6 +251,22 @@ __global__ void __launch_bounds__(128, 2) fa_fwd3_kernel(const bf16* __restrict_
     const int ch = (lane & 7) ^ ((((row >> 1) & 1) << 2) | ((row >> 2) & 3));
     v_voff[par] = (unsigned)(lane >> 3) * RSB + 16u * ch;
   }
+  // per-lane byte offsets of the two transposed reads of a V fragment (tile_off is periodic in
+  // 16 rows, so the key offset 32kh + 16ss becomes an immediate)
+  unsigned vto[2][2];
+#pragma unroll
+  for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int col = 32 * dh + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+      vto[dh][jj] = (unsigned)(tile_off(4 * hh + ((lane & 15) >> 2) + 8 * jj, col >> 3) + ((col & 4) << 1));
+    }
+  auto vfrag = [&](const char* t, int dh) -> uint4 {
+    const s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(t + vto[dh][0]));
+    const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(t + vto[dh][1]));
+    const uint2 ux = __builtin_bit_cast(uint2, x), uy = __builtin_bit_cast(uint2, y);
+    return uint4{ux.x, ux.y, uy.x, uy.y};
+  };
   auto dma = [&](int kt0, int buf) {
     const unsigned dst = __builtin_amdgcn_readfirstlane(lds_addr_of(smem[buf][w]));
     if (kt0 + BN <= T) {
@@ -361,7 +377,7 @@ __global__ void __launch_bounds__(128, 2) fa_fwd3_kernel(const bf16* __restrict_
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss)
 #pragma unroll
-        for (int dh = 0; dh < 2; ++dh) vfr[kh][ss][dh] = tr_frag(Vt, 32 * kh + 16 * ss, 32 * dh, lane);
+        for (int dh = 0; dh < 2; ++dh) vfr[kh][ss][dh] = vfrag(Vt + (32 * kh + 16 * ss) * 128, dh);
     softmax(mask_tag, 0, kt0, sA);
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh)
@@ -829,6 +845,243 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv2_kernel(const bf16* __rest
 }
 
 // ------------------------------------------------------------------------------------------
+// dK / dV, variant 3: fa_bwd_dkdv2_kernel with every LDS fragment address precomputed per lane
+// (4 row-read + 4 transposed-read offsets; the 32-row half, the 16-row sub-block and — the loop
+// unrolled by the 3 ring stages — the stage base all become immediates), removing the ~140
+// swizzle-address VALU instructions per iteration that the compiler otherwise rematerialises.
+// Derived from the variant-2 description below: same math and grid as fa_bwd_dkdv_kernel, but the Q / dO
+// slices and their LSE / δ rows arrive by LDS-DMA into a 3-stage ring, two slices ahead, so
+// global latency hides behind two iterations of MFMA work instead of one; K / V fragments are
+// laundered so no compiler-tracked load is outstanding inside the loop. Per iteration: waves
+// 0-1 fetch the Q slice (4 pieces each), waves 2-3 the dO slice, waves 0 / 1 also the LSE / δ
+// rows (one 4-byte DMA each).
+template <bool DROPOUT>
+__global__ void __launch_bounds__(256, 2) fa_bwd_dkdv3_kernel(const bf16* __restrict__ qkv,
+                                                              const bf16* __restrict__ dout,
+                                                              const float* __restrict__ lse,
+                                                              const float* __restrict__ delta,
+                                                              bf16* __restrict__ dqkv, int T, int H, int Hkv,
+                                                              float scale, float p_drop, uint64_t seed) {
+  constexpr int BK = 128, QS = 64, NST = 3;
+  constexpr int TILE = QS * 128;              // one 64-row slice, 128-B rows
+  constexpr int STAGE = 2 * TILE + 512;       // Q | dO | LSE[64] | δ[64]
+  __shared__ __attribute__((aligned(16))) char smem[NST * STAGE];
+  int kb, bh;
+  xcd_head_block(kb, bh);
+  const int b = bh / Hkv, hk = bh % Hkv;
+  const int G = H / Hkv;
+  const int lane = threadIdx.x & 63, w = wave_id(), hh = lane >> 5;
+  const size_t RS = (size_t)(H + 2 * Hkv) * kD;
+  const size_t ORS = (size_t)H * kD;
+  const int kw0 = kb * BK + 32 * w;
+  const int key = kw0 + (lane & 31);
+  const float c = scale * kLog2e;
+  const float inv_keep = DROPOUT ? 1.f / (1.f - p_drop) : 1.f;
+
+  const bf16* kbase = qkv + (size_t)b * T * RS + (size_t)(H + hk) * kD;
+  const bf16* vbase = qkv + (size_t)b * T * RS + (size_t)(H + Hkv + hk) * kD;
+  uint4 kf[4], vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    kf[s] = key < T ? *reinterpret_cast<const uint4*>(kbase + (size_t)key * RS + 16 * s + 8 * hh) : zero4();
+    vf[s] = key < T ? *reinterpret_cast<const uint4*>(vbase + (size_t)key * RS + 16 * s + 8 * hh) : zero4();
+  }
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    launder(kf[s]);
+    launder(vf[s]);
+  }
+  f32x16 dk[2], dv[2];
+#pragma unroll
+  for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dk[dh][i] = dv[dh][i] = 0.f;
+
+  // per-lane LDS byte offsets: row reads (row lane&31, chunk 2s+hh) and transposed reads (rows
+  // 4hh+q and 8+4hh+q, columns 32dh + 16((lane>>4)&1) + 4p); tile_off(r0 + x, ch) = 128·r0 +
+  // tile_off(x, ch) for r0 % 16 == 0, so the row bases below are immediates
+  unsigned ro[4], to[2][2];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) ro[s] = (unsigned)tile_off(lane & 31, 2 * s + hh);
+#pragma unroll
+  for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = 32 * dh + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+      to[dh][j] = (unsigned)(tile_off(4 * hh + ((lane & 15) >> 2) + 8 * j, col >> 3) + ((col & 4) << 1));
+    }
+  auto rowf = [&](const char* t, int s) -> uint4 { return *reinterpret_cast<const uint4*>(t + ro[s]); };
+  auto trf = [&](const char* t, int dh) -> uint4 {
+    const s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(t + to[dh][0]));
+    const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(t + to[dh][1]));
+    const uint2 ux = __builtin_bit_cast(uint2, x), uy = __builtin_bit_cast(uint2, y);
+    return uint4{ux.x, ux.y, uy.x, uy.y};
+  };
+
+  const int s_first = (kb * BK) / QS;
+  const int nslices = (T + QS - 1) / QS;
+  const int per_head = nslices - s_first;
+  const int total = G * per_head;
+
+  // DMA roles: w0/w1 -> Q rows 32w'..32w'+31 (pieces 4w'..4w'+3), w2/w3 -> dO likewise
+  const int is_do = w >> 1, half_sel = w & 1;
+  const unsigned rsb = (unsigned)(is_do ? ORS : RS) * 2;  // row stride in bytes
+  unsigned voff[2];
+#pragma unroll
+  for (int par = 0; par < 2; ++par) {
+    const int row = 8 * par + (lane >> 3);
+    const int ch = (lane & 7) ^ ((((row >> 1) & 1) << 2) | ((row >> 2) & 3));
+    voff[par] = (unsigned)(lane >> 3) * rsb + 16u * ch;
+  }
+  auto dma = [&](int it) {
+    const int itc = min(it, total - 1);  // beyond the end: refetch the last slice (uniform counts)
+    const int hq = hk * G + itc / per_head;
+    const int qs0 = (s_first + itc % per_head) * QS;
+    const unsigned st = __builtin_amdgcn_readfirstlane(lds_addr_of(smem + (it % NST) * STAGE));
+    const bf16* src = is_do ? dout + (size_t)b * T * ORS + (size_t)hq * kD : qkv + (size_t)b * T * RS + (size_t)hq * kD;
+    const size_t rs = is_do ? ORS : RS;
+    const unsigned dst = st + is_do * TILE + half_sel * 4096;
+    if (qs0 + QS <= T) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int p = 4 * half_sel + i;
+        glds16_s(reinterpret_cast<const char*>(src + (size_t)(qs0 + 8 * p) * rs), voff[p & 1], dst + i * 1024);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int p = 4 * half_sel + i;
+        const int row = 8 * p + (lane >> 3);
+        const int ch = (lane & 7) ^ ((((row >> 1) & 1) << 2) | ((row >> 2) & 3));
+        glds16(src + (size_t)min(qs0 + row, T - 1) * rs + 8 * ch, dst + i * 1024);
+      }
+    }
+    if (w < 2) {  // LSE (w0) / δ (w1) rows, clamped to T-1 (those rows are masked anyway)
+      const float* sp = (w == 0 ? lse : delta) + ((size_t)b * H + hq) * T + min(qs0 + lane, T - 1);
+      glds4(sp, st + 2 * TILE + 256 * w);
+    }
+  };
+  auto wait_next = [&]() {  // this wave's DMAs for the next stage done; the one after in flight
+    if (w < 2)
+      asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  };
+
+  if (total > 0) {
+    dma(0);
+    dma(1);
+    wait_next();
+  }
+  __syncthreads();
+  auto iter = [&](int it, auto stage_tag) {
+    constexpr int ST = decltype(stage_tag)::value;
+    dma(it + 2);  // into the stage consumed at it-1 (freed by its barrier)
+    const char* stg = smem + ST * STAGE;
+    const float* lse_s = reinterpret_cast<const float*>(stg + 2 * TILE);
+    const float* del_s = lse_s + QS;
+    const int hq = hk * G + it / per_head;
+    const int qs0 = (s_first + it % per_head) * QS;
+    bool act[2];
+    f32x16 sp[2], dp[2];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int qh0 = qs0 + 32 * half;
+      act[half] = qh0 + 31 >= kw0 && kw0 < T && qh0 < T;
+      if (act[half]) {
+        const char* Qt = stg + half * 32 * 128;
+        const char* Dt = stg + TILE + half * 32 * 128;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4_t dl = *reinterpret_cast<const float4_t*>(&del_s[32 * half + 8 * g + 4 * hh]);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            sp[half][4 * g + k] = 0.f;
+            dp[half][4 * g + k] = DROPOUT ? 0.f : -dl[k];
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          sp[half] = mfma32(rowf(Qt, s), kf[s], sp[half]);
+          dp[half] = mfma32(rowf(Dt, s), vf[s], dp[half]);
+        }
+      }
+    }
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int qh0 = qs0 + 32 * half;
+      if (act[half]) {
+        const char* Qt = stg + half * 32 * 128;
+        const char* Dt = stg + TILE + half * 32 * 128;
+        const bool need_mask = (kw0 + 31 > qh0) || (qh0 + 32 > T) || (kw0 + 32 > T);
+        auto grads = [&](auto mask_tag) {
+          constexpr bool MASK = decltype(mask_tag)::value;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int r0 = 8 * g + 4 * hh;
+            const float4_t l2 = *reinterpret_cast<const float4_t*>(&lse_s[32 * half + r0]) * kLog2e;
+            float4_t dl = {0.f, 0.f, 0.f, 0.f};
+            if constexpr (DROPOUT) dl = *reinterpret_cast<const float4_t*>(&del_s[32 * half + r0]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const int i = 4 * g + k;
+              const int q = qh0 + r0 + k;
+              float p = fexp2(fmaf(sp[half][i], c, -l2[k]));
+              if constexpr (MASK) p = (key > q || q >= T || key >= T) ? 0.f : p;
+              if constexpr (DROPOUT) {
+                const bool keep = dropout_keep(seed, b, hq, H, T, q, key, p_drop);
+                sp[half][i] = keep ? p * inv_keep : 0.f;
+                dp[half][i] = p * ((keep ? dp[half][i] * inv_keep : 0.f) - dl[k]);
+              } else {
+                sp[half][i] = p;
+                dp[half][i] = p * dp[half][i];
+              }
+            }
+          }
+        };
+        if (need_mask)
+          grads(std::true_type{});
+        else
+          grads(std::false_type{});
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          const uint4 pf = acc_frag(sp[half], ss), sf = acc_frag(dp[half], ss);
+#pragma unroll
+          for (int dh = 0; dh < 2; ++dh) {
+            dv[dh] = mfma32(trf(Dt + 16 * ss * 128, dh), pf, dv[dh]);
+            dk[dh] = mfma32(trf(Qt + 16 * ss * 128, dh), sf, dk[dh]);
+          }
+        }
+      }
+    }
+    wait_next();
+    __syncthreads();
+  };
+  int it = 0;
+  for (; it + 3 <= total; it += 3) {
+    iter(it, std::integral_constant<int, 0>{});
+    iter(it + 1, std::integral_constant<int, 1>{});
+    iter(it + 2, std::integral_constant<int, 2>{});
+  }
+  if (it < total) iter(it, std::integral_constant<int, 0>{});
+  if (it + 1 < total) iter(it + 1, std::integral_constant<int, 1>{});
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (key < T) {
+    bf16* dkrow = dqkv + ((size_t)b * T + key) * RS + (size_t)(H + hk) * kD;
+    bf16* dvrow = dqkv + ((size_t)b * T + key) * RS + (size_t)(H + Hkv + hk) * kD;
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = 32 * dh + 8 * g + 4 * hh;
+        store4(dkrow + d, dk[dh][4 * g] * scale, dk[dh][4 * g + 1] * scale, dk[dh][4 * g + 2] * scale,
+               dk[dh][4 * g + 3] * scale);
+        store4(dvrow + d, dv[dh][4 * g], dv[dh][4 * g + 1], dv[dh][4 * g + 2], dv[dh][4 * g + 3]);
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // dQ: grid (ceil(T/128) query blocks, heaviest first, B*H); forward-shaped
 template <bool DROPOUT>
 __global__ void __launch_bounds__(256, 2) fa_bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
@@ -1119,6 +1372,189 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dq3_kernel(const bf16* __restri
   }
 }
 
+// dQ, variant 3: fa_bwd_dq3_kernel with precomputed per-lane LDS fragment offsets and the ring
+// loop unrolled by its 3 stages (stage bases and row bases become immediates), as dK/dV variant 3.
+template <bool DROPOUT>
+__global__ void __launch_bounds__(256, 2) fa_bwd_dq4_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+                                                        const float* __restrict__ lse,
+                                                        const float* __restrict__ delta, bf16* __restrict__ dqkv,
+                                                        int T, int H, int Hkv, float scale, float p_drop,
+                                                        uint64_t seed) {
+  constexpr int BM = 128, BN = 64;
+  constexpr int NST = 3;
+  __shared__ __attribute__((aligned(16))) char smem[NST][2][BN * 128];
+  const int nqb = (T + BM - 1) / BM;
+  int qi, bh;
+  xcd_head_block(qi, bh);
+  const int qb = nqb - 1 - qi;
+  const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
+  const int lane = threadIdx.x & 63, w = wave_id(), hh = lane >> 5;
+  const size_t RS = (size_t)(H + 2 * Hkv) * kD;
+  const size_t ORS = (size_t)H * kD;
+  const bf16* kbase = qkv + (size_t)b * T * RS + (size_t)(H + hk) * kD;
+  const bf16* vbase = qkv + (size_t)b * T * RS + (size_t)(H + Hkv + hk) * kD;
+  const int q0 = qb * BM + 32 * w;
+  const int qrow = q0 + (lane & 31);
+  const float c = scale * kLog2e;
+  const float inv_keep = DROPOUT ? 1.f / (1.f - p_drop) : 1.f;
+
+  uint4 qf[4], dof[4];
+  const bool qok = qrow < T;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    qf[s] = qok ? *reinterpret_cast<const uint4*>(qkv + (size_t)b * T * RS + (size_t)h * kD + (size_t)qrow * RS + 16 * s +
+                                                  8 * hh)
+                : zero4();
+    dof[s] = qok ? *reinterpret_cast<const uint4*>(dout + (size_t)b * T * ORS + (size_t)h * kD + (size_t)qrow * ORS +
+                                                   16 * s + 8 * hh)
+                 : zero4();
+  }
+  const size_t rr = ((size_t)b * H + h) * T + qrow;
+  float l2 = qok ? lse[rr] * kLog2e : 0.f;
+  float dl = qok ? delta[rr] : 0.f;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    launder(qf[s]);
+    launder(dof[s]);
+  }
+  asm volatile("" : "+v"(l2), "+v"(dl));
+
+  // LDS-DMA ring (3 stages, two tiles ahead): waves 0-1 fetch the K tile, waves 2-3 the V
+  // tile, 4 pieces (8 keys x 128 B each) per wave, tile_off image
+  const int is_v = w >> 1, half_sel = w & 1;
+  const unsigned RSB = (unsigned)RS * 2;
+  unsigned voff[2];
+#pragma unroll
+  for (int par = 0; par < 2; ++par) {
+    const int row = 8 * par + (lane >> 3);
+    const int ch = (lane & 7) ^ ((((row >> 1) & 1) << 2) | ((row >> 2) & 3));
+    voff[par] = (unsigned)(lane >> 3) * RSB + 16u * ch;
+  }
+  const bf16* dsrc = is_v ? vbase : kbase;
+  const int kend = min(T, qb * BM + BM);
+  const int ntiles = (kend + BN - 1) / BN;
+  f32x16 dq[2];
+#pragma unroll
+  for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dq[dh][i] = 0.f;
+
+  unsigned ro[4], to[2][2];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) ro[s] = (unsigned)tile_off(lane & 31, 2 * s + hh);
+#pragma unroll
+  for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = 32 * dh + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+      to[dh][j] = (unsigned)(tile_off(4 * hh + ((lane & 15) >> 2) + 8 * j, col >> 3) + ((col & 4) << 1));
+    }
+  auto rowf = [&](const char* t, int s) -> uint4 { return *reinterpret_cast<const uint4*>(t + ro[s]); };
+  auto trf = [&](const char* t, int dh) -> uint4 {
+    const s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(t + to[dh][0]));
+    const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(t + to[dh][1]));
+    const uint2 ux = __builtin_bit_cast(uint2, x), uy = __builtin_bit_cast(uint2, y);
+    return uint4{ux.x, ux.y, uy.x, uy.y};
+  };
+  auto dma = [&](int jt) {
+    const int kt0 = min(jt, ntiles - 1) * BN;  // beyond the end: refetch the last tile (uniform counts)
+    const unsigned dst = __builtin_amdgcn_readfirstlane(lds_addr_of(smem[jt % NST][is_v])) + half_sel * 4096;
+    if (kt0 + BN <= T) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int p = 4 * half_sel + i;
+        glds16_s(reinterpret_cast<const char*>(dsrc + (size_t)(kt0 + 8 * p) * RS), voff[p & 1], dst + i * 1024);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int p = 4 * half_sel + i;
+        const int row = 8 * p + (lane >> 3);
+        const int ch = (lane & 7) ^ ((((row >> 1) & 1) << 2) | ((row >> 2) & 3));
+        glds16(dsrc + (size_t)min(kt0 + row, T - 1) * RS + 8 * ch, dst + i * 1024);
+      }
+    }
+  };
+  dma(0);
+  dma(1);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  __syncthreads();
+  auto iter = [&](int j, auto stage_tag) {
+    constexpr int ST = decltype(stage_tag)::value;
+    const int kt0 = j * BN;
+    dma(j + 2);  // into the stage consumed at j-1 (freed by its barrier)
+    const char* Kt = smem[ST][0];
+    const char* Vt = smem[ST][1];
+    if (kt0 <= q0 + 31) {
+      // dP starts from -δ (row constant = this lane's query row); per 32-key half the dS math
+      // is followed by its dQ MFMAs so the second half's VALU overlaps the first half's MFMAs
+      f32x16 s[2], dp[2];
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          s[kh][i] = 0.f;
+          dp[kh][i] = DROPOUT ? 0.f : -dl;
+        }
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+          s[kh] = mfma32(rowf(Kt + 32 * kh * 128, st), qf[st], s[kh]);
+          dp[kh] = mfma32(rowf(Vt + 32 * kh * 128, st), dof[st], dp[kh]);
+        }
+      }
+      const bool need_mask = (kt0 + BN - 1 > q0) || (kt0 + BN > T) || (q0 + 32 > T);
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+        auto grads = [&](auto mask_tag) {
+          constexpr bool MASK = decltype(mask_tag)::value;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int k = kt0 + 32 * kh + acc_row(i, lane);
+            float p = fexp2(fmaf(s[kh][i], c, -l2));
+            if constexpr (MASK) p = (k > qrow || k >= T || !qok) ? 0.f : p;
+            if constexpr (DROPOUT) {
+              const bool keep = dropout_keep(seed, b, h, H, T, qrow, k, p_drop);
+              s[kh][i] = p * ((keep ? dp[kh][i] * inv_keep : 0.f) - dl);
+            } else {
+              s[kh][i] = p * dp[kh][i];
+            }
+          }
+        };
+        if (need_mask)
+          grads(std::true_type{});
+        else
+          grads(std::false_type{});
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          const uint4 sf = acc_frag(s[kh], ss);
+#pragma unroll
+          for (int dh = 0; dh < 2; ++dh) dq[dh] = mfma32(trf(Kt + (32 * kh + 16 * ss) * 128, dh), sf, dq[dh]);
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // tile j+1 landed, j+2 in flight
+    __syncthreads();
+  };
+  int j = 0;
+  for (; j + 3 <= ntiles; j += 3) {
+    iter(j, std::integral_constant<int, 0>{});
+    iter(j + 1, std::integral_constant<int, 1>{});
+    iter(j + 2, std::integral_constant<int, 2>{});
+  }
+  if (j < ntiles) iter(j, std::integral_constant<int, 0>{});
+  if (j + 1 < ntiles) iter(j + 1, std::integral_constant<int, 1>{});
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (qok) {
+    bf16* dqrow = dqkv + ((size_t)b * T + qrow) * RS + (size_t)h * kD;
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        store4(dqrow + 32 * dh + 8 * g + 4 * hh, dq[dh][4 * g] * scale, dq[dh][4 * g + 1] * scale,
+               dq[dh][4 * g + 2] * scale, dq[dh][4 * g + 3] * scale);
+  }
+}
+
 }  // namespace penroz
 
 // ============================================================================ host side
@@ -1132,7 +1568,7 @@ static void check_qkv(const torch::Tensor& qkv, int64_t H, int64_t Hkv, int64_t 
 }
 
 static int g_fa_fwd_variant = 3;
-static int g_fa_bwd_variant = 2;
+static int g_fa_bwd_variant = 3;
 
 void flash_attn_fwd(torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int64_t H, int64_t Hkv, int64_t D,
                     double scale, double p_drop, int64_t seed) {
@@ -1160,7 +1596,8 @@ void flash_attn_fwd(torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int
 
 // forward: 1 = single-stage (fa_fwd_kernel; also the dropout path), 3 = two query blocks per
 // wave (fa_fwd3_kernel, default). backward:
-// 1 = register-staged dK/dV and dQ kernels, 2 = LDS-DMA pipelined dK/dV and dQ kernels (default)
+// 1 = register-staged dK/dV and dQ kernels, 2 = LDS-DMA pipelined dK/dV and dQ kernels,
+// 3 = variant 2 with precomputed per-lane LDS offsets and stage-unrolled rings (default)
 int64_t flash_bwd_variant(int64_t v) {
   const int64_t prev = g_fa_bwd_variant;
   if (v > 0) g_fa_bwd_variant = (int)v;
@@ -1191,28 +1628,23 @@ void flash_attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, to
   const bf16* d = reinterpret_cast<const bf16*>(dout.data_ptr());
   bf16* g = reinterpret_cast<bf16*>(dqkv.data_ptr());
   dim3 gkv((T + 127) / 128, B * Hkv), gq((T + 127) / 128, B * H);
-  if (p_drop > 0.0 && g_fa_bwd_variant == 1) {
-    hipLaunchKernelGGL(fa_bwd_dkdv_kernel<true>, gkv, dim3(256), 0, stream, q, d, lse.data_ptr<float>(),
-                       delta.data_ptr<float>(), g, T, (int)H, (int)Hkv, (float)scale, (float)p_drop, (uint64_t)seed);
-    hipLaunchKernelGGL(fa_bwd_dq_kernel<true>, gq, dim3(256), 0, stream, q, d, lse.data_ptr<float>(),
-                       delta.data_ptr<float>(), g, T, (int)H, (int)Hkv, (float)scale, (float)p_drop, (uint64_t)seed);
-  } else if (p_drop > 0.0) {
-    hipLaunchKernelGGL(fa_bwd_dkdv2_kernel<true>, gkv, dim3(256), 0, stream, q, d, lse.data_ptr<float>(),
-                       delta.data_ptr<float>(), g, T, (int)H, (int)Hkv, (float)scale, (float)p_drop, (uint64_t)seed);
-    hipLaunchKernelGGL(fa_bwd_dq3_kernel<true>, gq, dim3(256), 0, stream, q, d, lse.data_ptr<float>(),
-                       delta.data_ptr<float>(), g, T, (int)H, (int)Hkv, (float)scale, (float)p_drop, (uint64_t)seed);
-  } else {
-    if (g_fa_bwd_variant == 1)
-      hipLaunchKernelGGL(fa_bwd_dkdv_kernel<false>, gkv, dim3(256), 0, stream, q, d, lse.data_ptr<float>(),
-                         delta.data_ptr<float>(), g, T, (int)H, (int)Hkv, (float)scale, 0.f, (uint64_t)seed);
-    else
-      hipLaunchKernelGGL(fa_bwd_dkdv2_kernel<false>, gkv, dim3(256), 0, stream, q, d, lse.data_ptr<float>(),
-                         delta.data_ptr<float>(), g, T, (int)H, (int)Hkv, (float)scale, 0.f, (uint64_t)seed);
-    if (g_fa_bwd_variant == 1)
-      hipLaunchKernelGGL(fa_bwd_dq_kernel<false>, gq, dim3(256), 0, stream, q, d, lse.data_ptr<float>(),
-                         delta.data_ptr<float>(), g, T, (int)H, (int)Hkv, (float)scale, 0.f, (uint64_t)seed);
-    else
-      hipLaunchKernelGGL(fa_bwd_dq3_kernel<false>, gq, dim3(256), 0, stream, q, d, lse.data_ptr<float>(),
-                         delta.data_ptr<float>(), g, T, (int)H, (int)Hkv, (float)scale, 0.f, (uint64_t)seed);
+  using BwdKernel = void (*)(const bf16*, const bf16*, const float*, const float*, bf16*, int, int, int, float, float,
+                            uint64_t);
+  const bool drop = p_drop > 0.0;
+  BwdKernel kv, dq;
+  if (g_fa_bwd_variant == 1) {
+    kv = drop ? fa_bwd_dkdv_kernel<true> : fa_bwd_dkdv_kernel<false>;
+    dq = drop ? fa_bwd_dq_kernel<true> : fa_bwd_dq_kernel<false>;
+  } else if (g_fa_bwd_variant == 2) {
+    kv = drop ? fa_bwd_dkdv2_kernel<true> : fa_bwd_dkdv2_kernel<false>;
+    dq = drop ? fa_bwd_dq3_kernel<true> : fa_bwd_dq3_kernel<false>;
+  } else {  // (dK/dV with dropout stays on variant 2: the unrolled ring spills with the mask hashing live)
+    kv = drop ? fa_bwd_dkdv2_kernel<true> : fa_bwd_dkdv3_kernel<false>;
+    dq = drop ? fa_bwd_dq4_kernel<true> : fa_bwd_dq4_kernel<false>;
   }
+  const float pd = drop ? (float)p_drop : 0.f;
+  hipLaunchKernelGGL(kv, gkv, dim3(256), 0, stream, q, d, lse.data_ptr<float>(), delta.data_ptr<float>(), g, T,
+                     (int)H, (int)Hkv, (float)scale, pd, (uint64_t)seed);
+  hipLaunchKernelGGL(dq, gq, dim3(256), 0, stream, q, d, lse.data_ptr<float>(), delta.data_ptr<float>(), g, T,
+                     (int)H, (int)Hkv, (float)scale, pd, (uint64_t)seed);
 }

@@ -229,7 +229,7 @@ def test_flash_fwd(B, T, H, Hkv, variant):
     _close(lse, rl, 2e-3, 1e-4, "lse")
 
 
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3])
 @pytest.mark.parametrize("B,T,H,Hkv", [(2, 512, 4, 4), (1, 200, 3, 3), (2, 130, 4, 2), (1, 7, 2, 1), (1, 1024, 2, 2),
                                        (1, 320, 4, 1)])
 def test_flash_bwd(B, T, H, Hkv, variant):
