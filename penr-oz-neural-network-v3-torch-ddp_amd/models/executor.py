@@ -10,7 +10,11 @@ forward, per layer (N = B·T tokens, fp32 residual stream — the reference's au
   tensor, writes head-merged O + LSE) → proj GEMM+bias → residual-add+LN2 (one HIP pass)
   → fc GEMM+bias → GELU (HIP) → fc2 GEMM+bias → (residual-add fused into the next LN)
 head: final LN → lm_head GEMM → cross-entropy (HIP: one LDS-resident pass per row, writes
-  the logits gradient in place, no fp32 logits)
+  the logits gradient in place, no fp32 logits). The head can run in token chunks
+  (``_head_chunk_rows``: automatic above 8 GiB of logits, or ``PENROZ_HEAD_CHUNK`` rows):
+  lm_head GEMM → CE → dgrad → wgrad per chunk over two rotating chunk buffers, so the [N, V]
+  logits tensor is never materialised (the reference's ``F.cross_entropy`` over full logits,
+  ``neural_net_model.py:263-267``).
 backward mirrors it: dgrad/wgrad GEMMs (wgrad accumulated in fp32), GELU backward fused with
   the fc bias-gradient column sum, LayerNorm backward fused with dγ/dβ, the residual-gradient
   accumulation, its bf16 copy for the next GEMM, and the bias gradient of the preceding
@@ -96,6 +100,27 @@ def _dropout_ok(m) -> bool:
 
 
 # residual-dropout mask streams: one per (step seed, site); attention dropout uses seed + layer
+def _head_chunk_rows(N: int, V: int) -> int:
+    """Token rows per lm_head/CE chunk.
+
+    ``PENROZ_HEAD_CHUNK`` = rows (0 = one chunk of all N rows). Unset: one chunk while the bf16
+    [N, V] logits fit in ``PENROZ_HEAD_CHUNK_AUTO_GB`` (default 8 GiB), else chunks of ≈ 2 GiB.
+    Chunking trades time for memory on MI355X (GPT-2 124M headline, N = 65 536:
+    ``profiles/head_chunk_r2_sweep.log``): 67.7 ms/step unchunked, 68.7 at 16 384 rows, 69.1 at
+    8 192, 76.3 at 4 096 (per-chunk wgrad accumulation and untuned GEMM shapes), while the 6.6 GB
+    logits are < 3 % of the 288 GB HBM, so the full tensor stays the default at that size.
+    """
+    import os
+    env = os.environ.get("PENROZ_HEAD_CHUNK")
+    if env is not None:
+        c = int(env)
+    else:
+        row_bytes = ((V + 7) // 8 * 8) * 2
+        limit = float(os.environ.get("PENROZ_HEAD_CHUNK_AUTO_GB", "8")) * 2**30
+        c = 0 if N * row_bytes <= limit else max(1024, int(2 * 2**30 // row_bytes) // 1024 * 1024)
+    return N if c <= 0 or c >= N else c
+
+
 def _site_seed(seed: int, site: int) -> int:
     return (seed * 1_000_003 + 7_919 * (site + 1) + 0x5BD1E995) & 0x7FFFFFFFFFFFFFFF
 
@@ -322,8 +347,11 @@ class GPTExecutor:
         self.lnf_out = torch.empty(N, C, dtype=bf, device=dev)
         # rows padded to a multiple of 8 elements (16 B): the GEMMs take the row stride, the CE
         # kernel's 16-B chunks stay inside the row (HF GPT-2: V = 50257 -> stride 50264)
-        self._logits_buf = torch.empty(N, (V + 7) // 8 * 8, dtype=bf, device=dev)
-        self.logits = self._logits_buf[:, :V]
+        # training: two rotating [chunk, ld] buffers (lm_head → CE → dgrad/wgrad per token chunk);
+        # the full [N, ld] logits only exist transiently for logits_for / diagnostics captures
+        self.head_chunk = _head_chunk_rows(N, V)
+        self._head_bufs = [torch.empty(self.head_chunk, (V + 7) // 8 * 8, dtype=bf, device=dev)
+                           for _ in range(2 if self.head_chunk < N else 1)]
         self.tmp_c = torch.empty(N, C, dtype=bf, device=dev)
         self.dresid = torch.empty(N, C, dtype=f32, device=dev)
         # gradient buffers read by the side-stream weight-gradient GEMMs rotate between two
@@ -335,7 +363,7 @@ class GPTExecutor:
         self._acts_shape = (B, T)
 
     def free_buffers(self):
-        for name in ("resid", "resid_mid", "ln1", "ln2", "qkv", "fcpre", "fcact", "lnf_out", "logits", "_logits_buf", "tmp_c",
+        for name in ("resid", "resid_mid", "ln1", "ln2", "qkv", "fcpre", "fcact", "lnf_out", "_head_bufs", "tmp_c",
                      "dresid", "dresid_bf2", "d_f2", "d_c", "dqkv2", "att", "lse", "stats", "statsf"):
             if hasattr(self, name):
                 delattr(self, name)
@@ -356,6 +384,7 @@ class GPTExecutor:
         return p, _site_seed(seed, 2 * l + branch)
 
     def _forward(self, idx: Tensor, training: bool, dropout_seed: int = 0):
+        """Embedding … final LayerNorm (``self.lnf_out``); the lm_head runs in ``_head_*``."""
         s = self.spec
         B, T = idx.shape
         if T > s.P:
@@ -392,19 +421,34 @@ class GPTExecutor:
         dp, ds = self._drop(training, dropout_seed, Lc - 1, 1)
         norm_ops.add_ln_fwd(self.resid_mid[Lc - 1], self.tmp_c, self.resid[Lc], f(s.lnf.weight), f(s.lnf.bias),
                             s.lnf.eps, y=self.lnf_out, mean=meanf, rstd=rstdf, dropout_p=dp, dropout_seed=ds)
-        torch.mm(self.lnf_out, self.bf16(s.head.weight).t(), out=self.logits)
+
+    def _head_logits(self, r0: int, r1: int, buf: Tensor) -> Tensor:
+        """lm_head GEMM of token rows [r0, r1) into ``buf`` ([rows, ld]); returns the [rows, V] view."""
+        lg = buf[: r1 - r0, : self.spec.V]
+        torch.mm(self.lnf_out[r0:r1], self.bf16(self.spec.head.weight).t(), out=lg)
+        return lg
+
+    def _full_logits(self) -> Tensor:
+        N, V = self.lnf_out.shape[0], self.spec.V
+        buf = torch.empty(N, (V + 7) // 8 * 8, dtype=torch.bfloat16, device=self.device)
+        return self._head_logits(0, N, buf)
 
     # ------------------------------------------------------------------ public API
     @torch.no_grad()
     def eval_loss(self, idx: Tensor, targets: Tensor) -> Tensor:
         self._forward(idx, training=False)
-        rows = fused_ops.cross_entropy_fwd_bwd(self.logits, targets.reshape(-1), 0.0)
-        return rows.mean()
+        N, tg = self.lnf_out.shape[0], targets.reshape(-1)
+        total = torch.zeros((), dtype=torch.float32, device=self.device)
+        for r0 in range(0, N, self.head_chunk):
+            r1 = min(N, r0 + self.head_chunk)
+            total += fused_ops.cross_entropy_fwd_bwd(self._head_logits(r0, r1, self._head_bufs[0]), tg[r0:r1],
+                                                     0.0).sum()
+        return total / N
 
     @torch.no_grad()
     def logits_for(self, idx: Tensor) -> Tensor:
         self._forward(idx, training=False)
-        return self.logits.view(idx.shape[0], idx.shape[1], -1)
+        return self._full_logits().view(idx.shape[0], idx.shape[1], -1)
 
     def setup_training(self, distributed: bool):
         from penroz.parallel.reducer import GradReducer, plan_buckets, DEFAULT_BUCKET_MB
@@ -532,17 +576,27 @@ class GPTExecutor:
         with trace_range("forward"):
             self._forward(idx, training=True, dropout_seed=seed)
         cap = capture and self._captured is None
-        if cap:
-            acts = [self.resid[0].view(B, T, C).clone()] * 2 + [r.view(B, T, C).clone() for r in self.resid[1:]] + \
-                   [self.lnf_out.view(B, T, C).float().clone(), self.logits.view(B, T, -1).clone()]
-        # ---- head: CE (in place -> dlogits), lm_head backward, final LN backward
+        # ---- head, per token chunk: lm_head GEMM, CE (in place -> dlogits), dgrad, wgrad
         head_range = trace_range("backward.head")
         head_range.__enter__()
         self._defer_reductions(True)
-        rows = fused_ops.cross_entropy_fwd_bwd(self.logits, targets.reshape(-1), scale / N)
-        loss = rows.sum() * (scale / N)
-        torch.mm(self.logits, self._dgrad_w(s.head.weight), out=self.d_c)
-        self._wgrad(self.logits, self.lnf_out, s.head.weight)
+        tg = targets.reshape(-1)
+        if cap:  # diagnostics want the whole logits / dlogits tensors: one transient chunk
+            full = self._full_logits()
+            acts = [self.resid[0].view(B, T, C).clone()] * 2 + [r.view(B, T, C).clone() for r in self.resid[1:]] + \
+                   [self.lnf_out.view(B, T, C).float().clone(), full.view(B, T, -1).clone()]
+            chunks = [(0, N, full)]
+        else:
+            chunks = [(r0, min(N, r0 + self.head_chunk), None) for r0 in range(0, N, self.head_chunk)]
+        loss = torch.zeros((), dtype=torch.float32, device=self.device)
+        w_dgrad = self._dgrad_w(s.head.weight)
+        for i, (r0, r1, lg) in enumerate(chunks):
+            if lg is None:  # the side stream may still be reading this buffer (wgrad two chunks back)
+                lg = self._head_logits(r0, r1, self._reuse(self._head_bufs[i % len(self._head_bufs)]))
+            loss += fused_ops.cross_entropy_fwd_bwd(lg, tg[r0:r1], scale / N).sum()
+            torch.mm(lg, w_dgrad, out=self.d_c[r0:r1])
+            self._wgrad(lg, self.lnf_out[r0:r1], s.head.weight)
+        loss *= scale / N
         mean, rstd = self.statsf
         last = s.blocks[-1]
         rb = 0  # rotating dresid_bf buffer index
@@ -552,7 +606,7 @@ class GPTExecutor:
                         self.grad(last.fc2.bias), dropout_p=dp, dropout_seed=ds)
         grads_cap = []
         if cap:
-            grads_cap = [self.logits.view(B, T, -1).clone(), self.d_c.view(B, T, C).float().clone(),
+            grads_cap = [full.view(B, T, -1).clone(), self.d_c.view(B, T, C).float().clone(),
                          self.dresid.view(B, T, C).clone()]
         self._segment_done(0, sync)
         head_range.__exit__(None, None, None)

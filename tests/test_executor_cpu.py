@@ -42,3 +42,15 @@ def test_non_matching_layouts():
     assert GPTExecutor.match(_model(odd_head)) is None
     mlp = [{"linear": {"in_features": 4, "out_features": 4}}, {"relu": {}}, {"linear": {"in_features": 4, "out_features": 2}}]
     assert GPTExecutor.match(_model(mlp)) is None
+
+
+def test_head_chunk_policy(monkeypatch):
+    from penroz.models.executor import _head_chunk_rows
+    monkeypatch.delenv("PENROZ_HEAD_CHUNK", raising=False)
+    assert _head_chunk_rows(65536, 50304) == 65536          # 6.6 GB of logits: one chunk
+    c = _head_chunk_rows(4 * 65536, 50304)                   # 26 GB: ~2 GiB chunks
+    assert c % 1024 == 0 and 1024 <= c < 4 * 65536 and c * 50304 * 2 <= 2 * 2**30
+    monkeypatch.setenv("PENROZ_HEAD_CHUNK", "8192")
+    assert _head_chunk_rows(65536, 50304) == 8192
+    monkeypatch.setenv("PENROZ_HEAD_CHUNK", "0")
+    assert _head_chunk_rows(4 * 65536, 50304) == 4 * 65536

@@ -174,3 +174,30 @@ def test_executor_dropout_masks_are_consistent_between_fwd_and_bwd():
     ex._step_seed = seed0 + 1000
     ex.zero_grad()
     assert abs(ex.train_micro_step(x, y, 1.0).item() - loss.item()) > 1e-4
+
+
+@pytest.mark.parametrize("V", [512, 509])
+def test_executor_chunked_head_matches_one_chunk(monkeypatch, V):
+    """Token-chunked lm_head/CE (PENROZ_HEAD_CHUNK rows, two rotating buffers, wgrad per chunk
+    on the side stream) gives the loss and gradients of the single-chunk head."""
+    torch.manual_seed(0)
+    m = tiny(V=V).cuda()
+    m2 = copy.deepcopy(m)
+    B, T = 4, 128
+    x = torch.randint(0, V, (B, T), device="cuda")
+    y = torch.randint(0, V, (B, T), device="cuda")
+    out = []
+    for model, chunk in ((m, "0"), (m2, "96")):  # 96 does not divide 512: a ragged last chunk
+        monkeypatch.setenv("PENROZ_HEAD_CHUNK", chunk)
+        ex = GPTExecutor(model, torch.device("cuda"))
+        ex.setup_training(False)
+        ex.zero_grad()
+        loss = ex.train_micro_step(x, y, 1.0)
+        ev = ex.eval_loss(x, y)
+        torch.cuda.synchronize()
+        assert len(ex._head_bufs) == (1 if chunk == "0" else 2)
+        out.append((loss.item(), ev.item(), ex.flat_grad.clone()))
+    (l1, e1, g1), (l2, e2, g2) = out
+    assert abs(l1 - l2) < 1e-4 and abs(e1 - e2) < 1e-4, (l1, l2, e1, e2)
+    rel = (g1 - g2).norm() / g1.norm()
+    assert rel < 1e-3, rel
