@@ -25,18 +25,12 @@ if "wgrad" in which:
         x = torch.randn(N, n, device="cuda", dtype=torch.bfloat16)
         g = torch.zeros(m, n, device="cuda")
         fl = 2 * N * m * n
-        tn = timeit(lambda: k.wgrad_gemm(dy, x, g, 256, 1))
-        treg = timeit(lambda: k.wgrad_gemm(dy, x, g, 256, 0))
-        tr4 = timeit(lambda: k.wgrad_gemm(dy, x, g, 256, 2))
-        tr5 = timeit(lambda: k.wgrad_gemm(dy, x, g, 256, 3))
+        tn = timeit(lambda: k.wgrad_gemm(dy, x, g))
         tr16 = timeit(lambda: k.wgrad_gemm(dy, x, g, 256, 4))
-        tr16b = timeit(lambda: k.wgrad_gemm(dy, x, g, 256, 5))
         t128 = timeit(lambda: k.wgrad_gemm(dy, x, g, 128))
         tt = timeit(lambda: g.add_(torch.mm(dy.t(), x, out_dtype=torch.float32)))
-        emit(kernel="wgrad", shape=name, native_TF=round(fl / tn / 1e12, 1), native_regstage_TF=round(fl / treg / 1e12, 1),
-             ring4_TF=round(fl / tr4 / 1e12, 1), ring5_TF=round(fl / tr5 / 1e12, 1), ring16_TF=round(fl / tr16 / 1e12, 1), ring16x5_TF=round(fl / tr16b / 1e12, 1),
-             native128_TF=round(fl / t128 / 1e12, 1),
-             hipblaslt_TF=round(fl / tt / 1e12, 1),
+        emit(kernel="wgrad", shape=name, native_TF=round(fl / tn / 1e12, 1), ring16_TF=round(fl / tr16 / 1e12, 1),
+             native128_TF=round(fl / t128 / 1e12, 1), hipblaslt_TF=round(fl / tt / 1e12, 1),
              native_us=round(tn * 1e6, 1), hipblaslt_us=round(tt * 1e6, 1))
 if "attn" in which:
     B, T, H, D = 64, 1024, 12, 64

@@ -1,4 +1,4 @@
-"""Run the native wgrad kernel (ring16, the default) a few times on one GPT-2 124M shape — a
+"""Run the native wgrad kernel (default variant) a few times on one GPT-2 124M shape — a
 target for rocprofv3 --pmc passes (bench/gpu_pmc_wgrad.sh).  python bench/wgrad_one.py lm_head"""
 import os
 import sys
@@ -14,5 +14,5 @@ dy = (torch.rand(N, m, device="cuda") * 2 - 1).to(torch.bfloat16)
 x = (torch.rand(N, n, device="cuda") * 2 - 1).to(torch.bfloat16)
 g = torch.zeros(m, n, device="cuda")
 for _ in range(3):
-    _ext.kernels().wgrad_gemm(dy, x, g, 256, 4)
+    _ext.kernels().wgrad_gemm(dy, x, g)
 torch.cuda.synchronize()

@@ -2,23 +2,26 @@
 //
 // For a linear y = x·Wᵀ: A = dY [tokens, out], B = X [tokens, in], G = dW [out, in]. Both
 // operands are row-major in the reduction dimension k (tokens), which is what makes this GEMM
-// awkward for library kernels at GPT-2 shapes (hipBLASLt measured 270–980 TF here: small M×N,
-// K = 65 536).  Design (default path = wgrad256_ring_kernel<32, 4>):
-//   * 256×256 output tile per 512-thread workgroup (8 waves as 2×4, each 128×64 = 4×2 MFMA
-//     32x32x16 tiles), one workgroup per CU (128 KiB LDS);
+// awkward for library kernels at GPT-2 shapes (hipBLASLt measured 270–980 TF here, 410–1000 TF
+// tuned: profiles/wgrad_native_vs_hipblaslt_r2.log).  Design (default path =
+// wgrad256_ring16o_kernel<32, 4>, variant 6):
+//   * 256×256 output tile per 512-thread workgroup (8 waves as 2×4, each 128×64 = 8×4 MFMA
+//     16x16x32 tiles), one workgroup per CU (128 KiB LDS);
 //   * operand tiles arrive by LDS-DMA (global_load_lds_dwordx4, issued in inline asm so the
 //     compiler does not serialise it against ds_reads) into a 4-stage ring of [32 k][256]
-//     tiles; three stages are in flight and the end-of-step wait is a counted vmcnt;
+//     tiles; three stages are in flight and the end-of-step wait is a counted vmcnt; DMA
+//     sources are a scalar row base plus a per-lane offset fixed for the kernel;
 //   * tiles are consumed column-wise with ds_read_b64_tr_b16 (no transposes in memory); the
-//     512-B rows use the XOR swizzle ch ^ ((row&3)<<2), applied on the DMA SOURCE address
-//     because the DMA destination is lane-linear;
+//     512-B rows use an XOR swizzle of the 16-B chunk (swz16), applied on the DMA SOURCE
+//     address because the DMA destination is lane-linear; per-lane fragment offsets are
+//     computed once;
 //   * split-K over tokens chosen by a wave-quantisation cost model; each split writes an fp32
 //     slab and a deterministic fixed-order reduction adds the slabs into the gradient buffer
 //     (bitwise reproducible); one split => direct read-add-write;
 //   * XCD-aware bijective block remap: a contiguous chunk of (split, tile) pairs per XCD so
 //     workgroups sharing a k-range and an operand panel share that XCD's L2.
-// wgrad_kernel (128×128, 4 waves, register staging) and wgrad256_kernel (double-buffered)
-// are kept as selectable variants for A/B measurement.
+// wgrad_kernel (128×128, 4 waves, register staging; tile=128) and wgrad256_ring16_kernel
+// (variant 4, the round-1 default) stay selectable for A/B measurement.
 #include "common.h"
 #include "host_plan.h"
 #include <torch/extension.h>
@@ -151,272 +154,17 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(const bf16* __restrict__ 
 
 
 // ---------------------------------------------------------------------------------------
-// 256×256 tile, 8 waves (2 along M × 4 along N, each wave 128×64 = 4×2 MFMA tiles), BK = 64.
-// Per k-step: 64 KiB of operands for 2·256·256·64 FLOP = 128 FLOP/B (the 128² tile's 64 FLOP/B
-// left it L2-bandwidth-bound at 320–500 TF). LDS rows are 512 B; chunk ch of row r lives at
-// ch ^ ((r&3)<<2), which keeps the 4-row × 4-chunk transposed half-wave reads conflict-free.
-constexpr int BM2 = 256, BN2 = 256, BK2 = 64;
+// 256×256 tile, 8 waves (2 along M × 4 along N, each wave 128×64). Per 32-deep k-step: 32 KiB
+// of operands for 2·256·256·32 FLOP = 128 FLOP/B (the 128² tile's 64 FLOP/B left it
+// L2-bandwidth-bound at 320–500 TF). LDS rows are 512 B. (The 32x32x16 and register-staged
+// 256-tile variants of round 1 measured slower and were removed.)
+constexpr int BM2 = 256, BN2 = 256, BK2 = 32;
 
-__device__ __forceinline__ int off512(int row, int ch) { return row * 512 + ((ch ^ ((row & 3) << 2)) << 4); }
-
-__device__ __forceinline__ uint2 tr_read512(const char* tile, int row, int col) {
-  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + off512(row, col >> 3) + ((col & 4) << 1)));
-  return __builtin_bit_cast(uint2, v);
-}
-
-__device__ __forceinline__ uint4 tr_frag512(const char* tile, int rbase, int cbase, int lane) {
-  const int hh = lane >> 5, q = (lane & 15) >> 2, p = lane & 3;
-  const int col = cbase + 16 * ((lane >> 4) & 1) + 4 * p;
-  const uint2 a = tr_read512(tile, rbase + 4 * hh + q, col);
-  const uint2 b = tr_read512(tile, rbase + 8 + 4 * hh + q, col);
-  return uint4{a.x, a.y, b.x, b.y};
-}
-
-// GLDS: stage tiles with global_load_lds_dwordx4 (LDS-DMA, no VGPR round trip, no ds_write
-// transfer cost). The DMA destination is lane-linear (1 KiB per wave-instruction = two 512-B
-// k-rows), so the XOR swizzle is applied on the per-lane SOURCE address instead.
-template <bool GLDS>
-__global__ void __launch_bounds__(512, 1) wgrad256_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
-                                                          float* __restrict__ out, int M, int N, int K, int lda,
-                                                          int ldb, int klen, int tiles_m, int tiles_n, int direct) {
-  extern __shared__ __attribute__((aligned(16))) char smem2[];  // [2 buf][A|B][BK2 * 512]
-  const int nwg = gridDim.x, wg = blockIdx.x;
-  const int xcd = wg & 7, qd = nwg >> 3, rd = nwg & 7;
-  const int id = (xcd < rd ? xcd * (qd + 1) : rd * (qd + 1) + (xcd - rd) * qd) + (wg >> 3);
-  const int ntiles = tiles_m * tiles_n;
-  const int split = id / ntiles, tile = id - split * ntiles;
-  const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
-  const int m0 = tm * BM2, n0 = tn * BN2;
-  const int k0 = split * klen, k1 = min(K, k0 + klen);
-  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), hh = lane >> 5;
-  const int wm = w >> 2, wn = w & 3;
-  constexpr int TILE = BK2 * 512;
-
-  // staging: thread t -> chunk t&31 of rows (t>>5) + 16i, i = 0..3 (a wave covers two whole
-  // 512-B rows: coalesced loads, conflict-free ds_write_b128 groups)
-  const int sr = threadIdx.x >> 5, sc = threadIdx.x & 31;
-  uint4 ast[4], bst[4];
-  auto gload = [&](int kk) {
-    const int mc = m0 + 8 * sc, nc = n0 + 8 * sc;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int k = kk + sr + 16 * i;
-      const bool kok = k < k1;
-      ast[i] = (kok && mc < M) ? *reinterpret_cast<const uint4*>(A + (size_t)k * lda + mc) : uint4{0, 0, 0, 0};
-      bst[i] = (kok && nc < N) ? *reinterpret_cast<const uint4*>(B + (size_t)k * ldb + nc) : uint4{0, 0, 0, 0};
-    }
-  };
-  auto lstore = [&](int buf) {
-    char* a = smem2 + buf * 2 * TILE;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      *reinterpret_cast<uint4*>(a + off512(sr + 16 * i, sc)) = ast[i];
-      *reinterpret_cast<uint4*>(a + TILE + off512(sr + 16 * i, sc)) = bst[i];
-    }
-  };
-
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  // LDS-DMA staging: wave w fills pieces 4w..4w+3 (rows 2p, 2p+1) of both tiles. Per-lane
-  // source offsets are fixed across k-steps (row-in-tile and swizzled chunk); out-of-range
-  // lanes read the zero page.
-  const int rl = lane >> 5, pc = lane & 31;
-  const bf16* asrc[4];
-  const bf16* bsrc[4];
-  int krow[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = 2 * (4 * w + i) + rl;
-    const int ch = pc ^ ((row & 3) << 2);  // off512's swizzle, inverted (an involution)
-    const int mc = m0 + 8 * ch, nc = n0 + 8 * ch;
-    krow[i] = k0 + row;
-    asrc[i] = mc < M ? A + (size_t)krow[i] * lda + mc : nullptr;
-    bsrc[i] = nc < N ? B + (size_t)krow[i] * ldb + nc : nullptr;
-  }
-  const unsigned lds_base = (unsigned)(size_t)(lds_void_t*)smem2;
-  const void* zero = (const void*)g_zero16;
-  auto dma = [&](int st, int buf) {
-    const int dk = st * BK2;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const bool kok = krow[i] + dk < k1;
-      const void* ga = (kok && asrc[i]) ? (const void*)(asrc[i] + (size_t)dk * lda) : zero;
-      const void* gb = (kok && bsrc[i]) ? (const void*)(bsrc[i] + (size_t)dk * ldb) : zero;
-      const unsigned la = __builtin_amdgcn_readfirstlane(lds_base + buf * 2 * TILE + (4 * w + i) * 1024);
-      glds16(ga, la);
-      glds16(gb, la + TILE);
-    }
-  };
-
-  const int nsteps = (k1 - k0 + BK2 - 1) / BK2;
-  if (nsteps > 0) {
-    if constexpr (GLDS) {
-      dma(0, 0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      gload(k0);
-      lstore(0);
-    }
-  }
-  __syncthreads();
-  for (int st = 0; st < nsteps; ++st) {
-    if constexpr (GLDS) {
-      if (st + 1 < nsteps) dma(st + 1, (st + 1) & 1);
-    } else {
-      if (st + 1 < nsteps) gload(k0 + (st + 1) * BK2);
-    }
-    const char* At = smem2 + (st & 1) * 2 * TILE;
-    const char* Bt = At + TILE;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      uint4 af[4], bf[2];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) bf[j] = tr_frag512(Bt, 16 * s, 64 * wn + 32 * j, lane);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = tr_frag512(At, 16 * s, 128 * wm + 32 * i, lane);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(af[i], bf[j], acc[i][j]);
-    }
-    if constexpr (GLDS) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      if (st + 1 < nsteps) lstore((st + 1) & 1);
-    }
-    __syncthreads();
-  }
-  float* o = direct ? out : out + (size_t)split * M * N;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = n0 + 64 * wn + 32 * j + (lane & 31);
-      if (n >= N) continue;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + 128 * wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        if (m < M) {
-          float* p = o + (size_t)m * N + n;
-          if (direct) *p += acc[i][j][r];
-          else *p = acc[i][j][r];
-        }
-      }
-    }
-}
-
+// ---- 16x16x32 MFMA variant ---------------------------------------------------------------
 // LDS-DMA ring: NBUF stages of BKT k-rows; tile t+NBUF-1 is issued while tile t is consumed,
 // and the end-of-step wait is a counted vmcnt that leaves NBUF-2 tiles in flight across the
 // barrier (tiles beyond the split's range DMA the zero page, so the count is uniform).
-template <int BKT, int NBUF>
-__global__ void __launch_bounds__(512, 1) wgrad256_ring_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
-                                                               float* __restrict__ out, int M, int N, int K, int lda,
-                                                               int ldb, int klen, int tiles_m, int tiles_n,
-                                                               int direct) {
-  extern __shared__ __attribute__((aligned(16))) char smem2[];  // [NBUF][A|B][BKT * 512]
-  constexpr int TILE = BKT * 512;
-  constexpr int PIECES = BKT / 16;  // 1-KiB pieces per wave per operand per stage
-  constexpr int G = 2 * PIECES;     // DMA instructions per wave per stage
-  static_assert(BKT % 16 == 0 && NBUF >= 3 && (NBUF - 2) * G <= 63, "ring geometry");
-  const int nwg = gridDim.x, wg = blockIdx.x;
-  const int xcd = wg & 7, qd = nwg >> 3, rd = nwg & 7;
-  const int id = (xcd < rd ? xcd * (qd + 1) : rd * (qd + 1) + (xcd - rd) * qd) + (wg >> 3);
-  const int ntiles = tiles_m * tiles_n;
-  const int split = id / ntiles, tile = id - split * ntiles;
-  const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
-  const int m0 = tm * BM2, n0 = tn * BN2;
-  const int k0 = split * klen, k1 = min(K, k0 + klen);
-  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), hh = lane >> 5;
-  const int wm = w >> 2, wn = w & 3;
-
-  const int rl = lane >> 5, pc = lane & 31;
-  const bf16* asrc[PIECES];
-  const bf16* bsrc[PIECES];
-  int krow[PIECES];
-#pragma unroll
-  for (int i = 0; i < PIECES; ++i) {
-    const int row = 2 * (PIECES * w + i) + rl;
-    const int ch = pc ^ ((row & 3) << 2);
-    const int mc = m0 + 8 * ch, nc = n0 + 8 * ch;
-    krow[i] = k0 + row;
-    asrc[i] = mc < M ? A + (size_t)krow[i] * lda + mc : nullptr;
-    bsrc[i] = nc < N ? B + (size_t)krow[i] * ldb + nc : nullptr;
-  }
-  const unsigned lds_base = (unsigned)(size_t)(lds_void_t*)smem2;
-  const void* zero = (const void*)g_zero16;
-  auto dma = [&](int st) {
-    const int dk = st * BKT, buf = st % NBUF;
-#pragma unroll
-    for (int i = 0; i < PIECES; ++i) {
-      const bool kok = krow[i] + dk < k1;
-      const void* ga = (kok && asrc[i]) ? (const void*)(asrc[i] + (size_t)dk * lda) : zero;
-      const void* gb = (kok && bsrc[i]) ? (const void*)(bsrc[i] + (size_t)dk * ldb) : zero;
-      const unsigned la = __builtin_amdgcn_readfirstlane(lds_base + buf * 2 * TILE + (PIECES * w + i) * 1024);
-      glds16(ga, la);
-      glds16(gb, la + TILE);
-    }
-  };
-
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  const int nsteps = (k1 - k0 + BKT - 1) / BKT;
-#pragma unroll
-  for (int t = 0; t < NBUF - 1; ++t) dma(t);
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NBUF - 2) * G) : "memory");
-  __syncthreads();
-  for (int st = 0; st < nsteps; ++st) {
-    dma(st + NBUF - 1);  // into the stage consumed at step st-1 (freed by its barrier)
-    const char* At = smem2 + (st % NBUF) * 2 * TILE;
-    const char* Bt = At + TILE;
-#pragma unroll
-    for (int s = 0; s < BKT / 16; ++s) {
-      uint4 af[4], bf[2];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) bf[j] = tr_frag512(Bt, 16 * s, 64 * wn + 32 * j, lane);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = tr_frag512(At, 16 * s, 128 * wm + 32 * i, lane);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(af[i], bf[j], acc[i][j]);
-    }
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NBUF - 2) * G) : "memory");  // stage st+1 landed
-    __syncthreads();
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the zero-page prefetches
-  float* o = direct ? out : out + (size_t)split * M * N;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = n0 + 64 * wn + 32 * j + (lane & 31);
-      if (n >= N) continue;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + 128 * wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        if (m < M) {
-          float* p = o + (size_t)m * N + n;
-          if (direct) *p += acc[i][j][r];
-          else *p = acc[i][j][r];
-        }
-      }
-    }
-}
-
-// ---- 16x16x32 MFMA variant ---------------------------------------------------------------
-// Same ring pipeline; each wave's 128×64 output is 8×4 tiles of v_mfma_f32_16x16x32_bf16 (the
+// Each wave's 128×64 output is 8×4 tiles of v_mfma_f32_16x16x32_bf16 (the
 // 16x16 shape holds a higher clock than 32x32x16 on random data at equal cycles per FLOP).
 // Operand fragment (A or B, from a [k][256] tile): lane l holds k = 8·(l>>4) + j, j = 0..7, of
 // column c0 + (l&15) — two ds_read_b64_tr_b16 (rows 8g..8g+3 and 8g+4..8g+7 of its 16-lane
@@ -547,6 +295,152 @@ __global__ void __launch_bounds__(512, 1) wgrad256_ring16_kernel(const bf16* __r
     }
 }
 
+// ---- ring16 with scalar-base DMA and precomputed fragment offsets (variant 6, default) ------
+// The ring16 pipeline with the per-step address work moved off the vector ALUs: each DMA piece
+// is global_load_lds with a wave-uniform SGPR row base (A + k·lda, advanced by scalar adds) and
+// a per-lane 32-bit offset fixed for the whole kernel; tile columns past M / N are clamped to
+// the last valid 16-B chunk (their products only reach output rows / columns that are never
+// stored), so only a ragged K tail takes the per-lane zero-page path. Fragment reads use
+// per-lane LDS offsets computed once (off512b is periodic in 16 rows, so the k slice and the
+// second half-read are immediates) and the loop is unrolled by the ring depth, making every
+// stage base a constant. (s_setprio around the MFMA clusters measured 4 % slower.)
+template <int BKT, int NBUF>
+__global__ void __launch_bounds__(512, 1) wgrad256_ring16o_kernel(const bf16* __restrict__ A,
+                                                                  const bf16* __restrict__ B,
+                                                                  float* __restrict__ out, int M, int N, int K,
+                                                                  int lda, int ldb, int klen, int tiles_m,
+                                                                  int tiles_n, int direct) {
+  extern __shared__ __attribute__((aligned(16))) char smem2[];  // [NBUF][A|B][BKT * 512]
+  constexpr int TILE = BKT * 512;
+  constexpr int PIECES = BKT / 16;
+  constexpr int G = 2 * PIECES;
+  static_assert(BKT % 32 == 0 && NBUF == 4 && (NBUF - 2) * G <= 63, "ring geometry");
+  const int nwg = gridDim.x, wg = blockIdx.x;
+  const int xcd = wg & 7, qd = nwg >> 3, rd = nwg & 7;
+  const int id = (xcd < rd ? xcd * (qd + 1) : rd * (qd + 1) + (xcd - rd) * qd) + (wg >> 3);
+  const int ntiles = tiles_m * tiles_n;
+  const int split = id / ntiles, tile = id - split * ntiles;
+  const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+  const int m0 = tm * BM2, n0 = tn * BN2;
+  const int k0 = split * klen, k1 = min(K, k0 + klen);
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = w >> 2, wn = w & 3;
+
+  // DMA: piece i of wave w = tile rows 2(PIECES·w + i) + (lane>>5), 16-B chunk (lane&31) ^ swz
+  const int rl = lane >> 5, pc = lane & 31;
+  const int mlast = ((M + 7) & ~7) - 8, nlast = N - 8;
+  unsigned aoff[PIECES], boff[PIECES];
+#pragma unroll
+  for (int i = 0; i < PIECES; ++i) {
+    const int row = 2 * (PIECES * w + i) + rl;
+    const int ch = pc ^ swz16(row);
+    aoff[i] = (unsigned)(row * lda + min(m0 + 8 * ch, mlast)) * 2u;
+    boff[i] = (unsigned)(row * ldb + min(n0 + 8 * ch, nlast)) * 2u;
+  }
+  const unsigned lds_base = (unsigned)(size_t)(lds_void_t*)smem2;
+  const char* zero = reinterpret_cast<const char*>(g_zero16);
+  auto dma = [&](int st) {
+    const int kr = k0 + st * BKT;
+    const unsigned la = __builtin_amdgcn_readfirstlane(lds_base + (st % NBUF) * 2 * TILE + PIECES * w * 1024);
+    const char* sa = reinterpret_cast<const char*>(A + (size_t)kr * lda);
+    const char* sb = reinterpret_cast<const char*>(B + (size_t)kr * ldb);
+    if (kr + BKT <= k1) {
+#pragma unroll
+      for (int i = 0; i < PIECES; ++i) {
+        glds16_s(sa, aoff[i], la + i * 1024);
+        glds16_s(sb, boff[i], la + TILE + i * 1024);
+      }
+    } else {  // ragged K tail or a prefetch past the end: rows >= k1 read the zero page
+#pragma unroll
+      for (int i = 0; i < PIECES; ++i) {
+        const bool ok = kr + 2 * (PIECES * w + i) + rl < k1;
+        glds16(ok ? sa + aoff[i] : zero, la + i * 1024);
+        glds16(ok ? sb + boff[i] : zero, la + TILE + i * 1024);
+      }
+    }
+  };
+
+  // fragment reads: lane holds k = 8·(lane>>4) + j of column c0 + (lane&15); rows r and r + 4
+  const int g = lane >> 4, q = (lane & 15) >> 2, p4 = 4 * (lane & 3);
+  unsigned fa[8], fb[4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int col = 128 * wm + 16 * i + p4;
+    fa[i] = (unsigned)(off512b(8 * g + q, col >> 3) + ((col & 4) << 1));
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = 64 * wn + 16 * j + p4;
+    fb[j] = (unsigned)(off512b(8 * g + q, col >> 3) + ((col & 4) << 1));
+  }
+  auto frag = [&](const char* t, unsigned off) -> uint4 {
+    const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(t + off));
+    const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(t + off + 4 * 512));
+    const uint2 ua = __builtin_bit_cast(uint2, a), ub = __builtin_bit_cast(uint2, b);
+    return uint4{ua.x, ua.y, ub.x, ub.y};
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nsteps = (k1 - k0 + BKT - 1) / BKT;
+#pragma unroll
+  for (int t = 0; t < NBUF - 1; ++t) dma(t);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NBUF - 2) * G) : "memory");
+  __syncthreads();
+  auto step = [&](int st, auto stage_tag) {
+    constexpr int ST = decltype(stage_tag)::value;
+    dma(st + NBUF - 1);  // into the stage consumed at step st-1 (freed by its barrier)
+    const char* At = smem2 + ST * 2 * TILE;
+    const char* Bt = At + TILE;
+#pragma unroll
+    for (int s = 0; s < BKT / 32; ++s) {
+      uint4 bf[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf[j] = frag(Bt + s * 32 * 512, fb[j]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint4 af = frag(At + s * 32 * 512, fa[i]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af, bf[j], acc[i][j]);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NBUF - 2) * G) : "memory");  // stage st+1 landed
+    __syncthreads();
+  };
+  int st = 0;
+  for (; st + NBUF <= nsteps; st += NBUF) {
+    step(st, std::integral_constant<int, 0>{});
+    step(st + 1, std::integral_constant<int, 1>{});
+    step(st + 2, std::integral_constant<int, 2>{});
+    step(st + 3, std::integral_constant<int, 3>{});
+  }
+  if (st < nsteps) step(st, std::integral_constant<int, 0>{});
+  if (st + 1 < nsteps) step(st + 1, std::integral_constant<int, 1>{});
+  if (st + 2 < nsteps) step(st + 2, std::integral_constant<int, 2>{});
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the zero-page prefetches
+  float* o = direct ? out : out + (size_t)split * M * N;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + 64 * wn + 16 * j + (lane & 15);
+      if (n >= N) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + 128 * wm + 16 * i + 4 * g + r;
+        if (m < M) {
+          float* pp = o + (size_t)m * N + n;
+          if (direct) *pp += acc[i][j][r];
+          else *pp = acc[i][j][r];
+        }
+      }
+    }
+}
+
 // G[e] += Σ_s slab[s][e]  (vectorised, fixed order)
 __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restrict__ slab, float* __restrict__ g,
                                                           int64_t n4, int splits, int64_t stride4) {
@@ -607,55 +501,27 @@ void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad, int64_t t
   }
   const int direct = splits == 1 ? 1 : 0;
   if (T == 256) {
-    // variant: 0 = register staging, 1 = LDS-DMA double buffer (BK 64), 2 = LDS-DMA ring
-    // (BK 32 x 4 stages; default, fastest measured), 3 = LDS-DMA ring (BK 32 x 5 stages),
-    // 4 = ring with 16x16x32 MFMAs (default), 5 = the same with 5 stages.
-    // GPT-2 124M, K = 65 536 (TF): qkv 703/809/863/873, proj 683/766/774/766,
-    // fc 792/911/962/956, fc2 829/954/984/960, lm_head 911/1019/1032/1024.
+    // variant 6 (default): ring16o; 4: ring16 (per-lane 64-bit DMA addresses and fragment
+    // address math in the loop; kept for A/B). v4 / v6 (TF): qkv 879/959, proj 822/914,
+    // fc 1006/1089, fc2 1020/1058, lm_head 1128/1255 (bench/wgrad_variants.py,
+    // profiles/wgrad_variants_r2.log; s_setprio around the MFMA clusters: 909/850/1067/1045/1162).
+    TORCH_CHECK(variant == 4 || variant == 6, "wgrad: variant must be 4 or 6");
+    constexpr int lds = 4 * 2 * BK2 * 512;
     static bool attr_set = false;
     if (!attr_set) {
-      const int l2 = 2 * 2 * BK2 * 512;
-      hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad256_kernel<true>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, l2);
-      hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad256_kernel<false>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, l2);
-      hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad256_ring_kernel<32, 4>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, 4 * 2 * 32 * 512);
-      hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad256_ring_kernel<32, 5>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, 5 * 2 * 32 * 512);
-      hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad256_ring16_kernel<32, 4>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, 4 * 2 * 32 * 512);
-      hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad256_ring16_kernel<32, 5>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, 5 * 2 * 32 * 512);
+      hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad256_ring16_kernel<BK2, 4>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad256_ring16o_kernel<BK2, 4>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       attr_set = true;
     }
     const int lda = (int)dy.stride(0), ldb = (int)x.stride(0);
-    switch (variant) {
-      case 0:
-        hipLaunchKernelGGL(wgrad256_kernel<false>, dim3(nwg), dim3(512), 2 * 2 * BK2 * 512, stream, a, b, dst, M, N,
-                           K, lda, ldb, klen, tiles_m, tiles_n, direct);
-        break;
-      case 1:
-        hipLaunchKernelGGL(wgrad256_kernel<true>, dim3(nwg), dim3(512), 2 * 2 * BK2 * 512, stream, a, b, dst, M, N,
-                           K, lda, ldb, klen, tiles_m, tiles_n, direct);
-        break;
-      case 2:
-        hipLaunchKernelGGL((wgrad256_ring_kernel<32, 4>), dim3(nwg), dim3(512), 4 * 2 * 32 * 512, stream, a, b, dst,
-                           M, N, K, lda, ldb, klen, tiles_m, tiles_n, direct);
-        break;
-      case 3:
-        hipLaunchKernelGGL((wgrad256_ring_kernel<32, 5>), dim3(nwg), dim3(512), 5 * 2 * 32 * 512, stream, a, b, dst,
-                           M, N, K, lda, ldb, klen, tiles_m, tiles_n, direct);
-        break;
-      case 4:
-        hipLaunchKernelGGL((wgrad256_ring16_kernel<32, 4>), dim3(nwg), dim3(512), 4 * 2 * 32 * 512, stream, a, b,
-                           dst, M, N, K, lda, ldb, klen, tiles_m, tiles_n, direct);
-        break;
-      default:
-        hipLaunchKernelGGL((wgrad256_ring16_kernel<32, 5>), dim3(nwg), dim3(512), 5 * 2 * 32 * 512, stream, a, b,
-                           dst, M, N, K, lda, ldb, klen, tiles_m, tiles_n, direct);
-        break;
-    }
+    if (variant == 4)
+      hipLaunchKernelGGL((wgrad256_ring16_kernel<BK2, 4>), dim3(nwg), dim3(512), lds, stream, a, b, dst, M, N, K,
+                         lda, ldb, klen, tiles_m, tiles_n, direct);
+    else
+      hipLaunchKernelGGL((wgrad256_ring16o_kernel<BK2, 4>), dim3(nwg), dim3(512), lds, stream, a, b, dst, M, N, K,
+                         lda, ldb, klen, tiles_m, tiles_n, direct);
   } else {
     hipLaunchKernelGGL(wgrad_kernel, dim3(nwg), dim3(256), 0, stream, a, b, dst, M, N, K, (int)dy.stride(0),
                        (int)x.stride(0), klen, tiles_m, tiles_n, direct);
