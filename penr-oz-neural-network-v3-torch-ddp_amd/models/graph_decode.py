@@ -192,6 +192,21 @@ class GPTDecodeProgram:
         return self._linear(add_ln(delta, wf, bf, ef, dbias), sp.head)
 
 
+def _packed_gate_up(mlp):
+    """The [gate; up] weight of one gated MLP as one contiguous tensor, built once per weight
+    version and cached on the module, so every decoder of the model shares one copy (no autograd
+    graph: built under no_grad)."""
+    g, u = mlp.gate_proj.weight, mlp.up_proj.weight
+    key = (g.data_ptr(), g._version, u.data_ptr(), u._version)
+    hit = mlp.__dict__.get("_packed_gu")
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    with torch.no_grad():
+        gu = torch.cat([g, u]).contiguous()
+    mlp.__dict__["_packed_gu"] = (key, gu)
+    return gu
+
+
 class GemmaDecodeProgram:
     """One decode step of a Gemma-family bf16 model (``models/hf.py`` layer list) as an explicit
     kernel sequence.
@@ -219,7 +234,7 @@ class GemmaDecodeProgram:
             self.blocks.append(dict(
                 in_norm=in_norm, qkv=qkv.weight, attn=attn, o=o.weight, pre_mlp=pre_mlp, mode=mode,
                 post_attn=b.post_attn_norm, post_mlp=b.post_mlp_norm,
-                gu=torch.cat([mlp.gate_proj.weight, mlp.up_proj.weight]).contiguous(), down=mlp.down_proj.weight,
+                gu=_packed_gate_up(mlp), down=mlp.down_proj.weight,
                 kind=act_ops._GATED[mlp.act_kind], inter=mlp.gate_proj.out_features))
 
     @staticmethod

@@ -168,3 +168,21 @@ def test_gatedmlp_activation_variants(act, fn):
     x = torch.randn(2, 8)
     ref = m.down_proj(fn(m.gate_proj(x)) * m.up_proj(x))
     assert torch.allclose(m(x), ref, atol=1e-6)
+
+
+def test_packed_gate_up_is_shared_and_tracks_weight_versions():
+    """The Gemma decode program's fused [gate; up] weight is built once per weight version and
+    shared by every decoder of the model (advisor: one copy per decoder)."""
+    import torch
+    from penroz.models import layers as L
+    from penroz.models.graph_decode import _packed_gate_up
+    mlp = L.GatedMLP(16, 32)
+    a = _packed_gate_up(mlp)
+    assert not a.requires_grad and a.shape == (64, 16)
+    assert _packed_gate_up(mlp) is a
+    torch.testing.assert_close(a, torch.cat([mlp.gate_proj.weight, mlp.up_proj.weight]).detach())
+    with torch.no_grad():
+        mlp.up_proj.weight.add_(1.0)  # an optimizer step bumps the version
+    b = _packed_gate_up(mlp)
+    assert b is not a
+    torch.testing.assert_close(b[32:], mlp.up_proj.weight.detach())
