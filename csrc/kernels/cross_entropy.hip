@@ -2,7 +2,7 @@
 //
 // One 1024-thread workgroup (16 waves) per row. The row (V bf16, e.g. 50304 × 2 B = 98 KiB)
 // is read ONCE into registers — 8 elements (16 B) per chunk, CPT chunks per thread, chunk k of
-// thread t covers elements 8·(t + 1024·k) — i.e. ≤ 28 VGPRs of packed bf16 per lane at GPT-2's
+// thread t covers elements 8·(t + 1024·k) — i.e. 56 fp32 VGPRs per lane at GPT-2's
 // vocabulary. The register file (512 KiB/CU) holds two rows per CU at once, more than LDS
 // (160 KiB) could. max → Σexp → log-sum-exp are block reductions; the loss needs only the
 // target logit; the gradient (softmax − onehot)·scale is rounded to bf16 and stored over the
@@ -57,13 +57,18 @@ __global__ void __launch_bounds__(kCEThreads) ce_kernel(T* __restrict__ logits, 
     }
   }
   m = block_reduce(m, sh, true);
+  // v becomes exp(v - m) in the sum pass, so the gradient pass needs no second exponential:
+  // softmax = exp(v - m) / Σ
   float s = 0.f;
 #pragma unroll
   for (int k = 0; k < CPT; ++k) {
     const int c = 8 * (t + kCEThreads * k);
     if (c < V) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s += __expf(v[k][j] - m);
+      for (int j = 0; j < 8; ++j) {
+        v[k][j] = __expf(v[k][j] - m);
+        s += v[k][j];
+      }
     }
   }
   s = block_reduce(s, sh, false);
@@ -72,6 +77,7 @@ __global__ void __launch_bounds__(kCEThreads) ce_kernel(T* __restrict__ logits, 
   if (t == 0) loss[row] = valid ? lse - to_f(rp[tgt]) : 0.f;
   if (scale == 0.f) return;
   const float sc = valid ? scale : 0.f;
+  const float ps = sc / s;
   __syncthreads();  // the target logit is read before any thread overwrites it
 #pragma unroll
   for (int k = 0; k < CPT; ++k) {
@@ -79,7 +85,7 @@ __global__ void __launch_bounds__(kCEThreads) ce_kernel(T* __restrict__ logits, 
     if (c < V) {
       float g[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] = (__expf(v[k][j] - lse) - (c + j == tgt ? 1.f : 0.f)) * sc;
+      for (int j = 0; j < 8; ++j) g[j] = fmaf(v[k][j], ps, c + j == tgt ? -sc : 0.f);
       Vec8<T>::store(rp + c, g);
     }
   }
