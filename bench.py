@@ -24,7 +24,8 @@ Extra fields (outside the timed region):
   * ``comm``: bucket plan, wire dtype, transport, RCCL version, ranks seen by the communicator,
     and ``allreduce_exposed_ms`` = ms/step of the timed run minus ms/step of a few further
     steps with the gradient all-reduce switched off (the part of the collective NOT hidden
-    behind the backward);
+    behind the backward), and ``probe_busbw_GBps`` = ring bus bandwidth of bare all-reduces of
+    one default-size bucket (RCCL over xGMI at N > 1; compare 7 links × ≈153 GB/s);
   * ``vs_reference_eager_same_gpu``: the same config through the ``reference`` engine (stock
     PyTorch eager + autocast + foreach AdamW, the reference's semantics) measured in this same
     process right after (1 GPU only; ``--ref-steps 0`` skips it).
@@ -106,6 +107,9 @@ def parse_args(argv=None):
     ap.add_argument("--ref-steps", type=int, default=4,
                     help="steps of the reference engine measured after the run for vs_reference_eager_same_gpu "
                          "(1 GPU, gpt2-124m only; 0 = skip)")
+    ap.add_argument("--comm-probe-iters", type=int, default=5,
+                    help="world > 1: time this many bare all-reduces of one gradient bucket after the timed "
+                         "run and report the bus bandwidth in comm (0 = skip)")
     ap.add_argument("--nocomm-steps", type=int, default=4,
                     help="steps without the gradient all-reduce, for allreduce_exposed_ms (world > 1; 0 = skip)")
     ap.add_argument("--via-runtime", action="store_true",
@@ -205,6 +209,22 @@ def _comm_info(runner, world: int) -> dict:
                      "transport": "native-rccl" if red._native is not None else red.backend,
                      "grad_mb": round(sum(sizes), 2)})
     return info
+
+
+def _allreduce_probe(device, world: int, iters: int) -> dict:
+    """Bare in-place AVG all-reduces of one default-size fp32 gradient bucket (RCCL over xGMI on
+    the GPU; a 4 MB bucket over gloo on the CPU): ms per call and ring bus bandwidth
+    (bytes · 2(n−1)/n per second, the per-rank link traffic), max over ranks."""
+    from penroz.parallel.reducer import DEFAULT_BUCKET_MB
+    mb = DEFAULT_BUCKET_MB if device.type == "cuda" else 4
+    buf = torch.ones(int(mb * 2**20) // 4, device=device, dtype=torch.float32)
+    op = dist.ReduceOp.AVG if device.type == "cuda" else dist.ReduceOp.SUM
+    for _ in range(2):
+        dist.all_reduce(buf, op=op)
+    dt, _ = _timed(lambda i: dist.all_reduce(buf, op=op), iters, world, device)
+    t = dt / iters
+    return {"probe_allreduce_mb": mb, "probe_allreduce_ms": t * 1e3,
+            "probe_busbw_GBps": buf.numel() * 4 * 2 * (world - 1) / world / t / 1e9}
 
 
 def _timed(step, n, world, device):
@@ -371,6 +391,8 @@ def run_rank(args):
         comm["allreduce_exposed_ms"] = max(0.0, ms - comm["ms_per_step_without_allreduce"])
     elif world == 1:
         comm["allreduce_exposed_ms"] = 0.0
+    if world > 1 and args.comm_probe_iters > 0:  # outside the timed region
+        comm.update(_allreduce_probe(device, world, args.comm_probe_iters))
 
     if args.profile:  # outside the timed region
         from penroz.utils.profiling import profile_steps

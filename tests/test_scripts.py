@@ -88,6 +88,7 @@ def test_bench_self_launches_ranks_cpu_gloo():
     assert d["config"]["global_batch"] == 2 * d["config"]["micro_batch_per_gpu"]
     assert d["comm"]["nranks"] == 2 and d["comm"]["transport"] == "gloo" and d["comm"]["buckets"] >= 1
     assert d["comm"]["allreduce_exposed_ms"] >= 0.0
+    assert d["comm"]["probe_allreduce_mb"] == 4 and d["comm"]["probe_busbw_GBps"] > 0
     assert d["steps"] == 2 and d["warmup"] == 1 and d["value"] > 0
 
 
