@@ -46,3 +46,19 @@ if "attn" in which:
     emit(kernel="flash_fwd", native_us=round(tf * 1e6, 1), native_TF=round(fl / tf / 1e12, 1),
          sdpa_us=round(ts * 1e6, 1), sdpa_TF=round(fl / ts / 1e12, 1))
     emit(kernel="flash_bwd", native_us=round(tb * 1e6, 1), native_TF=round(2.5 * fl / tb / 1e12, 1))
+if "ce" in which:
+    from penroz.ops import fused as Fu
+    V = 50304
+    logits = (torch.randn(N, V, device="cuda") * 3).to(torch.bfloat16)
+    tgt = torch.randint(0, V, (N,), device="cuda")
+    buf = logits.clone()
+    t = timeit(lambda: Fu.cross_entropy_fwd_bwd(buf, tgt, 1.0 / N), iters=5, warmup=2)
+    emit(kernel="cross_entropy", us=round(t * 1e6, 1),
+         TBps=round(2 * N * V * 2 / t / 1e12, 2))
+if "adam" in which:
+    n = 163_087_104
+    p, g, m, v = (torch.randn(n, device="cuda") for _ in range(4))
+    v.abs_()
+    sh = torch.empty(n, device="cuda", dtype=torch.bfloat16)
+    t = timeit(lambda: k.adamw_step(p, g, m, v, sh, 6e-4, 0.9, 0.95, 1e-8, 0.01, 10, 1.0, False))
+    emit(kernel="adamw_flat", n=n, us=round(t * 1e6, 1), TBps=round(30 * n / t / 1e12, 2))
