@@ -532,13 +532,31 @@ class NeuralNetworkModel(nn.Module):
                 dist.destroy_process_group()
 
     @staticmethod
+    def amp_dtype(device) -> torch.dtype | None:
+        """Autocast dtype on the GPU, as the reference picks it (``neural_net_model.py:570-575``):
+        bf16 where the device supports it (every MI355X), else fp16 with a GradScaler.
+        ``PENROZ_AMP_DTYPE=fp16`` forces the fp16 + GradScaler path (generic engine) for parity
+        runs of that fallback; ``bf16`` forces bf16."""
+        if device.type != "cuda":
+            return None
+        env = os.environ.get("PENROZ_AMP_DTYPE", "auto").lower()
+        if env in ("fp16", "float16", "half"):
+            return torch.float16
+        if env in ("bf16", "bfloat16"):
+            return torch.bfloat16
+        return torch.bfloat16 if torch.cuda.is_bf16_supported() else torch.float16
+
+    @staticmethod
     def _autocast(device):
-        if device.type == "cuda":
-            return torch.amp.autocast("cuda", dtype=torch.bfloat16)
+        dtype = NeuralNetworkModel.amp_dtype(device)
+        if dtype is not None:
+            return torch.amp.autocast("cuda", dtype=dtype)
         return nullcontext()
 
     def _engine(self, device) -> str:
         eng = os.environ.get("PENROZ_ENGINE", "auto")
+        if self.amp_dtype(device) == torch.float16:
+            return "reference" if eng == "reference" else "generic"  # the fused executor is bf16-only
         if eng == "auto":
             from penroz.models.executor import GPTExecutor
             return "fused" if device.type == "cuda" and GPTExecutor.match(self) is not None else "generic"
@@ -665,6 +683,8 @@ class _GenericRunner:
         self.device = device
         self.reference = reference
         self.amp = NeuralNetworkModel._autocast(device)
+        # fp16 autocast needs loss scaling (reference neural_net_model.py:573-575, 650-675)
+        self.scaler = torch.amp.GradScaler("cuda") if NeuralNetworkModel.amp_dtype(device) == torch.float16 else None
         self.reducer = None
         self.ddp_model = None
         if distributed:
@@ -701,13 +721,23 @@ class _GenericRunner:
             for a in acts:
                 a.retain_grad()
             self._acts.extend(acts)
-        scaled.backward()
+        (self.scaler.scale(scaled) if self.scaler is not None else scaled).backward()
         if last and self.reducer is not None:
             self.reducer.finish()
         return scaled.detach().float()
 
     def step(self):
-        self.model.optimizer.step()
+        if self.scaler is None:
+            self.model.optimizer.step()
+            return
+        # unscale + inf/nan check, skipped step on overflow; the captured activation gradients
+        # (dashboard stats) were scaled too: unscale them with the scale of this step
+        self.scaler.step(self.model.optimizer)
+        inv = 1.0 / self.scaler.get_scale()
+        for a in self._acts:
+            if a.grad is not None:
+                a.grad.mul_(inv)
+        self.scaler.update()
 
     @staticmethod
     def grad_of(p):

@@ -49,7 +49,8 @@ def wgrad(dy: Tensor, x: Tensor, grad: Tensor) -> None:
 # PyTorch / HIP / hipBLASLt / rocBLAS versions and the gfx950 arch at load; a mismatch is refused
 # by torch and the heuristic picks stay). Loaded read-only (no tuning at run time; shapes not in
 # the file keep the default solution). PENROZ_TUNED_GEMMS=0 disables.
-TUNED_GEMM_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned", "tunableop_gfx950.csv")
+TUNED_GEMM_FILE = os.environ.get("PENROZ_TUNED_GEMM_FILE") or os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), "tuned", "tunableop_gfx950.csv")
 _tuned_state: dict = {}
 
 

@@ -173,3 +173,21 @@ def test_shm_detection(monkeypatch):
     import platform
     monkeypatch.setattr(platform, "system", lambda: "Plan9")
     assert ckpt.detect_shm_path() == __import__("tempfile").gettempdir()
+
+
+def test_amp_dtype_selection(monkeypatch):
+    """bf16 where supported, fp16 (+ GradScaler in the generic runner) otherwise, as the reference
+    (neural_net_model.py:570-575); PENROZ_AMP_DTYPE overrides; CPU has no autocast."""
+    import torch
+    from penroz.models.model import NeuralNetworkModel as M
+    cuda = torch.device("cuda")
+    assert M.amp_dtype(torch.device("cpu")) is None
+    monkeypatch.setattr(torch.cuda, "is_bf16_supported", lambda *a, **k: True)
+    assert M.amp_dtype(cuda) == torch.bfloat16
+    monkeypatch.setattr(torch.cuda, "is_bf16_supported", lambda *a, **k: False)
+    assert M.amp_dtype(cuda) == torch.float16
+    monkeypatch.setenv("PENROZ_AMP_DTYPE", "bf16")
+    assert M.amp_dtype(cuda) == torch.bfloat16
+    monkeypatch.setenv("PENROZ_AMP_DTYPE", "fp16")
+    monkeypatch.setattr(torch.cuda, "is_bf16_supported", lambda *a, **k: True)
+    assert M.amp_dtype(cuda) == torch.float16

@@ -49,6 +49,23 @@ def test_fused_matches_generic_engine_losses(workdir):
         assert abs(pa["cost"] - pb["cost"]) < 0.05, (pa["cost"], pb["cost"])
 
 
+def test_fp16_gradscaler_fallback(workdir, monkeypatch):
+    """The reference's fallback when bf16 is unsupported: fp16 autocast + GradScaler (forced with
+    PENROZ_AMP_DTYPE=fp16; reference neural_net_model.py:570-575, 650-675)."""
+    loaders.synthetic_shards("ds", 1, 1 << 15, 512)
+    monkeypatch.setenv("PENROZ_AMP_DTYPE", "fp16")
+    m = gpt().to("cuda")
+    dev = torch.device("cuda")
+    assert NeuralNetworkModel.amp_dtype(dev) == torch.float16 and m._engine(dev) == "generic"
+    from penroz.models.model import _make_runner
+    r = _make_runner(m, m._engine(dev), dev, False)
+    assert r.scaler is not None and r.scaler.get_scale() > 1.0
+    m.train_model("ds", 0, 6, 8, 64, 4)
+    costs = [p["cost"] for p in m.progress]
+    assert m.status["code"] == "Trained" and all(c == c for c in costs) and costs[-1] < costs[0], costs
+    assert all(torch.isfinite(p).all() for p in m.parameters())
+
+
 def test_gpu_generation_matches_cpu():
     m = gpt()
     cpu = m.generate_tokens([[1, 2, 3, 4]], 32, 12, temperature=0.0)
