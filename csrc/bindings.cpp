@@ -131,7 +131,7 @@ PYBIND11_MODULE(penroz_kernels, m) {
         pybind11::arg("out"), pybind11::arg("ws"), pybind11::arg("cnt"), pybind11::arg("splitk") = 0,
         "decode-shaped out[M<=64, N] = x·wᵀ (+bias), bf16; returns the split-K factor used");
   m.def("wgrad_gemm", &wgrad_gemm, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("grad"),
-        pybind11::arg("tile") = 256, pybind11::arg("variant") = 6);
+        pybind11::arg("tile") = 256, pybind11::arg("variant") = 8);
   m.def("flash_attn_fwd", &flash_attn_fwd);
   m.def("flash_bwd_variant", &flash_bwd_variant, pybind11::arg("variant") = 0,
         "select the dK/dV kernel (1 register-staged, 2 LDS-DMA pipelined); returns the previous one");

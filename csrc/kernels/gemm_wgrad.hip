@@ -4,7 +4,7 @@
 // operands are row-major in the reduction dimension k (tokens), which is what makes this GEMM
 // awkward for library kernels at GPT-2 shapes (hipBLASLt measured 270–980 TF here, 410–1000 TF
 // tuned: profiles/wgrad_native_vs_hipblaslt_r2.log).  Design (default path =
-// wgrad256_ring16o_kernel<32, 4>, variant 6):
+// wgrad256_ring16o_kernel<32, 4, true>, variant 8):
 //   * 256×256 output tile per 512-thread workgroup (8 waves as 2×4, each 128×64 = 8×4 MFMA
 //     16x16x32 tiles), one workgroup per CU (128 KiB LDS);
 //   * operand tiles arrive by LDS-DMA (global_load_lds_dwordx4, issued in inline asm so the
@@ -295,7 +295,7 @@ __global__ void __launch_bounds__(512, 1) wgrad256_ring16_kernel(const bf16* __r
     }
 }
 
-// ---- ring16 with scalar-base DMA and precomputed fragment offsets (variant 6, default) ------
+// ---- ring16 with scalar-base DMA and precomputed fragment offsets (variant 6; + PF: 8, default) --
 // The ring16 pipeline with the per-step address work moved off the vector ALUs: each DMA piece
 // is global_load_lds with a wave-uniform SGPR row base (A + k·lda, advanced by scalar adds) and
 // a per-lane 32-bit offset fixed for the whole kernel; tile columns past M / N are clamped to
@@ -304,7 +304,15 @@ __global__ void __launch_bounds__(512, 1) wgrad256_ring16_kernel(const bf16* __r
 // per-lane LDS offsets computed once (off512b is periodic in 16 rows, so the k slice and the
 // second half-read are immediates) and the loop is unrolled by the ring depth, making every
 // stage base a constant. (s_setprio around the MFMA clusters measured 4 % slower.)
-template <int BKT, int NBUF>
+template <int I, int N, typename F>
+__device__ __forceinline__ void unroll_steps(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    unroll_steps<I + 1, N>(f);
+  }
+}
+
+template <int BKT, int NBUF, bool PF = false>
 __global__ void __launch_bounds__(512, 1) wgrad256_ring16o_kernel(const bf16* __restrict__ A,
                                                                   const bf16* __restrict__ B,
                                                                   float* __restrict__ out, int M, int N, int K,
@@ -315,6 +323,7 @@ __global__ void __launch_bounds__(512, 1) wgrad256_ring16o_kernel(const bf16* __
   constexpr int PIECES = BKT / 16;
   constexpr int G = 2 * PIECES;
   static_assert(BKT % 32 == 0 && NBUF == 4 && (NBUF - 2) * G <= 63, "ring geometry");
+  static_assert(!PF || (BKT == 32 && NBUF == 4), "fragment prefetch: 32-deep stages, 4-stage ring");
   const int nwg = gridDim.x, wg = blockIdx.x;
   const int xcd = wg & 7, qd = nwg >> 3, rd = nwg & 7;
   const int id = (xcd < rd ? xcd * (qd + 1) : rd * (qd + 1) + (xcd - rd) * qd) + (wg >> 3);
@@ -387,15 +396,59 @@ __global__ void __launch_bounds__(512, 1) wgrad256_ring16o_kernel(const bf16* __
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nsteps = (k1 - k0 + BKT - 1) / BKT;
+  // PF (fragment prefetch): each step's MFMAs run on fragments read during the PREVIOUS step, so
+  // no wave starts a step waiting on LDS reads after the barrier; the barrier at the end of step
+  // st must then publish stage st+2 (read during step st+1), leaving one stage in flight
+  constexpr int WAITN = PF ? (NBUF - 3) * G : (NBUF - 2) * G;
 #pragma unroll
   for (int t = 0; t < NBUF - 1; ++t) dma(t);
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NBUF - 2) * G) : "memory");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WAITN) : "memory");
   __syncthreads();
+  constexpr int PFA = 2;  // A fragments read one step ahead
+  uint4 ca[PFA], cb[4];  // PF: the current step's prefetched fragments
+  if constexpr (PF) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cb[j] = frag(smem2 + TILE, fb[j]);
+#pragma unroll
+    for (int i = 0; i < PFA; ++i) ca[i] = frag(smem2, fa[i]);
+  }
   auto step = [&](int st, auto stage_tag) {
     constexpr int ST = decltype(stage_tag)::value;
     dma(st + NBUF - 1);  // into the stage consumed at step st-1 (freed by its barrier)
     const char* At = smem2 + ST * 2 * TILE;
     const char* Bt = At + TILE;
+    if constexpr (PF) {
+      // the B fragments and the first PFA A fragments come from the previous step; the other A
+      // fragments of this stage are read under those MFMAs, then next stage's prefetch is read
+      // under the rest (all 8 A fragments ahead would need 48 more VGPRs: 31 spilled)
+      const char* An = smem2 + ((ST + 1) % NBUF) * 2 * TILE;  // published by the previous barrier
+      uint4 la[8 - PFA];
+#pragma unroll
+      for (int i = PFA; i < 8; ++i) la[i - PFA] = frag(At, fa[i]);
+#pragma unroll
+      for (int i = 0; i < PFA; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(ca[i], cb[j], acc[i][j]);
+      uint4 nb[4], na[PFA];
+#pragma unroll
+      for (int i = PFA; i < 8; ++i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(la[i - PFA], cb[j], acc[i][j]);
+        if (i == PFA) {
+#pragma unroll
+          for (int q = 0; q < PFA; ++q) na[q] = frag(An, fa[q]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) nb[j] = frag(An + TILE, fb[j]);
+#pragma unroll
+      for (int i = 0; i < PFA; ++i) ca[i] = na[i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) cb[j] = nb[j];
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WAITN) : "memory");  // stage st+2 landed
+      __syncthreads();
+      return;
+    }
 #pragma unroll
     for (int s = 0; s < BKT / 32; ++s) {
       uint4 bf[4];
@@ -412,15 +465,11 @@ __global__ void __launch_bounds__(512, 1) wgrad256_ring16o_kernel(const bf16* __
     __syncthreads();
   };
   int st = 0;
-  for (; st + NBUF <= nsteps; st += NBUF) {
-    step(st, std::integral_constant<int, 0>{});
-    step(st + 1, std::integral_constant<int, 1>{});
-    step(st + 2, std::integral_constant<int, 2>{});
-    step(st + 3, std::integral_constant<int, 3>{});
-  }
-  if (st < nsteps) step(st, std::integral_constant<int, 0>{});
-  if (st + 1 < nsteps) step(st + 1, std::integral_constant<int, 1>{});
-  if (st + 2 < nsteps) step(st + 2, std::integral_constant<int, 2>{});
+  for (; st + NBUF <= nsteps; st += NBUF)  // unrolled by the ring depth: stage bases are immediates
+    unroll_steps<0, NBUF>([&](auto ic) { step(st + decltype(ic)::value, ic); });
+  unroll_steps<0, NBUF - 1>([&](auto ic) {
+    if (st + decltype(ic)::value < nsteps) step(st + decltype(ic)::value, ic);
+  });
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the zero-page prefetches
   float* o = direct ? out : out + (size_t)split * M * N;
 #pragma unroll
@@ -501,11 +550,14 @@ void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad, int64_t t
   }
   const int direct = splits == 1 ? 1 : 0;
   if (T == 256) {
-    // variant 6 (default): ring16o; 4: ring16 (per-lane 64-bit DMA addresses and fragment
+    // variant 6: ring16o; 4: ring16 (per-lane 64-bit DMA addresses and fragment
     // address math in the loop; kept for A/B). v4 / v6 (TF): qkv 879/959, proj 822/914,
     // fc 1006/1089, fc2 1020/1058, lm_head 1128/1255 (bench/wgrad_variants.py,
     // profiles/wgrad_variants_r2.log; s_setprio around the MFMA clusters: 909/850/1067/1045/1162).
-    TORCH_CHECK(variant == 4 || variant == 6, "wgrad: variant must be 4 or 6");
+    // 8 (default): ring16o with the B and first A fragments read one step ahead (PF): 14.54 vs
+    // 14.68 ms/step of wgrad (profiles/wgrad_variants_r2b.log; a 64-deep 2-stage ring measured
+    // 16.23: the per-step barrier is not what bounds this kernel)
+    TORCH_CHECK(variant == 4 || variant == 6 || variant == 8, "wgrad: variant must be 4, 6 or 8");
     constexpr int lds = 4 * 2 * BK2 * 512;
     static bool attr_set = false;
     if (!attr_set) {
@@ -513,12 +565,17 @@ void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad, int64_t t
                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad256_ring16o_kernel<BK2, 4>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad256_ring16o_kernel<BK2, 4, true>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       attr_set = true;
     }
     const int lda = (int)dy.stride(0), ldb = (int)x.stride(0);
     if (variant == 4)
       hipLaunchKernelGGL((wgrad256_ring16_kernel<BK2, 4>), dim3(nwg), dim3(512), lds, stream, a, b, dst, M, N, K,
                          lda, ldb, klen, tiles_m, tiles_n, direct);
+    else if (variant == 8)
+      hipLaunchKernelGGL((wgrad256_ring16o_kernel<BK2, 4, true>), dim3(nwg), dim3(512), lds, stream, a, b, dst, M,
+                         N, K, lda, ldb, klen, tiles_m, tiles_n, direct);
     else
       hipLaunchKernelGGL((wgrad256_ring16o_kernel<BK2, 4>), dim3(nwg), dim3(512), lds, stream, a, b, dst, M, N, K,
                          lda, ldb, klen, tiles_m, tiles_n, direct);

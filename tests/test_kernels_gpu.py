@@ -487,7 +487,7 @@ def test_tensor_stats():
     _close(hist.cpu(), h.hist, 2e-3, 0.01)
 
 
-@pytest.mark.parametrize("tile,variant", [(128, 0), (256, 4), (256, 6)])
+@pytest.mark.parametrize("tile,variant", [(128, 0), (256, 4), (256, 6), (256, 8)])
 @pytest.mark.parametrize("K,M,N", [(65536, 2304, 768), (4096, 768, 768), (1000, 200, 136), (8192, 50304, 768), (3000, 1600, 6400)])
 def test_wgrad_gemm(K, M, N, tile, variant):
     from penroz.ops import gemm as G
@@ -759,7 +759,7 @@ def test_embedding_dropout():
     _close(dwpe, w2.grad, 1e-4)
 
 
-@pytest.mark.parametrize("tile,variant", [(128, 0), (256, 4), (256, 6)])
+@pytest.mark.parametrize("tile,variant", [(128, 0), (256, 4), (256, 6), (256, 8)])
 @pytest.mark.parametrize("M", [50257, 1001])
 def test_wgrad_gemm_padded_rows(M, tile, variant):
     """HF GPT-2 vocab (V = 50257): dlogits rows padded to a multiple of 8 (zero pad columns, as the
