@@ -296,8 +296,13 @@ class GPTExecutor:
             for w, t in self._tw.values():
                 k.transpose_bf16(self.bf16(w), t)
             return
+        # the copies must see this step's weights: the side stream waits for everything the main
+        # stream has queued (the optimizer's shadow refresh). The main stream is captured BEFORE
+        # entering the side-stream context — inside it, current_stream() IS the side stream, and
+        # waiting on it orders nothing (that was a race: transposes of a half-refreshed shadow)
+        main = torch.cuda.current_stream(self.device)
         with torch.cuda.stream(side):
-            side.wait_stream(torch.cuda.current_stream(self.device))
+            side.wait_stream(main)
             for w, t in self._tw.values():
                 k.transpose_bf16(self.bf16(w), t)
             self._t_ready = torch.cuda.Event()

@@ -20,6 +20,8 @@ from penroz.ops._ext import use_kernels, kernels
 # "auto"/"1": the native kernel (faster than hipBLASLt on every measured GPT-2 shape);
 # "0": hipBLASLt (A/B switch for benchmarking).
 NATIVE_WGRAD = os.environ.get("PENROZ_NATIVE_WGRAD", "auto")
+# pipeline variant of the 256-tile kernel (csrc/kernels/gemm_wgrad.hip): 8 (default), 6, 4 — A/B knob
+WGRAD_VARIANT = int(os.environ.get("PENROZ_WGRAD_VARIANT", "8"))
 
 
 def _native_ok(m: int, n: int, lda: int | None = None) -> bool:
@@ -34,7 +36,7 @@ def reference_wgrad(dy: Tensor, x: Tensor, grad: Tensor) -> None:
 def wgrad(dy: Tensor, x: Tensor, grad: Tensor) -> None:
     if (use_kernels(dy) and _native_ok(dy.shape[1], x.shape[1], dy.stride(0)) and dy.dtype == torch.bfloat16
             and x.dtype == torch.bfloat16 and dy.stride(0) % 8 == 0 and x.stride(0) % 8 == 0):
-        kernels().wgrad_gemm(dy, x, grad)
+        kernels().wgrad_gemm(dy, x, grad, 256, WGRAD_VARIANT)
     elif dy.is_cuda:
         grad.add_(torch.mm(dy.t(), x, out_dtype=torch.float32))
     else:

@@ -201,3 +201,21 @@ def test_executor_chunked_head_matches_one_chunk(monkeypatch, V):
     assert abs(l1 - l2) < 1e-4 and abs(e1 - e2) < 1e-4, (l1, l2, e1, e2)
     rel = (g1 - g2).norm() / g1.norm()
     assert rel < 1e-3, rel
+
+
+def test_transposed_dgrad_weights_follow_the_main_stream():
+    """The side-stream transposes of the bf16 shadow (dgrad operands) are ordered after every
+    shadow write queued on the main stream (regression: the side stream once waited on itself,
+    so the copies could be taken from a half-refreshed shadow)."""
+    torch.manual_seed(0)
+    m = tiny().cuda()
+    ex = GPTExecutor(m, torch.device("cuda"))
+    ex.setup_training(False)
+    assert ex._tw, "transposed dgrad weights expected on the GPU"
+    torch.cuda.synchronize()
+    torch.cuda._sleep(200_000_000)  # keep the main stream busy, then rewrite the shadow behind it
+    ex.shadow.mul_(2.0)
+    ex._refresh_transposed()
+    torch.cuda.synchronize()
+    for w, t in ex._tw.values():
+        assert torch.equal(t, ex.bf16(w).t()), "transpose ran before the main stream's shadow write"
