@@ -63,6 +63,9 @@ void gemm_bf16(torch::Tensor a, torch::Tensor b, bool b_kn, c10::optional<torch:
 // skinny_gemm.hip
 int64_t skinny_gemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> bias, torch::Tensor out,
                     torch::Tensor ws, torch::Tensor cnt, int64_t splitk);
+void decode_ln_linear(torch::Tensor rin, c10::optional<torch::Tensor> delta, c10::optional<torch::Tensor> dbias,
+                      c10::optional<torch::Tensor> rout, torch::Tensor gamma, torch::Tensor beta, double eps,
+                      torch::Tensor w, c10::optional<torch::Tensor> bias, torch::Tensor out, int64_t act);
 // gemm_wgrad.hip
 void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad, int64_t tile, int64_t variant);
 // flash_attn.hip
@@ -130,6 +133,11 @@ PYBIND11_MODULE(penroz_kernels, m) {
   m.def("skinny_gemm", &skinny_gemm, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("bias"),
         pybind11::arg("out"), pybind11::arg("ws"), pybind11::arg("cnt"), pybind11::arg("splitk") = 0,
         "decode-shaped out[M<=64, N] = x·wᵀ (+bias), bf16; returns the split-K factor used");
+  m.def("decode_ln_linear", &decode_ln_linear, pybind11::arg("resid_in"), pybind11::arg("delta"),
+        pybind11::arg("dbias"), pybind11::arg("resid_out"), pybind11::arg("gamma"), pybind11::arg("beta"),
+        pybind11::arg("eps"), pybind11::arg("w"), pybind11::arg("bias"), pybind11::arg("out"), pybind11::arg("act") = 0,
+        "decode step: out = act(LN(resid_in + delta + dbias)·wᵀ + bias) for M <= 64 rows, K <= 1024; "
+        "resid_out receives the residual sum");
   m.def("wgrad_gemm", &wgrad_gemm, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("grad"),
         pybind11::arg("tile") = 256, pybind11::arg("variant") = 8);
   m.def("flash_attn_fwd", &flash_attn_fwd);

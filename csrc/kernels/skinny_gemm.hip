@@ -128,9 +128,204 @@ __global__ void __launch_bounds__(256) skinny_gemm_kernel(const bf16* __restrict
   }
 }
 
+// Decode-step linear with the residual add + LayerNorm fused in front and an optional GELU
+// behind: out = act(LN(resid_in + delta + dbias) · Wᵀ + bias), M ≤ 64 rows, K ≤ 1024. Every
+// workgroup normalises all M rows itself (one wave per row, the add+LayerNorm kernel's math:
+// fp32 two-pass statistics on the register copy) into a padded bf16 LDS image, then runs the
+// skinny main loop with its x fragments read from LDS; workgroup 0 also writes resid_out (the
+// fp32 residual stream after the add). It replaces add+LN → GEMM (→ GELU): 2-3 kernels of the
+// graph-replayed decode step, whose fixed per-kernel cost (~4.5 µs at batch 64) exceeds what
+// each of them computes. The redundant per-workgroup LayerNorm reads the rows from L2.
+// act: 0 none, 1 GELU (erf), 2 GELU (tanh), applied to the bf16-rounded linear output (the
+// rounding point of the unfused GEMM → GELU pair).
+template <int MB>
+__global__ void __launch_bounds__(256) decode_ln_linear_kernel(
+    const float* __restrict__ rin, const bf16* __restrict__ delta, const float* __restrict__ dbias,
+    float* __restrict__ rout, const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
+    const bf16* __restrict__ w, const bf16* __restrict__ bias, bf16* __restrict__ out, int64_t o_rs, int M, int N,
+    int K, int act) {
+  extern __shared__ __attribute__((aligned(16))) char dsm[];  // [MB*16][K + 8] bf16 | partial tiles
+  const int LDX = K + 8;  // +16 B per row: the 16 rows of a fragment read land on distinct banks
+  bf16* xs = reinterpret_cast<bf16*>(dsm);
+  float* red = reinterpret_cast<float*>(dsm + (size_t)MB * 16 * LDX * 2);
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const bool write_resid = rout != nullptr && blockIdx.x == 0;
+  // rows wid, wid+4, ...: a compile-time trip count, so the loads of later rows can be issued
+  // under the reductions of earlier ones (a runtime-bounded loop serialised one row's HBM/L2
+  // latency after another)
+#pragma unroll
+  for (int i = 0; i < MB * 4; ++i) {
+    const int m = wid + 4 * i;
+    bf16* xr = xs + (size_t)m * LDX;
+    if (m >= M) {
+      for (int c = 8 * lane; c < K; c += 512) *reinterpret_cast<uint4*>(xr + c) = uint4{0u, 0u, 0u, 0u};
+      continue;
+    }
+    const size_t base = (size_t)m * K;
+    float v[4][4];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = 4 * (lane + 64 * j);
+      if (c >= K) {
+        v[j][0] = v[j][1] = v[j][2] = v[j][3] = 0.f;
+        continue;
+      }
+      const float4_t r = *reinterpret_cast<const float4_t*>(rin + base + c);
+      v[j][0] = r[0]; v[j][1] = r[1]; v[j][2] = r[2]; v[j][3] = r[3];
+      if (delta) {
+        const uint2 u = *reinterpret_cast<const uint2*>(delta + base + c);
+        float d[4] = {__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                      __uint_as_float(u.y & 0xffff0000u)};
+        if (dbias) {
+          const float4_t e = *reinterpret_cast<const float4_t*>(dbias + c);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) d[k] += e[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[j][k] += d[k];
+        if (write_resid) *reinterpret_cast<float4_t*>(rout + base + c) = float4_t{v[j][0], v[j][1], v[j][2], v[j][3]};
+      }
+      s += v[j][0] + v[j][1] + v[j][2] + v[j][3];
+    }
+    const float mean = wave_sum(s) / K;
+    float ss = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float d = v[j][k] - mean;
+        ss += 4 * (lane + 64 * j) < K ? d * d : 0.f;
+      }
+    const float rstd = rsqrtf(wave_sum(ss) / K + eps);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = 4 * (lane + 64 * j);
+      if (c >= K) continue;
+      const float4_t g = *reinterpret_cast<const float4_t*>(gamma + c);
+      const float4_t b = *reinterpret_cast<const float4_t*>(beta + c);
+      *reinterpret_cast<uint2*>(xr + c) =
+          uint2{pack_bf16x2((v[j][0] - mean) * rstd * g[0] + b[0], (v[j][1] - mean) * rstd * g[1] + b[1]),
+                pack_bf16x2((v[j][2] - mean) * rstd * g[2] + b[2], (v[j][3] - mean) * rstd * g[3] + b[3])};
+    }
+  }
+  __syncthreads();
+
+  const int n0 = blockIdx.x * 16;
+  const int steps = K / 32;
+  const int s0 = steps * wid / 4, s1 = steps * (wid + 1) / 4;
+  const int r16 = lane & 15, kq = 8 * (lane >> 4);
+  const bf16* wp = w + (size_t)min(n0 + r16, N - 1) * K + kq;  // rows past N: clamped, never stored
+  const bf16* xl = xs + (size_t)r16 * LDX + kq;
+  sk_f32x4 acc[MB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) acc[mb] = (sk_f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int s = s0; s < s1; s += kSkU) {
+    sk_u32x4 wa[kSkU];
+#pragma unroll
+    for (int u = 0; u < kSkU; ++u) wa[u] = *reinterpret_cast<const sk_u32x4*>(wp + (size_t)min(s + u, s1 - 1) * 32);
+#pragma unroll
+    for (int u = 0; u < kSkU; ++u) {
+      if (s + u < s1) {
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) {
+          const sk_u32x4 xb = *reinterpret_cast<const sk_u32x4*>(xl + (size_t)mb * 16 * LDX + (s + u) * 32);
+          acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(sk_bf16x8, wa[u]),
+                                                            __builtin_bit_cast(sk_bf16x8, xb), acc[mb], 0, 0, 0);
+        }
+      }
+    }
+  }
+  sk_f32x4* r4 = reinterpret_cast<sk_f32x4*>(red);
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) r4[(wid * MB + mb) * 64 + lane] = acc[mb];
+  __syncthreads();
+  for (int it = t; it < MB * 64; it += 256) {
+    const int mb = it >> 6, ln = it & 63;
+    const sk_f32x4 v = r4[mb * 64 + ln] + r4[(MB + mb) * 64 + ln] + r4[(2 * MB + mb) * 64 + ln] +
+                       r4[(3 * MB + mb) * 64 + ln];
+    const int m = mb * 16 + (ln & 15), nb = n0 + 4 * (ln >> 4);
+    if (m >= M) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = nb + r;
+      if (n >= N) continue;
+      float y = v[r] + (bias ? bf2f(bias[n]) : 0.f);
+      if (act) y = gelu_f(bf2f(from_f<bf16>(y)), act - 1);
+      out[(size_t)m * o_rs + n] = from_f<bf16>(y);
+    }
+  }
+}
+
 }  // namespace penroz
 
 using namespace penroz;
+
+// out = act(LN(resid_in + delta + dbias) · Wᵀ + bias); resid_out (optional) receives the sum.
+void decode_ln_linear(torch::Tensor rin, c10::optional<torch::Tensor> delta, c10::optional<torch::Tensor> dbias,
+                      c10::optional<torch::Tensor> rout, torch::Tensor gamma, torch::Tensor beta, double eps,
+                      torch::Tensor w, c10::optional<torch::Tensor> bias, torch::Tensor out, int64_t act) {
+  TORCH_CHECK(rin.is_cuda() && rin.scalar_type() == torch::kFloat32 && rin.dim() == 2 && rin.is_contiguous(),
+              "decode_ln_linear: fp32 contiguous [M, K] residual");
+  const int M = rin.size(0), K = rin.size(1), N = w.size(0);
+  TORCH_CHECK(M >= 1 && M <= 64 && K % 32 == 0 && K <= 1024, "decode_ln_linear: M <= 64, K % 32 == 0, K <= 1024");
+  TORCH_CHECK(w.scalar_type() == torch::kBFloat16 && w.is_contiguous() && w.size(1) == K &&
+                  reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0, "decode_ln_linear: bf16 contiguous W [N, K]");
+  TORCH_CHECK(out.scalar_type() == torch::kBFloat16 && out.dim() == 2 && out.size(0) == M && out.size(1) == N &&
+                  out.stride(1) == 1, "decode_ln_linear: bf16 out [M, N]");
+  TORCH_CHECK(gamma.scalar_type() == torch::kFloat32 && beta.scalar_type() == torch::kFloat32 && gamma.numel() == K &&
+                  beta.numel() == K && gamma.is_contiguous() && beta.is_contiguous(), "decode_ln_linear: fp32 gamma/beta [K]");
+  TORCH_CHECK(act >= 0 && act <= 2, "decode_ln_linear: act 0 (none), 1 (GELU erf), 2 (GELU tanh)");
+  const bf16* dp = nullptr;
+  const float* dbp = nullptr;
+  float* rop = nullptr;
+  const bf16* bp = nullptr;
+  if (delta.has_value() && delta->defined()) {
+    TORCH_CHECK(delta->scalar_type() == torch::kBFloat16 && delta->is_contiguous() && delta->numel() == (int64_t)M * K,
+                "decode_ln_linear: bf16 contiguous delta [M, K]");
+    dp = reinterpret_cast<const bf16*>(delta->data_ptr());
+    TORCH_CHECK(rout.has_value() && rout->defined(), "decode_ln_linear: a residual add needs resid_out");
+  }
+  if (dbias.has_value() && dbias->defined()) {
+    TORCH_CHECK(dp && dbias->scalar_type() == torch::kFloat32 && dbias->is_contiguous() && dbias->numel() == K,
+                "decode_ln_linear: fp32 dbias [K] (with delta)");
+    dbp = dbias->data_ptr<float>();
+  }
+  if (rout.has_value() && rout->defined()) {
+    TORCH_CHECK(rout->scalar_type() == torch::kFloat32 && rout->is_contiguous() && rout->numel() == (int64_t)M * K &&
+                    rout->data_ptr() != rin.data_ptr(), "decode_ln_linear: fp32 resid_out [M, K], not aliasing resid_in");
+    rop = rout->data_ptr<float>();
+  }
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->scalar_type() == torch::kBFloat16 && bias->is_contiguous() && bias->numel() == N,
+                "decode_ln_linear: bf16 bias [N]");
+    bp = reinterpret_cast<const bf16*>(bias->data_ptr());
+  }
+  const int MB = M <= 16 ? 1 : M <= 32 ? 2 : 4;
+  const size_t lds = (size_t)MB * 16 * (K + 8) * 2 + (size_t)4 * MB * 64 * 16;
+  static bool attr_set = false;
+  if (!attr_set) {
+    const int mx = 4 * 16 * (1024 + 8) * 2 + 4 * 4 * 64 * 16;
+    hipFuncSetAttribute(reinterpret_cast<const void*>(decode_ln_linear_kernel<1>), hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(decode_ln_linear_kernel<2>), hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(decode_ln_linear_kernel<4>), hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+    attr_set = true;
+  }
+  auto stream = at::hip::getCurrentHIPStream();
+  const dim3 grid((N + 15) / 16);
+  const float* rp = rin.data_ptr<float>();
+  const float* gp = gamma.data_ptr<float>();
+  const float* bt = beta.data_ptr<float>();
+  auto wp = reinterpret_cast<const bf16*>(w.data_ptr());
+  auto op = reinterpret_cast<bf16*>(out.data_ptr());
+#define PENROZ_DLL(MBV)                                                                                             \
+  hipLaunchKernelGGL(decode_ln_linear_kernel<MBV>, grid, dim3(256), lds, stream, rp, dp, dbp, rop, gp, bt, (float)eps, \
+                     wp, bp, op, (int64_t)out.stride(0), M, N, K, (int)act)
+  if (MB == 1) PENROZ_DLL(1);
+  else if (MB == 2) PENROZ_DLL(2);
+  else PENROZ_DLL(4);
+#undef PENROZ_DLL
+}
 
 // splitk <= 0: chosen here (workgroups ~ 192 when the 16-column slices alone are too few).
 // ws: fp32 workspace (>= splitk * ceil(N/16) * MB * 256 floats when splitk > 1); cnt: int32

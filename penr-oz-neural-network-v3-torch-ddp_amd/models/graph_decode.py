@@ -61,6 +61,14 @@ FUSED_APPEND = os.environ.get("PENROZ_FUSED_APPEND", "1") != "0"
 # decode rows up to which the linears use the decode-shaped MFMA kernel instead of hipBLASLt
 # (measured: a win at batch 1, none at batch 64 — profiles/bench_r1_decode_graph.log)
 SKINNY_MAX_ROWS = int(os.environ.get("PENROZ_SKINNY_MAX_ROWS", "16"))
+# GPT decode program: residual add + LayerNorm fused in front of the QKV and fc GEMMs (and GELU
+# behind fc) in one decode-shaped kernel (csrc/kernels/skinny_gemm.hip decode_ln_linear); "0":
+# separate add+LN, GEMM and GELU kernels
+FUSED_LN_LINEAR = os.environ.get("PENROZ_DECODE_FUSED", "1") != "0"
+# ... up to this many decode rows: every workgroup normalises all rows itself, which pays off
+# while the rows are few (batch 1 / 4 / 8: -8 / -10 / -3 %) and loses from 16 rows on (+14 % at 16,
+# +69 % at 64): profiles/decode_fused_rows_r2.log
+FUSED_MAX_ROWS = int(os.environ.get("PENROZ_DECODE_FUSED_MAX_ROWS", "8"))
 
 
 class _GraphMode:
@@ -157,12 +165,19 @@ class GPTDecodeProgram:
             return torch.addmm(b, x, lin.weight.t())
         return torch.mm(x, lin.weight.t())
 
+    def _fused_ok(self, rows: int) -> bool:
+        sp = self.spec
+        return (FUSED_LN_LINEAR and 1 <= rows <= min(64, FUSED_MAX_ROWS) and sp.C % 32 == 0 and sp.C <= 1024
+                and sp.gelu_approx in ("none", "tanh") and _ext.available())
+
     def forward(self, idx: Tensor, cache) -> Tensor:
         """idx [rows, 1] -> logits [rows, V] (bf16); appends this step's K/V at cache.pos_t."""
         sp = self.spec
         rows, C, H, D = idx.shape[0], sp.C, sp.H, sp.D
         x = fused_ops.embedding_fwd(idx, sp.wte.weight, sp.wpe.weight, 0, pos_dev=cache.pos_t)  # fp32 [rows, C]
         x2 = torch.empty_like(x)  # the residual stream ping-pongs between x and x2 (no aliasing)
+        if self._fused_ok(rows):
+            return self._forward_fused(x, x2, rows, cache)
 
         def add_ln(delta, w, b, eps, dbias=None):
             nonlocal x, x2
@@ -190,6 +205,37 @@ class GPTDecodeProgram:
             delta, dbias = self._linear(h, blk.fc2, bias=False), fb
         wf, bf, ef = self.lnf
         return self._linear(add_ln(delta, wf, bf, ef, dbias), sp.head)
+
+    def _forward_fused(self, x: Tensor, x2: Tensor, rows: int, cache) -> Tensor:
+        """Per block: [add + LN1 + QKV GEMM + bias] → decode attention (K/V append fused) → proj
+        GEMM → [add + proj bias + LN2 + fc GEMM + bias + GELU] → fc2 GEMM: 5 kernels instead of 8."""
+        sp = self.spec
+        K = _ext.kernels()
+        C, H, D = sp.C, sp.H, sp.D
+        act = 2 if sp.gelu_approx == "tanh" else 1
+        delta = dbias = None
+        for l, blk in enumerate(sp.blocks):
+            w1, b1, e1, w2, b2, e2 = self.ln[l]
+            pb, fb = self.out_bias[l]
+            qkv = torch.empty(rows, 3 * C, dtype=torch.bfloat16, device=x.device)
+            if delta is None:
+                K.decode_ln_linear(x, None, None, None, w1, b1, e1, blk.qkv.weight, blk.qkv.bias, qkv, 0)
+            else:
+                K.decode_ln_linear(x, delta, dbias, x2, w1, b1, e1, blk.qkv.weight, blk.qkv.bias, qkv, 0)
+                x, x2 = x2, x
+            qkv = qkv.view(rows, 1, 3 * C)
+            q = qkv[:, :, :C].view(rows, 1, H, D)
+            k = qkv[:, :, C:2 * C].view(rows, 1, H, D)
+            v = qkv[:, :, 2 * C:].view(rows, 1, H, D)
+            o = cache._attend_graph(l, q, k, v)
+            d = self._linear(o.view(rows, C), blk.proj, bias=False)
+            h = torch.empty(rows, blk.fc.out_features, dtype=torch.bfloat16, device=x.device)
+            K.decode_ln_linear(x, d, pb, x2, w2, b2, e2, blk.fc.weight, blk.fc.bias, h, act)
+            x, x2 = x2, x
+            delta, dbias = self._linear(h, blk.fc2, bias=False), fb
+        wf, bf, ef = self.lnf
+        y, _, _ = norm_ops.add_ln_fwd(x, delta, x2, wf, bf, ef, delta_bias=dbias)
+        return self._linear(y, sp.head)
 
 
 def _packed_gate_up(mlp):

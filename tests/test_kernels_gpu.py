@@ -778,3 +778,29 @@ def test_wgrad_gemm_padded_rows(M, tile, variant):
     _ext.kernels().wgrad_gemm(dy, x, grad, tile, variant)
     assert (grad - ref).norm() / ref.norm() < 1e-4
     assert torch.equal(flat[M * N:], tail), "wrote past the gradient's M rows"
+
+
+@pytest.mark.parametrize("M,K,N", [(64, 768, 2304), (3, 128, 200), (17, 256, 1000), (33, 1024, 64)])
+@pytest.mark.parametrize("act", [0, 1, 2])
+@pytest.mark.parametrize("with_delta", [True, False])
+def test_decode_ln_linear(M, K, N, act, with_delta):
+    """Fused decode kernel: out = act(LN(resid + delta + dbias)·Wᵀ + b) vs fp32 torch (+ the
+    residual sum it writes)."""
+    torch.manual_seed(0)
+    rin = torch.randn(M, K, device=DEV)
+    delta = torch.randn(M, K, device=DEV).to(torch.bfloat16) if with_delta else None
+    dbias = torch.randn(K, device=DEV) if with_delta else None
+    rout = torch.empty(M, K, device=DEV) if with_delta else None
+    gamma, beta = torch.randn(K, device=DEV), torch.randn(K, device=DEV)
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, device=DEV).to(torch.bfloat16)
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    _ext.kernels().decode_ln_linear(rin, delta, dbias, rout, gamma, beta, 1e-5, w, b, out, act)
+    s = rin + (delta.float() + dbias) if with_delta else rin
+    y = F.layer_norm(s, (K,), gamma, beta, 1e-5).to(torch.bfloat16).float()
+    ref = y @ w.float().t() + b.float()
+    if act:
+        ref = F.gelu(ref.to(torch.bfloat16).float(), approximate="tanh" if act == 2 else "none")
+    _close(out, ref, 2e-2, 2e-2, "out")
+    if with_delta:
+        _close(rout, s, 1e-6, 1e-6, "resid_out")
