@@ -63,7 +63,7 @@ def main():
         k = kernels()
         dout = torch.randn_like(out)
         dq = torch.empty_like(qkv)
-        variants = [1, 2, 3] if (hasattr(k, "flash_bwd_variant") and D == 64) else [0]
+        variants = [2, 3, 4] if (hasattr(k, "flash_bwd_variant") and D == 64) else [0]
         for v in variants:
             if v:
                 prev = k.flash_bwd_variant(v)

@@ -74,7 +74,8 @@ void flash_attn_fwd(torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int
 int64_t flash_fwd_variant(int64_t v);
 int64_t flash_bwd_variant(int64_t v);
 void flash_attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, torch::Tensor dqkv,
-                    int64_t H, int64_t Hkv, int64_t D, double scale, double p_drop, int64_t seed);
+                    int64_t H, int64_t Hkv, int64_t D, double scale, double p_drop, int64_t seed,
+                    c10::optional<torch::Tensor> dbias);
 // flash_attn_gen.hip (head_dim 128 / 256)
 void flash_attn_gen_fwd(torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int64_t H, int64_t Hkv, int64_t D,
                         double scale, double p_drop, int64_t seed);
@@ -145,7 +146,10 @@ PYBIND11_MODULE(penroz_kernels, m) {
         "select the dK/dV kernel (1 register-staged, 2 LDS-DMA pipelined); returns the previous one");
   m.def("flash_fwd_variant", &flash_fwd_variant, pybind11::arg("variant") = 0,
         "select the forward kernel (1 single-stage, 2 tile-pipelined); returns the previous one");
-  m.def("flash_attn_bwd", &flash_attn_bwd);
+  m.def("flash_attn_bwd", &flash_attn_bwd, pybind11::arg("dout"), pybind11::arg("qkv"), pybind11::arg("out"),
+        pybind11::arg("lse"), pybind11::arg("dqkv"), pybind11::arg("H"), pybind11::arg("Hkv"), pybind11::arg("D"),
+        pybind11::arg("scale"), pybind11::arg("p_drop"), pybind11::arg("seed"), pybind11::arg("dbias") = pybind11::none(),
+        "causal flash-attention backward (head_dim 64) into dqkv; dbias += column sums of dqkv when given");
   m.def("flash_attn_gen_fwd", &flash_attn_gen_fwd, "causal flash attention forward, head_dim 128 / 256");
   m.def("flash_attn_gen_bwd", &flash_attn_gen_bwd, "causal flash attention backward, head_dim 128 / 256");
 }

@@ -36,6 +36,7 @@
 // the identical mask; the softmax normaliser uses the undropped probabilities (SDPA
 // semantics).
 #include "attn_common.h"
+#include "deferred.h"
 #include <type_traits>
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
@@ -463,187 +464,9 @@ __global__ void __launch_bounds__(256) fa_bwd_pre_kernel(const bf16* __restrict_
 }
 
 // ------------------------------------------------------------------------------------------
-// dK / dV: grid (ceil(T/128) key blocks, B*Hkv); wave w owns keys kb*128 + 32w + (lane&31).
-// Query slices of 64 rows (two 32-row halves per barrier) are staged through registers into
-// double-buffered LDS; P / dS are computed in place in the S / dP accumulators.
-template <bool DROPOUT>
-__global__ void __launch_bounds__(256, 2) fa_bwd_dkdv_kernel(const bf16* __restrict__ qkv,
-                                                             const bf16* __restrict__ dout,
-                                                             const float* __restrict__ lse,
-                                                             const float* __restrict__ delta, bf16* __restrict__ dqkv,
-                                                             int T, int H, int Hkv, float scale, float p_drop,
-                                                             uint64_t seed) {
-  constexpr int BK = 128, QS = 64;
-  __shared__ __attribute__((aligned(16))) char qt[2][QS * 128];
-  __shared__ __attribute__((aligned(16))) char dot[2][QS * 128];
-  __shared__ __attribute__((aligned(16))) float lse2s[2][QS];
-  __shared__ __attribute__((aligned(16))) float dels[2][QS];
-  int kb, bh;
-  xcd_head_block(kb, bh);
-  const int b = bh / Hkv, hk = bh % Hkv;
-  const int G = H / Hkv;
-  const int lane = threadIdx.x & 63, w = wave_id(), hh = lane >> 5;
-  const size_t RS = (size_t)(H + 2 * Hkv) * kD;
-  const size_t ORS = (size_t)H * kD;
-  const int kw0 = kb * BK + 32 * w;
-  const int key = kw0 + (lane & 31);
-  const float c = scale * kLog2e;
-  const float inv_keep = DROPOUT ? 1.f / (1.f - p_drop) : 1.f;
-
-  const bf16* kbase = qkv + (size_t)b * T * RS + (size_t)(H + hk) * kD;
-  const bf16* vbase = qkv + (size_t)b * T * RS + (size_t)(H + Hkv + hk) * kD;
-  uint4 kf[4], vf[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    kf[s] = key < T ? *reinterpret_cast<const uint4*>(kbase + (size_t)key * RS + 16 * s + 8 * hh) : zero4();
-    vf[s] = key < T ? *reinterpret_cast<const uint4*>(vbase + (size_t)key * RS + 16 * s + 8 * hh) : zero4();
-  }
-  f32x16 dk[2], dv[2];
-#pragma unroll
-  for (int dh = 0; dh < 2; ++dh)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) dk[dh][i] = dv[dh][i] = 0.f;
-
-  // staging: threads 0..127 -> Q slice, 128..255 -> dO slice; thread -> chunk t&7 of rows
-  // ((t>>3)&15) + 16i, i = 0..3 (coalesced, conflict-free ds_write_b128 groups)
-  const int st_tile = threadIdx.x >> 7, sr = (threadIdx.x >> 3) & 15, sc = threadIdx.x & 7;
-  const int s_first = (kb * BK) / QS;
-  const int nslices = (T + QS - 1) / QS;
-  const int per_head = nslices - s_first;
-  const int total = G * per_head;
-  uint4 st[4];
-  float st_scalar = 0.f;
-  auto gload = [&](int it) {
-    const int hq = hk * G + it / per_head;
-    const int qs0 = (s_first + it % per_head) * QS;
-    const bf16* src = st_tile == 0 ? qkv + (size_t)b * T * RS + (size_t)hq * kD
-                                   : dout + (size_t)b * T * ORS + (size_t)hq * kD;
-    const size_t rs = st_tile == 0 ? RS : ORS;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int q = qs0 + sr + 16 * i;
-      st[i] = q < T ? *reinterpret_cast<const uint4*>(src + (size_t)q * rs + 8 * sc) : zero4();
-    }
-    if (threadIdx.x < 2 * QS) {
-      const int qq = qs0 + (threadIdx.x & (QS - 1));
-      const size_t r = ((size_t)b * H + hq) * T + qq;
-      st_scalar = qq < T ? (threadIdx.x < QS ? lse[r] * kLog2e : delta[r]) : 0.f;
-    }
-  };
-  auto lstore = [&](int buf) {
-    char* dst = st_tile == 0 ? qt[buf] : dot[buf];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(dst + tile_off(sr + 16 * i, sc)) = st[i];
-    if (threadIdx.x < QS) lse2s[buf][threadIdx.x] = st_scalar;
-    else if (threadIdx.x < 2 * QS) dels[buf][threadIdx.x - QS] = st_scalar;
-  };
-
-  if (total > 0) {
-    gload(0);
-    lstore(0);
-  }
-  __syncthreads();
-  for (int it = 0; it < total; ++it) {
-    if (it + 1 < total) gload(it + 1);
-    const int buf = it & 1;
-    const int hq = hk * G + it / per_head;
-    const int qs0 = (s_first + it % per_head) * QS;
-    // both 32-row halves' S and dP chains are issued before the first half's VALU so the
-    // matrix cores run half 1 under half 0's P / dS math; dP starts from -δ (the row constant
-    // as the initial accumulator), so dS = P·dP' needs no subtraction
-    bool act[2];
-    f32x16 sp[2], dp[2];
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      const int qh0 = qs0 + 32 * half;
-      act[half] = qh0 + 31 >= kw0 && kw0 < T && qh0 < T;
-      if (act[half]) {
-        const char* Qt = qt[buf] + half * 32 * 128;
-        const char* Dt = dot[buf] + half * 32 * 128;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const float4_t dl = *reinterpret_cast<const float4_t*>(&dels[buf][32 * half + 8 * g + 4 * hh]);
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            sp[half][4 * g + k] = 0.f;
-            dp[half][4 * g + k] = DROPOUT ? 0.f : -dl[k];
-          }
-        }
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          sp[half] = mfma32(row_frag(Qt, 0, s, lane), kf[s], sp[half]);
-          dp[half] = mfma32(row_frag(Dt, 0, s, lane), vf[s], dp[half]);
-        }
-      }
-    }
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      const int qh0 = qs0 + 32 * half;  // first query row of this 32-row half
-      if (act[half]) {
-        const char* Qt = qt[buf] + half * 32 * 128;
-        const char* Dt = dot[buf] + half * 32 * 128;
-        const bool need_mask = (kw0 + 31 > qh0) || (qh0 + 32 > T) || (kw0 + 32 > T);
-        auto grads = [&](auto mask_tag) {  // P and dS in place; mask path only on diagonal tiles
-          constexpr bool MASK = decltype(mask_tag)::value;
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int r0 = 8 * g + 4 * hh;
-            const float4_t l2 = *reinterpret_cast<const float4_t*>(&lse2s[buf][32 * half + r0]);
-            float4_t dl = {0.f, 0.f, 0.f, 0.f};
-            if constexpr (DROPOUT) dl = *reinterpret_cast<const float4_t*>(&dels[buf][32 * half + r0]);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              const int i = 4 * g + k;
-              const int q = qh0 + r0 + k;
-              float p = fexp2(fmaf(sp[half][i], c, -l2[k]));
-              if constexpr (MASK) p = (key > q || q >= T || key >= T) ? 0.f : p;
-              if constexpr (DROPOUT) {
-                const bool keep = dropout_keep(seed, b, hq, H, T, q, key, p_drop);
-                sp[half][i] = keep ? p * inv_keep : 0.f;
-                dp[half][i] = p * ((keep ? dp[half][i] * inv_keep : 0.f) - dl[k]);
-              } else {
-                sp[half][i] = p;
-                dp[half][i] = p * dp[half][i];
-              }
-            }
-          }
-        };
-        if (need_mask)
-          grads(std::true_type{});
-        else
-          grads(std::false_type{});
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss) {
-          const uint4 pf = acc_frag(sp[half], ss), sf = acc_frag(dp[half], ss);
-#pragma unroll
-          for (int dh = 0; dh < 2; ++dh) {
-            dv[dh] = mfma32(tr_frag(Dt, 16 * ss, 32 * dh, lane), pf, dv[dh]);
-            dk[dh] = mfma32(tr_frag(Qt, 16 * ss, 32 * dh, lane), sf, dk[dh]);
-          }
-        }
-      }
-    }
-    if (it + 1 < total) lstore((it + 1) & 1);
-    __syncthreads();
-  }
-  if (key < T) {
-    bf16* dkrow = dqkv + ((size_t)b * T + key) * RS + (size_t)(H + hk) * kD;
-    bf16* dvrow = dqkv + ((size_t)b * T + key) * RS + (size_t)(H + Hkv + hk) * kD;
-#pragma unroll
-    for (int dh = 0; dh < 2; ++dh)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d = 32 * dh + 8 * g + 4 * hh;
-        store4(dkrow + d, dk[dh][4 * g] * scale, dk[dh][4 * g + 1] * scale, dk[dh][4 * g + 2] * scale,
-               dk[dh][4 * g + 3] * scale);
-        store4(dvrow + d, dv[dh][4 * g], dv[dh][4 * g + 1], dv[dh][4 * g + 2], dv[dh][4 * g + 3]);
-      }
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// dK / dV, LDS-DMA pipeline (default): same math and grid as fa_bwd_dkdv_kernel, but the Q / dO
-// slices and their LSE / δ rows arrive by LDS-DMA into a 3-stage ring, two slices ahead, so
+// dK / dV, variant 2 (also the dropout path): grid (ceil(T/128) key blocks, B*Hkv); wave w owns
+// keys kb*128 + 32w + (lane&31); P / dS are computed in place in the S / dP accumulators. The
+// Q / dO slices and their LSE / δ rows arrive by LDS-DMA into a 3-stage ring, two slices ahead, so
 // global latency hides behind two iterations of MFMA work instead of one; K / V fragments are
 // laundered so no compiler-tracked load is outstanding inside the loop. Per iteration: waves
 // 0-1 fetch the Q slice (4 pieces each), waves 2-3 the dO slice, waves 0 / 1 also the LSE / δ
@@ -653,7 +476,7 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv2_kernel(const bf16* __rest
                                                               const bf16* __restrict__ dout,
                                                               const float* __restrict__ lse,
                                                               const float* __restrict__ delta,
-                                                              bf16* __restrict__ dqkv, int T, int H, int Hkv,
+                                                              bf16* __restrict__ dqkv, float* __restrict__ cpart, int T, int H, int Hkv,
                                                               float scale, float p_drop, uint64_t seed) {
   constexpr int BK = 128, QS = 64, NST = 3;
   constexpr int TILE = QS * 128;              // one 64-row slice, 128-B rows
@@ -849,20 +672,40 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv2_kernel(const bf16* __rest
 // (4 row-read + 4 transposed-read offsets; the 32-row half, the 16-row sub-block and — the loop
 // unrolled by the 3 ring stages — the stage base all become immediates), removing the ~140
 // swizzle-address VALU instructions per iteration that the compiler otherwise rematerialises.
-// Derived from the variant-2 description below: same math and grid as fa_bwd_dkdv_kernel, but the Q / dO
-// slices and their LSE / δ rows arrive by LDS-DMA into a 3-stage ring, two slices ahead, so
-// global latency hides behind two iterations of MFMA work instead of one; K / V fragments are
-// laundered so no compiler-tracked load is outstanding inside the loop. Per iteration: waves
-// 0-1 fetch the Q slice (4 pieces each), waves 2-3 the dO slice, waves 0 / 1 also the LSE / δ
-// rows (one 4-byte DMA each).
-template <bool DROPOUT>
+// NST = ring depth, NST - 1 slices in flight (3: variant 3, 4: variant 4).
+template <int NST>
+struct RingWait {  // s_waitcnt that leaves the newest NST - 2 stages' DMAs in flight
+  template <int PER>  // DMA instructions per stage and wave (4 pieces, +1 LSE / δ row)
+  static __device__ __forceinline__ void wait() {
+    static_assert(NST >= 3 && NST <= 4 && (PER == 4 || PER == 5), "ring depth / pieces");
+    if constexpr (NST == 3) {
+      if constexpr (PER == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    } else {
+      if constexpr (PER == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    }
+  }
+};
+
+// f(base + S, integral_constant<S>) for every S of the sequence (the ring stage is compile-time)
+template <typename F, int... S>
+__device__ __forceinline__ void ring_unroll(F&& f, int base, std::integer_sequence<int, S...>) {
+  (f(base + S, std::integral_constant<int, S>{}), ...);
+}
+template <typename F, int... S>
+__device__ __forceinline__ void ring_tail(F&& f, int base, int total, std::integer_sequence<int, S...>) {
+  ((base + S < total ? f(base + S, std::integral_constant<int, S>{}) : void()), ...);
+}
+
+template <bool DROPOUT, int NST>
 __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv3_kernel(const bf16* __restrict__ qkv,
                                                               const bf16* __restrict__ dout,
                                                               const float* __restrict__ lse,
                                                               const float* __restrict__ delta,
-                                                              bf16* __restrict__ dqkv, int T, int H, int Hkv,
+                                                              bf16* __restrict__ dqkv, float* __restrict__ cpart, int T, int H, int Hkv,
                                                               float scale, float p_drop, uint64_t seed) {
-  constexpr int BK = 128, QS = 64, NST = 3;
+  constexpr int BK = 128, QS = 64;
   constexpr int TILE = QS * 128;              // one 64-row slice, 128-B rows
   constexpr int STAGE = 2 * TILE + 512;       // Q | dO | LSE[64] | δ[64]
   __shared__ __attribute__((aligned(16))) char smem[NST * STAGE];
@@ -961,22 +804,22 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv3_kernel(const bf16* __rest
       glds4(sp, st + 2 * TILE + 256 * w);
     }
   };
-  auto wait_next = [&]() {  // this wave's DMAs for the next stage done; the one after in flight
+  auto wait_next = [&]() {  // this wave's DMAs for the next stage done; the later ones in flight
     if (w < 2)
-      asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      RingWait<NST>::template wait<5>();
     else
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      RingWait<NST>::template wait<4>();
   };
 
   if (total > 0) {
-    dma(0);
-    dma(1);
+#pragma unroll
+    for (int i = 0; i < NST - 1; ++i) dma(i);
     wait_next();
   }
   __syncthreads();
   auto iter = [&](int it, auto stage_tag) {
     constexpr int ST = decltype(stage_tag)::value;
-    dma(it + 2);  // into the stage consumed at it-1 (freed by its barrier)
+    dma(it + NST - 1);  // into the stage consumed at it-1 (freed by its barrier)
     const char* stg = smem + ST * STAGE;
     const float* lse_s = reinterpret_cast<const float*>(stg + 2 * TILE);
     const float* del_s = lse_s + QS;
@@ -1058,14 +901,15 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv3_kernel(const bf16* __rest
     __syncthreads();
   };
   int it = 0;
-  for (; it + 3 <= total; it += 3) {
-    iter(it, std::integral_constant<int, 0>{});
-    iter(it + 1, std::integral_constant<int, 1>{});
-    iter(it + 2, std::integral_constant<int, 2>{});
-  }
-  if (it < total) iter(it, std::integral_constant<int, 0>{});
-  if (it + 1 < total) iter(it + 1, std::integral_constant<int, 1>{});
+  for (; it + NST <= total; it += NST) ring_unroll(iter, it, std::make_integer_sequence<int, NST>{});
+  ring_tail(iter, it, total, std::make_integer_sequence<int, NST - 1>{});
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (cpart != nullptr) {  // qkv-bias gradient: this block's dK / dV column sums
+    float* red = reinterpret_cast<float*>(smem);
+    float* prow = cpart + ((size_t)b * gridDim.x + kb) * RS;
+    colsum128_part(dk, scale, key < T, red, prow + (size_t)(H + hk) * kD);
+    colsum128_part(dv, 1.f, key < T, red, prow + (size_t)(H + Hkv + hk) * kD);
+  }
   if (key < T) {
     bf16* dkrow = dqkv + ((size_t)b * T + key) * RS + (size_t)(H + hk) * kD;
     bf16* dvrow = dqkv + ((size_t)b * T + key) * RS + (size_t)(H + Hkv + hk) * kD;
@@ -1082,145 +926,13 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv3_kernel(const bf16* __rest
 }
 
 // ------------------------------------------------------------------------------------------
-// dQ: grid (ceil(T/128) query blocks, heaviest first, B*H); forward-shaped
-template <bool DROPOUT>
-__global__ void __launch_bounds__(256, 2) fa_bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
-                                                        const float* __restrict__ lse,
-                                                        const float* __restrict__ delta, bf16* __restrict__ dqkv,
-                                                        int T, int H, int Hkv, float scale, float p_drop,
-                                                        uint64_t seed) {
-  constexpr int BM = 128, BN = 64;
-  __shared__ __attribute__((aligned(16))) char smem[2][2][BN * 128];
-  const int nqb = (T + BM - 1) / BM;
-  int qi, bh;
-  xcd_head_block(qi, bh);
-  const int qb = nqb - 1 - qi;
-  const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
-  const int lane = threadIdx.x & 63, w = wave_id(), hh = lane >> 5;
-  const size_t RS = (size_t)(H + 2 * Hkv) * kD;
-  const size_t ORS = (size_t)H * kD;
-  const bf16* kbase = qkv + (size_t)b * T * RS + (size_t)(H + hk) * kD;
-  const bf16* vbase = qkv + (size_t)b * T * RS + (size_t)(H + Hkv + hk) * kD;
-  const int q0 = qb * BM + 32 * w;
-  const int qrow = q0 + (lane & 31);
-  const float c = scale * kLog2e;
-  const float inv_keep = DROPOUT ? 1.f / (1.f - p_drop) : 1.f;
-
-  uint4 qf[4], dof[4];
-  const bool qok = qrow < T;
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    qf[s] = qok ? *reinterpret_cast<const uint4*>(qkv + (size_t)b * T * RS + (size_t)h * kD + (size_t)qrow * RS + 16 * s +
-                                                  8 * hh)
-                : zero4();
-    dof[s] = qok ? *reinterpret_cast<const uint4*>(dout + (size_t)b * T * ORS + (size_t)h * kD + (size_t)qrow * ORS +
-                                                   16 * s + 8 * hh)
-                 : zero4();
-  }
-  const size_t rr = ((size_t)b * H + h) * T + qrow;
-  const float l2 = qok ? lse[rr] * kLog2e : 0.f;
-  const float dl = qok ? delta[rr] : 0.f;
-
-  // staging: thread t -> chunk t&7 of rows (t>>3) + 32i (8 lanes cover one 128-B row:
-  // coalesced, conflict-free ds_write_b128 groups)
-  const int sr = threadIdx.x >> 3, sc = threadIdx.x & 7;
-  uint4 kst[2], vst[2];
-  auto gload = [&](int kt0) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int key = kt0 + sr + 32 * i;
-      kst[i] = key < T ? *reinterpret_cast<const uint4*>(kbase + (size_t)key * RS + 8 * sc) : zero4();
-      vst[i] = key < T ? *reinterpret_cast<const uint4*>(vbase + (size_t)key * RS + 8 * sc) : zero4();
-    }
-  };
-  auto lstore = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      *reinterpret_cast<uint4*>(smem[buf][0] + tile_off(sr + 32 * i, sc)) = kst[i];
-      *reinterpret_cast<uint4*>(smem[buf][1] + tile_off(sr + 32 * i, sc)) = vst[i];
-    }
-  };
-  const int kend = min(T, qb * BM + BM);
-  const int ntiles = (kend + BN - 1) / BN;
-  f32x16 dq[2];
-#pragma unroll
-  for (int dh = 0; dh < 2; ++dh)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) dq[dh][i] = 0.f;
-
-  gload(0);
-  lstore(0);
-  __syncthreads();
-  for (int j = 0; j < ntiles; ++j) {
-    const int kt0 = j * BN;
-    if (j + 1 < ntiles) gload(kt0 + BN);
-    const char* Kt = smem[j & 1][0];
-    const char* Vt = smem[j & 1][1];
-    if (kt0 <= q0 + 31) {
-      // dP starts from -δ (row constant = this lane's query row); per 32-key half the dS math
-      // is followed by its dQ MFMAs so the second half's VALU overlaps the first half's MFMAs
-      f32x16 s[2], dp[2];
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          s[kh][i] = 0.f;
-          dp[kh][i] = DROPOUT ? 0.f : -dl;
-        }
-#pragma unroll
-        for (int st = 0; st < 4; ++st) {
-          s[kh] = mfma32(row_frag(Kt, 32 * kh, st, lane), qf[st], s[kh]);
-          dp[kh] = mfma32(row_frag(Vt, 32 * kh, st, lane), dof[st], dp[kh]);
-        }
-      }
-      const bool need_mask = (kt0 + BN - 1 > q0) || (kt0 + BN > T) || (q0 + 32 > T);
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh) {
-        auto grads = [&](auto mask_tag) {
-          constexpr bool MASK = decltype(mask_tag)::value;
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int k = kt0 + 32 * kh + acc_row(i, lane);
-            float p = fexp2(fmaf(s[kh][i], c, -l2));
-            if constexpr (MASK) p = (k > qrow || k >= T || !qok) ? 0.f : p;
-            if constexpr (DROPOUT) {
-              const bool keep = dropout_keep(seed, b, h, H, T, qrow, k, p_drop);
-              s[kh][i] = p * ((keep ? dp[kh][i] * inv_keep : 0.f) - dl);
-            } else {
-              s[kh][i] = p * dp[kh][i];
-            }
-          }
-        };
-        if (need_mask)
-          grads(std::true_type{});
-        else
-          grads(std::false_type{});
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss) {
-          const uint4 sf = acc_frag(s[kh], ss);
-#pragma unroll
-          for (int dh = 0; dh < 2; ++dh) dq[dh] = mfma32(tr_frag(Kt, 32 * kh + 16 * ss, 32 * dh, lane), sf, dq[dh]);
-        }
-      }
-    }
-    if (j + 1 < ntiles) lstore((j + 1) & 1);
-    __syncthreads();
-  }
-  if (qok) {
-    bf16* dqrow = dqkv + ((size_t)b * T + qrow) * RS + (size_t)h * kD;
-#pragma unroll
-    for (int dh = 0; dh < 2; ++dh)
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        store4(dqrow + 32 * dh + 8 * g + 4 * hh, dq[dh][4 * g] * scale, dq[dh][4 * g + 1] * scale,
-               dq[dh][4 * g + 2] * scale, dq[dh][4 * g + 3] * scale);
-  }
-}
-
+// dQ, variant 2 (also the dropout path of variant 2): grid (ceil(T/128) query blocks, heaviest
+// first, B*H); forward-shaped — a wave keeps 32 query rows' Q, dO, LSE, δ and dQᵀ in registers
+// while K / V tiles of 64 keys arrive by LDS-DMA into a 3-stage ring, two tiles ahead.
 template <bool DROPOUT>
 __global__ void __launch_bounds__(256, 2) fa_bwd_dq3_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                                         const float* __restrict__ lse,
-                                                        const float* __restrict__ delta, bf16* __restrict__ dqkv,
+                                                        const float* __restrict__ delta, bf16* __restrict__ dqkv, float* __restrict__ cpart,
                                                         int T, int H, int Hkv, float scale, float p_drop,
                                                         uint64_t seed) {
   constexpr int BM = 128, BN = 64;
@@ -1374,14 +1086,13 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dq3_kernel(const bf16* __restri
 
 // dQ, variant 3: fa_bwd_dq3_kernel with precomputed per-lane LDS fragment offsets and the ring
 // loop unrolled by its 3 stages (stage bases and row bases become immediates), as dK/dV variant 3.
-template <bool DROPOUT>
+template <bool DROPOUT, int NST>
 __global__ void __launch_bounds__(256, 2) fa_bwd_dq4_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                                         const float* __restrict__ lse,
-                                                        const float* __restrict__ delta, bf16* __restrict__ dqkv,
+                                                        const float* __restrict__ delta, bf16* __restrict__ dqkv, float* __restrict__ cpart,
                                                         int T, int H, int Hkv, float scale, float p_drop,
                                                         uint64_t seed) {
   constexpr int BM = 128, BN = 64;
-  constexpr int NST = 3;
   __shared__ __attribute__((aligned(16))) char smem[NST][2][BN * 128];
   const int nqb = (T + BM - 1) / BM;
   int qi, bh;
@@ -1475,14 +1186,14 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dq4_kernel(const bf16* __restri
       }
     }
   };
-  dma(0);
-  dma(1);
-  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < NST - 1; ++i) dma(i);
+  RingWait<NST>::template wait<4>();
   __syncthreads();
   auto iter = [&](int j, auto stage_tag) {
     constexpr int ST = decltype(stage_tag)::value;
     const int kt0 = j * BN;
-    dma(j + 2);  // into the stage consumed at j-1 (freed by its barrier)
+    dma(j + NST - 1);  // into the stage consumed at j-1 (freed by its barrier)
     const char* Kt = smem[ST][0];
     const char* Vt = smem[ST][1];
     if (kt0 <= q0 + 31) {
@@ -1532,18 +1243,16 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dq4_kernel(const bf16* __restri
         }
       }
     }
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // tile j+1 landed, j+2 in flight
+    RingWait<NST>::template wait<4>();  // tile j+1 landed, the later ones in flight
     __syncthreads();
   };
   int j = 0;
-  for (; j + 3 <= ntiles; j += 3) {
-    iter(j, std::integral_constant<int, 0>{});
-    iter(j + 1, std::integral_constant<int, 1>{});
-    iter(j + 2, std::integral_constant<int, 2>{});
-  }
-  if (j < ntiles) iter(j, std::integral_constant<int, 0>{});
-  if (j + 1 < ntiles) iter(j + 1, std::integral_constant<int, 1>{});
+  for (; j + NST <= ntiles; j += NST) ring_unroll(iter, j, std::make_integer_sequence<int, NST>{});
+  ring_tail(iter, j, ntiles, std::make_integer_sequence<int, NST - 1>{});
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (cpart != nullptr)  // qkv-bias gradient: this block's dQ column sums
+    colsum128_part(dq, scale, qok, reinterpret_cast<float*>(&smem[0][0][0]),
+                   cpart + ((size_t)b * nqb + qb) * RS + (size_t)h * kD);
   if (qok) {
     bf16* dqrow = dqkv + ((size_t)b * T + qrow) * RS + (size_t)h * kD;
 #pragma unroll
@@ -1596,10 +1305,11 @@ void flash_attn_fwd(torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int
 
 // forward: 1 = single-stage (fa_fwd_kernel; also the dropout path), 3 = two query blocks per
 // wave (fa_fwd3_kernel, default). backward:
-// 1 = register-staged dK/dV and dQ kernels, 2 = LDS-DMA pipelined dK/dV and dQ kernels,
-// 3 = variant 2 with precomputed per-lane LDS offsets and stage-unrolled rings (default)
+// 2 = LDS-DMA pipelined dK/dV and dQ kernels, 3 = variant 2 with precomputed per-lane LDS offsets
+// and stage-unrolled 3-stage rings (default), 4 = variant 3 with 4-stage rings
 int64_t flash_bwd_variant(int64_t v) {
   const int64_t prev = g_fa_bwd_variant;
+  TORCH_CHECK(v <= 0 || (v >= 2 && v <= 4), "flash backward variant must be 2, 3 or 4");
   if (v > 0) g_fa_bwd_variant = (int)v;
   return prev;
 }
@@ -1610,8 +1320,15 @@ int64_t flash_fwd_variant(int64_t v) {
   return prev;
 }
 
+void colsum(torch::Tensor x, torch::Tensor out);  // elementwise.hip
+
+// dbias (optional, fp32 [(H + 2·Hkv)·D]): += the column sums of dqkv over all B·T rows (the fused
+// QKV projection's bias gradient). Variants 3 / 4 without dropout produce them in the kernels'
+// epilogues (one fp32 partial row per 128-row block, finished by the deferred reduction); the
+// other paths run the column-sum kernel over dqkv.
 void flash_attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, torch::Tensor dqkv,
-                    int64_t H, int64_t Hkv, int64_t D, double scale, double p_drop, int64_t seed) {
+                    int64_t H, int64_t Hkv, int64_t D, double scale, double p_drop, int64_t seed,
+                    c10::optional<torch::Tensor> dbias) {
   check_qkv(qkv, H, Hkv, D);
   const int B = qkv.size(0), T = qkv.size(1);
   TORCH_CHECK(dout.is_contiguous() && dout.scalar_type() == torch::kBFloat16 && dout.numel() == (int64_t)B * T * H * D);
@@ -1628,23 +1345,38 @@ void flash_attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, to
   const bf16* d = reinterpret_cast<const bf16*>(dout.data_ptr());
   bf16* g = reinterpret_cast<bf16*>(dqkv.data_ptr());
   dim3 gkv((T + 127) / 128, B * Hkv), gq((T + 127) / 128, B * H);
-  using BwdKernel = void (*)(const bf16*, const bf16*, const float*, const float*, bf16*, int, int, int, float, float,
+  using BwdKernel = void (*)(const bf16*, const bf16*, const float*, const float*, bf16*, float*, int, int, int, float, float,
                             uint64_t);
   const bool drop = p_drop > 0.0;
   BwdKernel kv, dq;
-  if (g_fa_bwd_variant == 1) {
-    kv = drop ? fa_bwd_dkdv_kernel<true> : fa_bwd_dkdv_kernel<false>;
-    dq = drop ? fa_bwd_dq_kernel<true> : fa_bwd_dq_kernel<false>;
-  } else if (g_fa_bwd_variant == 2) {
+  if (g_fa_bwd_variant == 2) {
     kv = drop ? fa_bwd_dkdv2_kernel<true> : fa_bwd_dkdv2_kernel<false>;
     dq = drop ? fa_bwd_dq3_kernel<true> : fa_bwd_dq3_kernel<false>;
+  } else if (g_fa_bwd_variant == 4) {  // 4-stage rings: three slices / tiles in flight
+    kv = drop ? fa_bwd_dkdv2_kernel<true> : fa_bwd_dkdv3_kernel<false, 4>;
+    dq = drop ? fa_bwd_dq4_kernel<true, 4> : fa_bwd_dq4_kernel<false, 4>;
   } else {  // (dK/dV with dropout stays on variant 2: the unrolled ring spills with the mask hashing live)
-    kv = drop ? fa_bwd_dkdv2_kernel<true> : fa_bwd_dkdv3_kernel<false>;
-    dq = drop ? fa_bwd_dq4_kernel<true> : fa_bwd_dq4_kernel<false>;
+    kv = drop ? fa_bwd_dkdv2_kernel<true> : fa_bwd_dkdv3_kernel<false, 3>;
+    dq = drop ? fa_bwd_dq4_kernel<true, 3> : fa_bwd_dq4_kernel<false, 3>;
   }
   const float pd = drop ? (float)p_drop : 0.f;
-  hipLaunchKernelGGL(kv, gkv, dim3(256), 0, stream, q, d, lse.data_ptr<float>(), delta.data_ptr<float>(), g, T,
+  const bool want_bias = dbias.has_value() && dbias->defined();
+  const int W = (int)((H + 2 * Hkv) * D), nblk = (T + 127) / 128;
+  if (want_bias)
+    TORCH_CHECK(dbias->is_cuda() && dbias->scalar_type() == torch::kFloat32 && dbias->is_contiguous() &&
+                    dbias->numel() == W, "dbias must be a contiguous fp32 [(H + 2*Hkv)*D] GPU tensor");
+  const bool fused_bias = want_bias && !drop && g_fa_bwd_variant != 2;
+  torch::Tensor part;
+  if (fused_bias) part = torch::empty({(int64_t)B * nblk, W}, qkv.options().dtype(torch::kFloat32));
+  float* pp = fused_bias ? part.data_ptr<float>() : nullptr;
+  hipLaunchKernelGGL(kv, gkv, dim3(256), 0, stream, q, d, lse.data_ptr<float>(), delta.data_ptr<float>(), g, pp, T,
                      (int)H, (int)Hkv, (float)scale, pd, (uint64_t)seed);
-  hipLaunchKernelGGL(dq, gq, dim3(256), 0, stream, q, d, lse.data_ptr<float>(), delta.data_ptr<float>(), g, T,
+  hipLaunchKernelGGL(dq, gq, dim3(256), 0, stream, q, d, lse.data_ptr<float>(), delta.data_ptr<float>(), g, pp, T,
                      (int)H, (int)Hkv, (float)scale, pd, (uint64_t)seed);
+  if (fused_bias) {
+    float* outs[1] = {dbias->data_ptr<float>()};
+    reduce_partials_auto(part, 1, B * nblk, W, outs, stream);
+  } else if (want_bias) {
+    colsum(dqkv.view({(int64_t)B * T, W}), *dbias);
+  }
 }

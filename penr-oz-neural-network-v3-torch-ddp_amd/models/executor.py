@@ -637,9 +637,11 @@ class GPTExecutor:
             # ---- attention branch
             torch.mm(dres_bf, self._dgrad_w(b.proj.weight), out=self.d_c)
             self._wgrad(dres_bf, self.att[l], b.proj.weight)
+            # the qkv bias gradient comes out of the attention-backward epilogues (partials finished
+            # on the side stream by the deferred reduction)
             attn_ops.flash_bwd(self.d_c.view(B, T, C), self.qkv[l].view(B, T, 3 * C), self.att[l].view(B, T, C),
-                               self.lse[l], s.H, s.H, s.D, b.attn.dropout, seed + l, dqkv=dqkv.view(B, T, 3 * C))
-            self._side_call(dqkv, lambda: fused_ops.colsum(dqkv, self.grad(b.qkv.bias)))
+                               self.lse[l], s.H, s.H, s.D, b.attn.dropout, seed + l, dqkv=dqkv.view(B, T, 3 * C),
+                               dbias=self.grad(b.qkv.bias))
             torch.mm(dqkv, self._dgrad_w(b.qkv.weight), out=self.d_c)
             self._wgrad(dqkv, self.ln1[l], b.qkv.weight)
             mean, rstd, _, _ = self.stats[l]

@@ -21,6 +21,7 @@ Replaces the reference's SDPA call (``neural_net_layers.py:59-95``).
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 from torch import Tensor
@@ -76,12 +77,36 @@ def flash_fwd(qkv: Tensor, H: int, Hkv: int, D: int, dropout_p: float = 0.0, see
     return out, lse
 
 
+_BWD_VARIANT_ENV = "PENROZ_FLASH_BWD_VARIANT"  # 2 / 3 / 4 (A/B knob; unset = the kernel default)
+_bwd_variant_applied = False
+
+
+def _apply_bwd_variant():
+    global _bwd_variant_applied
+    if not _bwd_variant_applied:
+        _bwd_variant_applied = True
+        v = int(os.environ.get(_BWD_VARIANT_ENV, "0"))
+        if v:
+            kernels().flash_bwd_variant(v)
+
+
 def flash_bwd(dout: Tensor, qkv: Tensor, out: Tensor, lse: Tensor, H: int, Hkv: int, D: int,
-              dropout_p: float = 0.0, seed: int = 0, dqkv: Tensor | None = None) -> Tensor:
-    """-> dqkv bf16 [B,T,(H+2Hkv)D] (written into ``dqkv`` when given)."""
+              dropout_p: float = 0.0, seed: int = 0, dqkv: Tensor | None = None,
+              dbias: Tensor | None = None) -> Tensor:
+    """-> dqkv bf16 [B,T,(H+2Hkv)D] (written into ``dqkv`` when given).
+
+    ``dbias`` (fp32 [(H+2Hkv)D]): += the column sums of dqkv, i.e. the fused QKV projection's bias
+    gradient. At head_dim 64 the dK/dV and dQ kernels produce them in their epilogues (no second
+    pass over the 2304-wide gradient); other head dims run the column-sum kernel afterwards."""
     dqkv = torch.empty_like(qkv) if dqkv is None else dqkv
-    fn = kernels().flash_attn_bwd if D == 64 else kernels().flash_attn_gen_bwd
-    fn(dout, qkv, out, lse, dqkv, H, Hkv, D, 1.0 / math.sqrt(D), float(dropout_p), int(seed))
+    scale = 1.0 / math.sqrt(D)
+    _apply_bwd_variant()
+    if D == 64:
+        kernels().flash_attn_bwd(dout, qkv, out, lse, dqkv, H, Hkv, D, scale, float(dropout_p), int(seed), dbias)
+    else:
+        kernels().flash_attn_gen_bwd(dout, qkv, out, lse, dqkv, H, Hkv, D, scale, float(dropout_p), int(seed))
+        if dbias is not None:
+            kernels().colsum(dqkv.view(-1, dqkv.shape[-1]), dbias)
     return dqkv
 
 

@@ -229,7 +229,7 @@ def test_flash_fwd(B, T, H, Hkv, variant):
     _close(lse, rl, 2e-3, 1e-4, "lse")
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3])
+@pytest.mark.parametrize("variant", [2, 3, 4])
 @pytest.mark.parametrize("B,T,H,Hkv", [(2, 512, 4, 4), (1, 200, 3, 3), (2, 130, 4, 2), (1, 7, 2, 1), (1, 1024, 2, 2),
                                        (1, 320, 4, 1)])
 def test_flash_bwd(B, T, H, Hkv, variant):
@@ -251,6 +251,30 @@ def test_flash_bwd(B, T, H, Hkv, variant):
         a, r = dq[..., sl].float(), ref[..., sl]
         rel = (a - r).norm() / r.norm()
         assert rel < 0.02, f"{name} relative error {rel}"
+
+
+@pytest.mark.parametrize("variant", [2, 3, 4])
+@pytest.mark.parametrize("B,T,H,Hkv,p", [(2, 512, 4, 4, 0.0), (1, 200, 3, 3, 0.0), (2, 130, 4, 2, 0.0),
+                                         (1, 7, 2, 1, 0.0), (1, 300, 2, 2, 0.1)])
+def test_flash_bwd_fused_bias_grad(B, T, H, Hkv, p, variant):
+    """dbias (the qkv bias gradient) from the attention-backward epilogues == the column sums of the
+    dqkv the same call stored, accumulated onto the existing value (fp32 torch reference)."""
+    torch.manual_seed(0)
+    qkv = _qkv(B, T, H, Hkv)
+    out, lse = A.flash_fwd(qkv, H, Hkv, 64, p, 7)
+    dout = torch.randn(B, T, H * 64, device=DEV).to(torch.bfloat16)
+    k = _ext.kernels()
+    prev = k.flash_bwd_variant(variant)
+    try:
+        base = torch.randn((H + 2 * Hkv) * 64, device=DEV)
+        dbias = base.clone()
+        dq = A.flash_bwd(dout, qkv, out, lse, H, Hkv, 64, p, 7, dbias=dbias)
+        dq_plain = A.flash_bwd(dout, qkv, out, lse, H, Hkv, 64, p, 7)
+    finally:
+        k.flash_bwd_variant(prev)
+    torch.testing.assert_close(dq, dq_plain, rtol=0, atol=0)  # the epilogue does not change dqkv
+    ref = base + dq.float().reshape(-1, dq.shape[-1]).sum(0)
+    torch.testing.assert_close(dbias, ref, rtol=1e-4, atol=1e-3)
 
 
 def test_flash_dropout_matches_masked_reference():
