@@ -62,3 +62,21 @@ if "adam" in which:
     sh = torch.empty(n, device="cuda", dtype=torch.bfloat16)
     t = timeit(lambda: k.adamw_step(p, g, m, v, sh, 6e-4, 0.9, 0.95, 1e-8, 0.01, 10, 1.0, False))
     emit(kernel="adamw_flat", n=n, us=round(t * 1e6, 1), TBps=round(30 * n / t / 1e12, 2))
+if "stream" in which:
+    # memory-bound streams at the fc activation shape [65536, 3072] bf16: GELU forward (read +
+    # write), GELU backward fused with the fc bias-gradient column sum (2 reads + 1 write), the
+    # plain column sum (1 read) — effective TB/s against a torch copy of the same bytes
+    F_ = 3072
+    x = torch.randn(N, F_, device="cuda", dtype=torch.bfloat16)
+    dy = torch.randn(N, F_, device="cuda", dtype=torch.bfloat16)
+    y = torch.empty_like(x)
+    db = torch.zeros(F_, device="cuda")
+    nb = x.numel() * 2
+    t = timeit(lambda: k.gelu_fwd(x, 0, y), 20)
+    emit(kernel="gelu_fwd", us=round(t * 1e6, 1), TBps=round(2 * nb / t / 1e12, 2))
+    t = timeit(lambda: k.gelu_bwd(dy, x, 0, db, y), 20)
+    emit(kernel="gelu_bwd_colsum", us=round(t * 1e6, 1), TBps=round(3 * nb / t / 1e12, 2))
+    t = timeit(lambda: k.colsum(dy, db), 20)
+    emit(kernel="colsum", us=round(t * 1e6, 1), TBps=round(nb / t / 1e12, 2))
+    t = timeit(lambda: y.copy_(x), 20)
+    emit(kernel="torch_copy", us=round(t * 1e6, 1), TBps=round(2 * nb / t / 1e12, 2))

@@ -125,33 +125,36 @@ __device__ __forceinline__ void xcd_head_block(int& blk, int& head) {
 }
 
 
-// Bias-gradient partial of one 128-row block (4 waves × 32 rows on the lanes) of a 64-column
-// head slice held in MFMA accumulators: acc[dh][4g + k] is column 32·dh + 8·g + 4·(lane>>5) + k of
-// row 32·wave + (lane&31). Each value is scaled by `mul` and rounded to bf16 exactly as the
-// kernel stores it (so the sum equals the column sum of the stored gradient), invalid rows count
-// 0, and part[0..63] receives the 64 column sums. `red`: ≥ 128·65 floats of LDS no longer in use
-// (the ring), every thread of the 256-thread workgroup must call (barriers inside).
-__device__ __forceinline__ void colsum128_part(const f32x16 (&acc)[2], float mul, bool valid, float* red,
-                                               float* __restrict__ part) {
-  const int lane = threadIdx.x & 63, hh = lane >> 5;
-  const int r = 32 * (threadIdx.x >> 6) + (lane & 31);
-  __syncthreads();  // the LDS is free (ring drained, previous call's reads done)
+// Bias-gradient partial of one wave's 32 rows (on lanes lane&31) of a 64-column head slice held in
+// MFMA accumulators: acc[dh][i] is column 32·dh + 8·(i>>2) + 4·(lane>>5) + (i&3). Each value is
+// scaled by `mul` and rounded to bf16 exactly as the kernel stores it (so the sums equal the
+// column sums of the stored gradient); invalid rows count 0. A transpose-reduce over the five
+// lane bits (xor 16 … 1, each step halving the registers in play: 31 shuffles, no LDS, no
+// barrier) leaves lane L holding the sum of register 16·dh + i = L&31, stored to part[column].
+// one transpose-reduce step over lane bit N (registers v[0 .. 2N) in play -> v[0 .. N)); the
+// register count is a template constant so every index stays static (no dynamic register indexing)
+template <int N>
+__device__ __forceinline__ void transpose_reduce_step(float (&v)[32], int lane) {
+  const bool up = (lane & N) != 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const float send = up ? v[i] : v[i + N];
+    const float keep = up ? v[i + N] : v[i];
+    v[i] = keep + __shfl_xor(send, N, 64);
+  }
+  if constexpr (N > 1) transpose_reduce_step<N / 2>(v, lane);
+}
+
+__device__ __forceinline__ void colsum32_wave(const f32x16 (&acc)[2], float mul, bool valid, float* __restrict__ part) {
+  const int lane = threadIdx.x & 63;
+  float v[32];
 #pragma unroll
   for (int dh = 0; dh < 2; ++dh)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int col = 32 * dh + 8 * (i >> 2) + 4 * hh + (i & 3);
-      red[r * 65 + col] = valid ? __bfloat162float(__float2bfloat16(acc[dh][i] * mul)) : 0.f;
-    }
-  __syncthreads();
-  const int c = threadIdx.x & 63, qq = threadIdx.x >> 6;
-  float s = 0.f;
-#pragma unroll 8
-  for (int i = 0; i < 32; ++i) s += red[(32 * qq + i) * 65 + c];
-  __syncthreads();
-  red[qq * 64 + c] = s;
-  __syncthreads();
-  if (threadIdx.x < 64) part[c] = red[c] + red[64 + c] + red[128 + c] + red[192 + c];
+    for (int i = 0; i < 16; ++i) v[16 * dh + i] = valid ? __bfloat162float(__float2bfloat16(acc[dh][i] * mul)) : 0.f;
+  transpose_reduce_step<16>(v, lane);
+  const int r = lane & 31, dh = r >> 4, i = r & 15;
+  part[32 * dh + 8 * (i >> 2) + 4 * (lane >> 5) + (i & 3)] = v[0];
 }
 
 

@@ -904,11 +904,10 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv3_kernel(const bf16* __rest
   for (; it + NST <= total; it += NST) ring_unroll(iter, it, std::make_integer_sequence<int, NST>{});
   ring_tail(iter, it, total, std::make_integer_sequence<int, NST - 1>{});
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (cpart != nullptr) {  // qkv-bias gradient: this block's dK / dV column sums
-    float* red = reinterpret_cast<float*>(smem);
-    float* prow = cpart + ((size_t)b * gridDim.x + kb) * RS;
-    colsum128_part(dk, scale, key < T, red, prow + (size_t)(H + hk) * kD);
-    colsum128_part(dv, 1.f, key < T, red, prow + (size_t)(H + Hkv + hk) * kD);
+  if (cpart != nullptr) {  // qkv-bias gradient: this wave's dK / dV column sums (one partial row)
+    float* prow = cpart + (((size_t)b * gridDim.x + kb) * 4 + w) * RS;
+    colsum32_wave(dk, scale, key < T, prow + (size_t)(H + hk) * kD);
+    colsum32_wave(dv, 1.f, key < T, prow + (size_t)(H + Hkv + hk) * kD);
   }
   if (key < T) {
     bf16* dkrow = dqkv + ((size_t)b * T + key) * RS + (size_t)(H + hk) * kD;
@@ -1250,9 +1249,8 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dq4_kernel(const bf16* __restri
   for (; j + NST <= ntiles; j += NST) ring_unroll(iter, j, std::make_integer_sequence<int, NST>{});
   ring_tail(iter, j, ntiles, std::make_integer_sequence<int, NST - 1>{});
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (cpart != nullptr)  // qkv-bias gradient: this block's dQ column sums
-    colsum128_part(dq, scale, qok, reinterpret_cast<float*>(&smem[0][0][0]),
-                   cpart + ((size_t)b * nqb + qb) * RS + (size_t)h * kD);
+  if (cpart != nullptr)  // qkv-bias gradient: this wave's dQ column sums (one partial row)
+    colsum32_wave(dq, scale, qok, cpart + (((size_t)b * nqb + qb) * 4 + w) * RS + (size_t)h * kD);
   if (qok) {
     bf16* dqrow = dqkv + ((size_t)b * T + qrow) * RS + (size_t)h * kD;
 #pragma unroll
@@ -1324,7 +1322,7 @@ void colsum(torch::Tensor x, torch::Tensor out);  // elementwise.hip
 
 // dbias (optional, fp32 [(H + 2·Hkv)·D]): += the column sums of dqkv over all B·T rows (the fused
 // QKV projection's bias gradient). Variants 3 / 4 without dropout produce them in the kernels'
-// epilogues (one fp32 partial row per 128-row block, finished by the deferred reduction); the
+// epilogues (one fp32 partial row per 32-row wave slice, finished by the deferred reduction); the
 // other paths run the column-sum kernel over dqkv.
 void flash_attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, torch::Tensor dqkv,
                     int64_t H, int64_t Hkv, int64_t D, double scale, double p_drop, int64_t seed,
@@ -1367,7 +1365,7 @@ void flash_attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, to
                     dbias->numel() == W, "dbias must be a contiguous fp32 [(H + 2*Hkv)*D] GPU tensor");
   const bool fused_bias = want_bias && !drop && g_fa_bwd_variant != 2;
   torch::Tensor part;
-  if (fused_bias) part = torch::empty({(int64_t)B * nblk, W}, qkv.options().dtype(torch::kFloat32));
+  if (fused_bias) part = torch::empty({(int64_t)B * nblk * 4, W}, qkv.options().dtype(torch::kFloat32));
   float* pp = fused_bias ? part.data_ptr<float>() : nullptr;
   hipLaunchKernelGGL(kv, gkv, dim3(256), 0, stream, q, d, lse.data_ptr<float>(), delta.data_ptr<float>(), g, pp, T,
                      (int)H, (int)Hkv, (float)scale, pd, (uint64_t)seed);
@@ -1375,7 +1373,7 @@ void flash_attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, to
                      (int)H, (int)Hkv, (float)scale, pd, (uint64_t)seed);
   if (fused_bias) {
     float* outs[1] = {dbias->data_ptr<float>()};
-    reduce_partials_auto(part, 1, B * nblk, W, outs, stream);
+    reduce_partials_auto(part, 1, B * nblk * 4, W, outs, stream);
   } else if (want_bias) {
     colsum(dqkv.view({(int64_t)B * T, W}), *dbias);
   }

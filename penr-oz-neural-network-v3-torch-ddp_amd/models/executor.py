@@ -18,7 +18,8 @@ head: final LN → lm_head GEMM → cross-entropy (HIP: one LDS-resident pass pe
 backward mirrors it: dgrad/wgrad GEMMs (wgrad accumulated in fp32), GELU backward fused with
   the fc bias-gradient column sum, LayerNorm backward fused with dγ/dβ, the residual-gradient
   accumulation, its bf16 copy for the next GEMM, and the bias gradient of the preceding
-  linear; flash-attention backward; embedding backward (dwte scatter, dwpe reduction).
+  linear; flash-attention backward with the qkv bias gradient summed in its epilogues; embedding
+  backward (dwte scatter, dwpe reduction).
 
 Dropout (the HF GPT-2 import: embd/resid/attn_pdrop = 0.1, ``mappers.py:140-142`` in the
 reference): attention dropout runs inside the flash kernels; embedding dropout inside the
@@ -212,6 +213,7 @@ class GPTExecutor:
         self._reduce_pending = False
         import os
         self._overlap_opt = os.environ.get("PENROZ_OVERLAP_OPT", "1") != "0"
+        self._fused_qkv_bias = os.environ.get("PENROZ_FUSED_QKV_BIAS", "1") != "0"
         self._side_init()
 
     def _param_order(self):
@@ -497,8 +499,9 @@ class GPTExecutor:
                 self.reducer.bucket_ready(bkt)
 
     # ---- weight gradients on a side HIP stream -------------------------------------------------
-    # The weight-gradient GEMMs, the qkv bias column sum and the finishing kernels of every
-    # dγ / dβ / bias column reduction are off the backward's critical path (nothing in the
+    # The weight-gradient GEMMs and the finishing kernels of every dγ / dβ / bias column reduction
+    # (the qkv bias partials come from the attention-backward epilogues) are off the backward's
+    # critical path (nothing in the
     # backward reads parameter gradients), so they run on a second stream and overlap the
     # main stream's dgrad GEMMs, LayerNorm / GELU backward, flash-attention backward. Ordering: the side stream waits on an event
     # recorded after each operand's producer; before the main stream overwrites a rotating
@@ -638,10 +641,14 @@ class GPTExecutor:
             torch.mm(dres_bf, self._dgrad_w(b.proj.weight), out=self.d_c)
             self._wgrad(dres_bf, self.att[l], b.proj.weight)
             # the qkv bias gradient comes out of the attention-backward epilogues (partials finished
-            # on the side stream by the deferred reduction)
+            # on the side stream by the deferred reduction); PENROZ_FUSED_QKV_BIAS=0: a column-sum
+            # pass over dqkv on the side stream instead (A/B)
+            fused_bias = self._fused_qkv_bias
             attn_ops.flash_bwd(self.d_c.view(B, T, C), self.qkv[l].view(B, T, 3 * C), self.att[l].view(B, T, C),
                                self.lse[l], s.H, s.H, s.D, b.attn.dropout, seed + l, dqkv=dqkv.view(B, T, 3 * C),
-                               dbias=self.grad(b.qkv.bias))
+                               dbias=self.grad(b.qkv.bias) if fused_bias else None)
+            if not fused_bias:
+                self._side_call(dqkv, lambda: fused_ops.colsum(dqkv, self.grad(b.qkv.bias)))
             torch.mm(dqkv, self._dgrad_w(b.qkv.weight), out=self.d_c)
             self._wgrad(dqkv, self.ln1[l], b.qkv.weight)
             mean, rstd, _, _ = self.stats[l]
