@@ -99,7 +99,7 @@ PYBIND11_MODULE(penroz_kernels, m) {
   m.def("rms_residual", &rms_residual);
   m.def("gelu_fwd", &gelu_fwd);
   m.def("gelu_bwd", &gelu_bwd);
-  m.def("colsum", &colsum); returns the previous");
+  m.def("colsum", &colsum);
   m.def("gated_act_fwd", &gated_act_fwd);
   m.def("gated_act_packed", &gated_act_packed);
   m.def("gated_act_bwd", &gated_act_bwd);
