@@ -1,4 +1,4 @@
-"""Weight-gradient GEMM A/B at the GPT-2 124M shapes (M = 65 536 tokens): the native kernel
+"""Weight-gradient GEMM A/B at the GPT-2 124M (or ``--model gpt2-xl``) shapes (M = 65 536 tokens): the native kernel
 (``wgrad_gemm``) vs hipBLASLt through ``torch.addmm(g, dy.t(), x, out_dtype=float32)`` with
 the fp32 gradient accumulated in place (beta = 1). Run with PYTORCH_TUNABLEOP_ENABLED=1
 PYTORCH_TUNABLEOP_TUNING=1 to let TunableOp search hipBLASLt/rocBLAS solutions for the library
@@ -16,7 +16,13 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 from penroz.ops import _ext  # noqa: E402
 
-SHAPES = {"qkv": (2304, 768), "proj": (768, 768), "fc": (3072, 768), "fc2": (768, 3072), "lm_head": (50304, 768)}
+def shapes(C: int, L: int, V: int = 50304) -> tuple[dict, dict]:
+    """(out, in) of every weight gradient of a GPT-2 layout of width C, and calls per step."""
+    sh = {"qkv": (3 * C, C), "proj": (C, C), "fc": (4 * C, C), "fc2": (C, 4 * C), "lm_head": (V, C)}
+    return sh, {"qkv": L, "proj": L, "fc": L, "fc2": L, "lm_head": 1}
+
+
+MODELS = {"gpt2-124m": (768, 12), "gpt2-xl": (1600, 48)}
 
 
 def timeit(fn, iters):
@@ -34,11 +40,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--tokens", type=int, default=65536)
+    ap.add_argument("--model", default="gpt2-124m", choices=list(MODELS))
     a = ap.parse_args()
+    SHAPES, per_layer = shapes(*MODELS[a.model])
     N = a.tokens
     k = _ext.kernels()
     tot = {"native_ms": 0.0, "blas_ms": 0.0}
-    per_layer = {"qkv": 12, "proj": 12, "fc": 12, "fc2": 12, "lm_head": 1}
     for name, (m, n) in SHAPES.items():
         torch.manual_seed(0)
         dy = (torch.rand(N, m, device="cuda") * 2 - 1).to(torch.bfloat16)
@@ -64,7 +71,7 @@ def main():
                           "blas_bf16out_plus_add_us": round(t16a * 1e6, 1)}),
               flush=True)
         del dy, x, g1, g2, wb
-    print(json.dumps({k2: round(v, 2) for k2, v in tot.items()} | {"per": "GPT-2 124M step"}), flush=True)
+    print(json.dumps({k2: round(v, 2) for k2, v in tot.items()} | {"per": f"{a.model} step"}), flush=True)
 
 
 if __name__ == "__main__":
