@@ -38,14 +38,16 @@ def main():
     ap.add_argument("--D", type=int, default=64)
     ap.add_argument("--which", default="fwd,bwd")
     ap.add_argument("--sdpa", action="store_true")
+    ap.add_argument("--p", type=float, default=0.0, help="attention dropout probability")
+    ap.add_argument("--bwd-variants", default="3,4", help="flash backward variants to time (head_dim 64)")
     a = ap.parse_args()
     B, T, H, D = a.B, a.T, a.H, a.D
     Hkv = a.Hkv or H
     torch.manual_seed(0)
     qkv = torch.randn(B, T, (H + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
     fl = 4.0 * B * H * T * T * D / 2
-    res = {"B": B, "T": T, "H": H, "Hkv": Hkv, "D": D}
-    out, lse = A.flash_fwd(qkv, H, Hkv, D)
+    res = {"B": B, "T": T, "H": H, "Hkv": Hkv, "D": D, "p": a.p}
+    out, lse = A.flash_fwd(qkv, H, Hkv, D, a.p, 7)
     if "fwd" in a.which:
         from penroz.ops._ext import kernels
         k = kernels()
@@ -53,7 +55,7 @@ def main():
         for v in variants:
             if v:
                 prev = k.flash_fwd_variant(v)
-            t = timeit(lambda: A.flash_fwd(qkv, H, Hkv, D, out=out, lse=lse), a.iters)
+            t = timeit(lambda: A.flash_fwd(qkv, H, Hkv, D, a.p, 7, out=out, lse=lse), a.iters)
             sfx = f"_v{v}" if v else ""
             res.update({f"fwd{sfx}_us": round(t * 1e6, 1), f"fwd{sfx}_TF": round(fl / t / 1e12, 1)})
             if v:
@@ -63,11 +65,11 @@ def main():
         k = kernels()
         dout = torch.randn_like(out)
         dq = torch.empty_like(qkv)
-        variants = [2, 3, 4] if (hasattr(k, "flash_bwd_variant") and D == 64) else [0]
+        variants = [int(v) for v in a.bwd_variants.split(",")] if (hasattr(k, "flash_bwd_variant") and D == 64) else [0]
         for v in variants:
             if v:
                 prev = k.flash_bwd_variant(v)
-            t = timeit(lambda: A.flash_bwd(dout, qkv, out, lse, H, Hkv, D, dqkv=dq), a.iters)
+            t = timeit(lambda: A.flash_bwd(dout, qkv, out, lse, H, Hkv, D, a.p, 7, dqkv=dq), a.iters)
             sfx = f"_v{v}" if v else ""
             res.update({f"bwd{sfx}_us": round(t * 1e6, 1), f"bwd{sfx}_TF": round(2.5 * fl / t / 1e12, 1)})
             if v:

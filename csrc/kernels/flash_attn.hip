@@ -464,215 +464,18 @@ __global__ void __launch_bounds__(256) fa_bwd_pre_kernel(const bf16* __restrict_
 }
 
 // ------------------------------------------------------------------------------------------
-// dK / dV, variant 2 (also the dropout path): grid (ceil(T/128) key blocks, B*Hkv); wave w owns
-// keys kb*128 + 32w + (lane&31); P / dS are computed in place in the S / dP accumulators. The
-// Q / dO slices and their LSE / δ rows arrive by LDS-DMA into a 3-stage ring, two slices ahead, so
-// global latency hides behind two iterations of MFMA work instead of one; K / V fragments are
-// laundered so no compiler-tracked load is outstanding inside the loop. Per iteration: waves
-// 0-1 fetch the Q slice (4 pieces each), waves 2-3 the dO slice, waves 0 / 1 also the LSE / δ
-// rows (one 4-byte DMA each).
-template <bool DROPOUT>
-__global__ void __launch_bounds__(256, 2) fa_bwd_dkdv2_kernel(const bf16* __restrict__ qkv,
-                                                              const bf16* __restrict__ dout,
-                                                              const float* __restrict__ lse,
-                                                              const float* __restrict__ delta,
-                                                              bf16* __restrict__ dqkv, float* __restrict__ cpart, int T, int H, int Hkv,
-                                                              float scale, float p_drop, uint64_t seed) {
-  constexpr int BK = 128, QS = 64, NST = 3;
-  constexpr int TILE = QS * 128;              // one 64-row slice, 128-B rows
-  constexpr int STAGE = 2 * TILE + 512;       // Q | dO | LSE[64] | δ[64]
-  __shared__ __attribute__((aligned(16))) char smem[NST * STAGE];
-  int kb, bh;
-  xcd_head_block(kb, bh);
-  const int b = bh / Hkv, hk = bh % Hkv;
-  const int G = H / Hkv;
-  const int lane = threadIdx.x & 63, w = wave_id(), hh = lane >> 5;
-  const size_t RS = (size_t)(H + 2 * Hkv) * kD;
-  const size_t ORS = (size_t)H * kD;
-  const int kw0 = kb * BK + 32 * w;
-  const int key = kw0 + (lane & 31);
-  const float c = scale * kLog2e;
-  const float inv_keep = DROPOUT ? 1.f / (1.f - p_drop) : 1.f;
-
-  const bf16* kbase = qkv + (size_t)b * T * RS + (size_t)(H + hk) * kD;
-  const bf16* vbase = qkv + (size_t)b * T * RS + (size_t)(H + Hkv + hk) * kD;
-  uint4 kf[4], vf[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    kf[s] = key < T ? *reinterpret_cast<const uint4*>(kbase + (size_t)key * RS + 16 * s + 8 * hh) : zero4();
-    vf[s] = key < T ? *reinterpret_cast<const uint4*>(vbase + (size_t)key * RS + 16 * s + 8 * hh) : zero4();
-  }
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    launder(kf[s]);
-    launder(vf[s]);
-  }
-  f32x16 dk[2], dv[2];
-#pragma unroll
-  for (int dh = 0; dh < 2; ++dh)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) dk[dh][i] = dv[dh][i] = 0.f;
-
-  const int s_first = (kb * BK) / QS;
-  const int nslices = (T + QS - 1) / QS;
-  const int per_head = nslices - s_first;
-  const int total = G * per_head;
-
-  // DMA roles: w0/w1 -> Q rows 32w'..32w'+31 (pieces 4w'..4w'+3), w2/w3 -> dO likewise
-  const int is_do = w >> 1, half_sel = w & 1;
-  const unsigned rsb = (unsigned)(is_do ? ORS : RS) * 2;  // row stride in bytes
-  unsigned voff[2];
-#pragma unroll
-  for (int par = 0; par < 2; ++par) {
-    const int row = 8 * par + (lane >> 3);
-    const int ch = (lane & 7) ^ ((((row >> 1) & 1) << 2) | ((row >> 2) & 3));
-    voff[par] = (unsigned)(lane >> 3) * rsb + 16u * ch;
-  }
-  auto dma = [&](int it) {
-    const int itc = min(it, total - 1);  // beyond the end: refetch the last slice (uniform counts)
-    const int hq = hk * G + itc / per_head;
-    const int qs0 = (s_first + itc % per_head) * QS;
-    const unsigned st = __builtin_amdgcn_readfirstlane(lds_addr_of(smem + (it % NST) * STAGE));
-    const bf16* src = is_do ? dout + (size_t)b * T * ORS + (size_t)hq * kD : qkv + (size_t)b * T * RS + (size_t)hq * kD;
-    const size_t rs = is_do ? ORS : RS;
-    const unsigned dst = st + is_do * TILE + half_sel * 4096;
-    if (qs0 + QS <= T) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int p = 4 * half_sel + i;
-        glds16_s(reinterpret_cast<const char*>(src + (size_t)(qs0 + 8 * p) * rs), voff[p & 1], dst + i * 1024);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int p = 4 * half_sel + i;
-        const int row = 8 * p + (lane >> 3);
-        const int ch = (lane & 7) ^ ((((row >> 1) & 1) << 2) | ((row >> 2) & 3));
-        glds16(src + (size_t)min(qs0 + row, T - 1) * rs + 8 * ch, dst + i * 1024);
-      }
-    }
-    if (w < 2) {  // LSE (w0) / δ (w1) rows, clamped to T-1 (those rows are masked anyway)
-      const float* sp = (w == 0 ? lse : delta) + ((size_t)b * H + hq) * T + min(qs0 + lane, T - 1);
-      glds4(sp, st + 2 * TILE + 256 * w);
-    }
-  };
-  auto wait_next = [&]() {  // this wave's DMAs for the next stage done; the one after in flight
-    if (w < 2)
-      asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  };
-
-  if (total > 0) {
-    dma(0);
-    dma(1);
-    wait_next();
-  }
-  __syncthreads();
-  for (int it = 0; it < total; ++it) {
-    dma(it + 2);  // into the stage consumed at it-1 (freed by its barrier)
-    const char* stg = smem + (it % NST) * STAGE;
-    const float* lse_s = reinterpret_cast<const float*>(stg + 2 * TILE);
-    const float* del_s = lse_s + QS;
-    const int hq = hk * G + it / per_head;
-    const int qs0 = (s_first + it % per_head) * QS;
-    bool act[2];
-    f32x16 sp[2], dp[2];
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      const int qh0 = qs0 + 32 * half;
-      act[half] = qh0 + 31 >= kw0 && kw0 < T && qh0 < T;
-      if (act[half]) {
-        const char* Qt = stg + half * 32 * 128;
-        const char* Dt = stg + TILE + half * 32 * 128;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const float4_t dl = *reinterpret_cast<const float4_t*>(&del_s[32 * half + 8 * g + 4 * hh]);
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            sp[half][4 * g + k] = 0.f;
-            dp[half][4 * g + k] = DROPOUT ? 0.f : -dl[k];
-          }
-        }
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          sp[half] = mfma32(row_frag(Qt, 0, s, lane), kf[s], sp[half]);
-          dp[half] = mfma32(row_frag(Dt, 0, s, lane), vf[s], dp[half]);
-        }
-      }
-    }
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      const int qh0 = qs0 + 32 * half;
-      if (act[half]) {
-        const char* Qt = stg + half * 32 * 128;
-        const char* Dt = stg + TILE + half * 32 * 128;
-        const bool need_mask = (kw0 + 31 > qh0) || (qh0 + 32 > T) || (kw0 + 32 > T);
-        auto grads = [&](auto mask_tag) {
-          constexpr bool MASK = decltype(mask_tag)::value;
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int r0 = 8 * g + 4 * hh;
-            const float4_t l2 = *reinterpret_cast<const float4_t*>(&lse_s[32 * half + r0]) * kLog2e;
-            float4_t dl = {0.f, 0.f, 0.f, 0.f};
-            if constexpr (DROPOUT) dl = *reinterpret_cast<const float4_t*>(&del_s[32 * half + r0]);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              const int i = 4 * g + k;
-              const int q = qh0 + r0 + k;
-              float p = fexp2(fmaf(sp[half][i], c, -l2[k]));
-              if constexpr (MASK) p = (key > q || q >= T || key >= T) ? 0.f : p;
-              if constexpr (DROPOUT) {
-                const bool keep = dropout_keep(seed, b, hq, H, T, q, key, p_drop);
-                sp[half][i] = keep ? p * inv_keep : 0.f;
-                dp[half][i] = p * ((keep ? dp[half][i] * inv_keep : 0.f) - dl[k]);
-              } else {
-                sp[half][i] = p;
-                dp[half][i] = p * dp[half][i];
-              }
-            }
-          }
-        };
-        if (need_mask)
-          grads(std::true_type{});
-        else
-          grads(std::false_type{});
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss) {
-          const uint4 pf = acc_frag(sp[half], ss), sf = acc_frag(dp[half], ss);
-#pragma unroll
-          for (int dh = 0; dh < 2; ++dh) {
-            dv[dh] = mfma32(tr_frag(Dt, 16 * ss, 32 * dh, lane), pf, dv[dh]);
-            dk[dh] = mfma32(tr_frag(Qt, 16 * ss, 32 * dh, lane), sf, dk[dh]);
-          }
-        }
-      }
-    }
-    wait_next();
-    __syncthreads();
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (key < T) {
-    bf16* dkrow = dqkv + ((size_t)b * T + key) * RS + (size_t)(H + hk) * kD;
-    bf16* dvrow = dqkv + ((size_t)b * T + key) * RS + (size_t)(H + Hkv + hk) * kD;
-#pragma unroll
-    for (int dh = 0; dh < 2; ++dh)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d = 32 * dh + 8 * g + 4 * hh;
-        store4(dkrow + d, dk[dh][4 * g] * scale, dk[dh][4 * g + 1] * scale, dk[dh][4 * g + 2] * scale,
-               dk[dh][4 * g + 3] * scale);
-        store4(dvrow + d, dv[dh][4 * g], dv[dh][4 * g + 1], dv[dh][4 * g + 2], dv[dh][4 * g + 3]);
-      }
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// dK / dV, variant 3: fa_bwd_dkdv2_kernel with every LDS fragment address precomputed per lane
-// (4 row-read + 4 transposed-read offsets; the 32-row half, the 16-row sub-block and — the loop
-// unrolled by the 3 ring stages — the stage base all become immediates), removing the ~140
-// swizzle-address VALU instructions per iteration that the compiler otherwise rematerialises.
-// NST = ring depth, NST - 1 slices in flight (3: variant 3, 4: variant 4).
+// dK / dV: grid (ceil(T/128) key blocks, B*Hkv); wave w owns keys kb*128 + 32w + (lane&31); P / dS
+// are computed in place in the S / dP accumulators. The Q / dO slices (64 rows) and their LSE / δ
+// rows arrive by LDS-DMA into an NST-stage ring, NST - 1 slices ahead, so global latency hides
+// behind iterations of MFMA work; K / V fragments are laundered so no compiler-tracked load is
+// outstanding inside the loop. Per iteration waves 0-1 fetch the Q slice (4 pieces each), waves
+// 2-3 the dO slice, waves 0 / 1 also the LSE / δ rows (one 4-byte DMA each). Every LDS fragment
+// address is precomputed per lane (4 row-read + 4 transposed-read offsets; the 32-row half, the
+// 16-row sub-block and — the loop unrolled by the ring stages — the stage base become
+// immediates), removing ~140 swizzle-address VALU instructions per iteration.
+// NST = ring depth (3: variant 3, default; 4: variant 4). Dropout (hashed mask regenerated per
+// score) spills 9 VGPRs outside the hot loop and still beats the former rolled-ring kernel
+// (975 vs 987 µs at the GPT-2 shape, p = 0.1; profiles/attn_bench_r2_dropout_ring.log).
 template <int NST>
 struct RingWait {  // s_waitcnt that leaves the newest NST - 2 stages' DMAs in flight
   template <int PER>  // DMA instructions per stage and wave (4 pieces, +1 LSE / δ row)
@@ -924,167 +727,10 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv3_kernel(const bf16* __rest
   }
 }
 
-// ------------------------------------------------------------------------------------------
-// dQ, variant 2 (also the dropout path of variant 2): grid (ceil(T/128) query blocks, heaviest
-// first, B*H); forward-shaped — a wave keeps 32 query rows' Q, dO, LSE, δ and dQᵀ in registers
-// while K / V tiles of 64 keys arrive by LDS-DMA into a 3-stage ring, two tiles ahead.
-template <bool DROPOUT>
-__global__ void __launch_bounds__(256, 2) fa_bwd_dq3_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
-                                                        const float* __restrict__ lse,
-                                                        const float* __restrict__ delta, bf16* __restrict__ dqkv, float* __restrict__ cpart,
-                                                        int T, int H, int Hkv, float scale, float p_drop,
-                                                        uint64_t seed) {
-  constexpr int BM = 128, BN = 64;
-  constexpr int NST = 3;
-  __shared__ __attribute__((aligned(16))) char smem[NST][2][BN * 128];
-  const int nqb = (T + BM - 1) / BM;
-  int qi, bh;
-  xcd_head_block(qi, bh);
-  const int qb = nqb - 1 - qi;
-  const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
-  const int lane = threadIdx.x & 63, w = wave_id(), hh = lane >> 5;
-  const size_t RS = (size_t)(H + 2 * Hkv) * kD;
-  const size_t ORS = (size_t)H * kD;
-  const bf16* kbase = qkv + (size_t)b * T * RS + (size_t)(H + hk) * kD;
-  const bf16* vbase = qkv + (size_t)b * T * RS + (size_t)(H + Hkv + hk) * kD;
-  const int q0 = qb * BM + 32 * w;
-  const int qrow = q0 + (lane & 31);
-  const float c = scale * kLog2e;
-  const float inv_keep = DROPOUT ? 1.f / (1.f - p_drop) : 1.f;
-
-  uint4 qf[4], dof[4];
-  const bool qok = qrow < T;
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    qf[s] = qok ? *reinterpret_cast<const uint4*>(qkv + (size_t)b * T * RS + (size_t)h * kD + (size_t)qrow * RS + 16 * s +
-                                                  8 * hh)
-                : zero4();
-    dof[s] = qok ? *reinterpret_cast<const uint4*>(dout + (size_t)b * T * ORS + (size_t)h * kD + (size_t)qrow * ORS +
-                                                   16 * s + 8 * hh)
-                 : zero4();
-  }
-  const size_t rr = ((size_t)b * H + h) * T + qrow;
-  float l2 = qok ? lse[rr] * kLog2e : 0.f;
-  float dl = qok ? delta[rr] : 0.f;
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    launder(qf[s]);
-    launder(dof[s]);
-  }
-  asm volatile("" : "+v"(l2), "+v"(dl));
-
-  // LDS-DMA ring (3 stages, two tiles ahead): waves 0-1 fetch the K tile, waves 2-3 the V
-  // tile, 4 pieces (8 keys x 128 B each) per wave, tile_off image
-  const int is_v = w >> 1, half_sel = w & 1;
-  const unsigned RSB = (unsigned)RS * 2;
-  unsigned voff[2];
-#pragma unroll
-  for (int par = 0; par < 2; ++par) {
-    const int row = 8 * par + (lane >> 3);
-    const int ch = (lane & 7) ^ ((((row >> 1) & 1) << 2) | ((row >> 2) & 3));
-    voff[par] = (unsigned)(lane >> 3) * RSB + 16u * ch;
-  }
-  const bf16* dsrc = is_v ? vbase : kbase;
-  const int kend = min(T, qb * BM + BM);
-  const int ntiles = (kend + BN - 1) / BN;
-  f32x16 dq[2];
-#pragma unroll
-  for (int dh = 0; dh < 2; ++dh)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) dq[dh][i] = 0.f;
-
-  auto dma = [&](int jt) {
-    const int kt0 = min(jt, ntiles - 1) * BN;  // beyond the end: refetch the last tile (uniform counts)
-    const unsigned dst = __builtin_amdgcn_readfirstlane(lds_addr_of(smem[jt % NST][is_v])) + half_sel * 4096;
-    if (kt0 + BN <= T) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int p = 4 * half_sel + i;
-        glds16_s(reinterpret_cast<const char*>(dsrc + (size_t)(kt0 + 8 * p) * RS), voff[p & 1], dst + i * 1024);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int p = 4 * half_sel + i;
-        const int row = 8 * p + (lane >> 3);
-        const int ch = (lane & 7) ^ ((((row >> 1) & 1) << 2) | ((row >> 2) & 3));
-        glds16(dsrc + (size_t)min(kt0 + row, T - 1) * RS + 8 * ch, dst + i * 1024);
-      }
-    }
-  };
-  dma(0);
-  dma(1);
-  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  __syncthreads();
-  for (int j = 0; j < ntiles; ++j) {
-    const int kt0 = j * BN;
-    dma(j + 2);  // into the stage consumed at j-1 (freed by its barrier)
-    const char* Kt = smem[j % NST][0];
-    const char* Vt = smem[j % NST][1];
-    if (kt0 <= q0 + 31) {
-      // dP starts from -δ (row constant = this lane's query row); per 32-key half the dS math
-      // is followed by its dQ MFMAs so the second half's VALU overlaps the first half's MFMAs
-      f32x16 s[2], dp[2];
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          s[kh][i] = 0.f;
-          dp[kh][i] = DROPOUT ? 0.f : -dl;
-        }
-#pragma unroll
-        for (int st = 0; st < 4; ++st) {
-          s[kh] = mfma32(row_frag(Kt, 32 * kh, st, lane), qf[st], s[kh]);
-          dp[kh] = mfma32(row_frag(Vt, 32 * kh, st, lane), dof[st], dp[kh]);
-        }
-      }
-      const bool need_mask = (kt0 + BN - 1 > q0) || (kt0 + BN > T) || (q0 + 32 > T);
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh) {
-        auto grads = [&](auto mask_tag) {
-          constexpr bool MASK = decltype(mask_tag)::value;
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int k = kt0 + 32 * kh + acc_row(i, lane);
-            float p = fexp2(fmaf(s[kh][i], c, -l2));
-            if constexpr (MASK) p = (k > qrow || k >= T || !qok) ? 0.f : p;
-            if constexpr (DROPOUT) {
-              const bool keep = dropout_keep(seed, b, h, H, T, qrow, k, p_drop);
-              s[kh][i] = p * ((keep ? dp[kh][i] * inv_keep : 0.f) - dl);
-            } else {
-              s[kh][i] = p * dp[kh][i];
-            }
-          }
-        };
-        if (need_mask)
-          grads(std::true_type{});
-        else
-          grads(std::false_type{});
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss) {
-          const uint4 sf = acc_frag(s[kh], ss);
-#pragma unroll
-          for (int dh = 0; dh < 2; ++dh) dq[dh] = mfma32(tr_frag(Kt, 32 * kh + 16 * ss, 32 * dh, lane), sf, dq[dh]);
-        }
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // tile j+1 landed, j+2 in flight
-    __syncthreads();
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (qok) {
-    bf16* dqrow = dqkv + ((size_t)b * T + qrow) * RS + (size_t)h * kD;
-#pragma unroll
-    for (int dh = 0; dh < 2; ++dh)
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        store4(dqrow + 32 * dh + 8 * g + 4 * hh, dq[dh][4 * g] * scale, dq[dh][4 * g + 1] * scale,
-               dq[dh][4 * g + 2] * scale, dq[dh][4 * g + 3] * scale);
-  }
-}
-
-// dQ, variant 3: fa_bwd_dq3_kernel with precomputed per-lane LDS fragment offsets and the ring
-// loop unrolled by its 3 stages (stage bases and row bases become immediates), as dK/dV variant 3.
+// dQ: grid (ceil(T/128) query blocks, heaviest first, B*H); forward-shaped — a wave keeps 32 query
+// rows' Q, dO, LSE, δ and dQᵀ in registers while K / V tiles of 64 keys arrive by LDS-DMA into an
+// NST-stage ring; per-lane precomputed LDS fragment offsets and the ring loop unrolled by its
+// stages (stage bases and row bases become immediates), as in the dK/dV kernel.
 template <bool DROPOUT, int NST>
 __global__ void __launch_bounds__(256, 2) fa_bwd_dq4_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                                         const float* __restrict__ lse,
@@ -1303,11 +949,11 @@ void flash_attn_fwd(torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int
 
 // forward: 1 = single-stage (fa_fwd_kernel; also the dropout path), 3 = two query blocks per
 // wave (fa_fwd3_kernel, default). backward:
-// 2 = LDS-DMA pipelined dK/dV and dQ kernels, 3 = variant 2 with precomputed per-lane LDS offsets
-// and stage-unrolled 3-stage rings (default), 4 = variant 3 with 4-stage rings
+// 3 = LDS-DMA pipelined dK/dV and dQ kernels with precomputed per-lane LDS offsets and
+// stage-unrolled 3-stage rings (default; dropout included), 4 = the same with 4-stage rings
 int64_t flash_bwd_variant(int64_t v) {
   const int64_t prev = g_fa_bwd_variant;
-  TORCH_CHECK(v <= 0 || (v >= 2 && v <= 4), "flash backward variant must be 2, 3 or 4");
+  TORCH_CHECK(v <= 0 || v == 3 || v == 4, "flash backward variant must be 3 or 4");
   if (v > 0) g_fa_bwd_variant = (int)v;
   return prev;
 }
@@ -1318,12 +964,9 @@ int64_t flash_fwd_variant(int64_t v) {
   return prev;
 }
 
-void colsum(torch::Tensor x, torch::Tensor out);  // elementwise.hip
-
 // dbias (optional, fp32 [(H + 2·Hkv)·D]): += the column sums of dqkv over all B·T rows (the fused
-// QKV projection's bias gradient). Variants 3 / 4 without dropout produce them in the kernels'
-// epilogues (one fp32 partial row per 32-row wave slice, finished by the deferred reduction); the
-// other paths run the column-sum kernel over dqkv.
+// QKV projection's bias gradient), produced in the dK/dV and dQ epilogues (one fp32 partial row
+// per 32-row wave slice, finished by the deferred reduction).
 void flash_attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, torch::Tensor dqkv,
                     int64_t H, int64_t Hkv, int64_t D, double scale, double p_drop, int64_t seed,
                     c10::optional<torch::Tensor> dbias) {
@@ -1347,14 +990,11 @@ void flash_attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, to
                             uint64_t);
   const bool drop = p_drop > 0.0;
   BwdKernel kv, dq;
-  if (g_fa_bwd_variant == 2) {
-    kv = drop ? fa_bwd_dkdv2_kernel<true> : fa_bwd_dkdv2_kernel<false>;
-    dq = drop ? fa_bwd_dq3_kernel<true> : fa_bwd_dq3_kernel<false>;
-  } else if (g_fa_bwd_variant == 4) {  // 4-stage rings: three slices / tiles in flight
-    kv = drop ? fa_bwd_dkdv2_kernel<true> : fa_bwd_dkdv3_kernel<false, 4>;
+  if (g_fa_bwd_variant == 4) {  // 4-stage rings: three slices / tiles in flight
+    kv = drop ? fa_bwd_dkdv3_kernel<true, 4> : fa_bwd_dkdv3_kernel<false, 4>;
     dq = drop ? fa_bwd_dq4_kernel<true, 4> : fa_bwd_dq4_kernel<false, 4>;
-  } else {  // (dK/dV with dropout stays on variant 2: the unrolled ring spills with the mask hashing live)
-    kv = drop ? fa_bwd_dkdv2_kernel<true> : fa_bwd_dkdv3_kernel<false, 3>;
+  } else {
+    kv = drop ? fa_bwd_dkdv3_kernel<true, 3> : fa_bwd_dkdv3_kernel<false, 3>;
     dq = drop ? fa_bwd_dq4_kernel<true, 3> : fa_bwd_dq4_kernel<false, 3>;
   }
   const float pd = drop ? (float)p_drop : 0.f;
@@ -1363,18 +1003,15 @@ void flash_attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, to
   if (want_bias)
     TORCH_CHECK(dbias->is_cuda() && dbias->scalar_type() == torch::kFloat32 && dbias->is_contiguous() &&
                     dbias->numel() == W, "dbias must be a contiguous fp32 [(H + 2*Hkv)*D] GPU tensor");
-  const bool fused_bias = want_bias && !drop && g_fa_bwd_variant != 2;
   torch::Tensor part;
-  if (fused_bias) part = torch::empty({(int64_t)B * nblk * 4, W}, qkv.options().dtype(torch::kFloat32));
-  float* pp = fused_bias ? part.data_ptr<float>() : nullptr;
+  if (want_bias) part = torch::empty({(int64_t)B * nblk * 4, W}, qkv.options().dtype(torch::kFloat32));
+  float* pp = want_bias ? part.data_ptr<float>() : nullptr;
   hipLaunchKernelGGL(kv, gkv, dim3(256), 0, stream, q, d, lse.data_ptr<float>(), delta.data_ptr<float>(), g, pp, T,
                      (int)H, (int)Hkv, (float)scale, pd, (uint64_t)seed);
   hipLaunchKernelGGL(dq, gq, dim3(256), 0, stream, q, d, lse.data_ptr<float>(), delta.data_ptr<float>(), g, pp, T,
                      (int)H, (int)Hkv, (float)scale, pd, (uint64_t)seed);
-  if (fused_bias) {
+  if (want_bias) {
     float* outs[1] = {dbias->data_ptr<float>()};
     reduce_partials_auto(part, 1, B * nblk * 4, W, outs, stream);
-  } else if (want_bias) {
-    colsum(dqkv.view({(int64_t)B * T, W}), *dbias);
   }
 }

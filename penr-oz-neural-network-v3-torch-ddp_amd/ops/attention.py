@@ -77,7 +77,7 @@ def flash_fwd(qkv: Tensor, H: int, Hkv: int, D: int, dropout_p: float = 0.0, see
     return out, lse
 
 
-_BWD_VARIANT_ENV = "PENROZ_FLASH_BWD_VARIANT"  # 2 / 3 / 4 (A/B knob; unset = the kernel default)
+_BWD_VARIANT_ENV = "PENROZ_FLASH_BWD_VARIANT"  # 3 / 4 (A/B knob; unset = the kernel default, 3)
 _bwd_variant_applied = False
 
 
