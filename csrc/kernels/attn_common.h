@@ -67,12 +67,27 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t x) {
   return x;
 }
 
+// The same hash in pieces, for kernels that walk consecutive rows / key pairs: row·kDropRowMul and
+// (k>>1)·kDropKeyMul distribute over addition (mod 2³²), so a caller keeps one product per tile
+// and adds compile-time multiples of the constant instead of multiplying per element (v_mul_lo_u32
+// is a quarter-rate instruction; it dominated the dropout kernels' VALU time).
+constexpr uint32_t kDropRowMul = 0x9E3779B1u, kDropKeyMul = 0x85EBCA6Bu;
+__device__ __forceinline__ uint32_t dropout_seedmix(uint64_t seed) {
+  return (uint32_t)seed ^ ((uint32_t)(seed >> 32) * 0x27D4EB2Fu);
+}
+__device__ __forceinline__ uint32_t dropout_thr(float p) { return (uint32_t)(p * 65536.f); }
+// hashed input = seedmix ^ row·kDropRowMul ^ (k>>1)·kDropKeyMul (row = (b·H + h)·T + q), given as two
+// XOR terms so a kernel pre-combines the seed mix with whichever term is constant per lane
+// (x ^ y: one operand per lane, the other per element); odd = k & 1 picks the 16-bit half
+__device__ __forceinline__ bool dropout_keep_mixed(uint32_t x, uint32_t y, bool odd, uint32_t thr) {
+  const uint32_t hsh = fmix32(x ^ y);
+  const uint32_t u16 = odd ? (hsh >> 16) : (hsh & 0xFFFFu);
+  return u16 >= thr;
+}
+
 __device__ __forceinline__ bool dropout_keep(uint64_t seed, int b, int h, int H, int T, int q, int k, float p) {
-  const uint32_t row = (uint32_t)((b * H + h) * T + q);
-  const uint32_t rowkey = ((uint32_t)seed ^ ((uint32_t)(seed >> 32) * 0x27D4EB2Fu)) ^ (row * 0x9E3779B1u);
-  const uint32_t hsh = fmix32(rowkey ^ ((uint32_t)(k >> 1) * 0x85EBCA6Bu));
-  const uint32_t u16 = (k & 1) ? (hsh >> 16) : (hsh & 0xFFFFu);
-  return u16 >= (uint32_t)(p * 65536.f);
+  return dropout_keep_mixed(dropout_seedmix(seed) ^ ((uint32_t)((b * H + h) * T + q) * kDropRowMul),
+                            (uint32_t)(k >> 1) * kDropKeyMul, (k & 1) != 0, dropout_thr(p));
 }
 
 __device__ __forceinline__ uint4 zero4() { return uint4{0u, 0u, 0u, 0u}; }

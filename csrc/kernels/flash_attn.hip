@@ -65,6 +65,9 @@ __global__ void __launch_bounds__(256, 2) fa_fwd_kernel(const bf16* __restrict__
   const bf16* vbase = qkv + (size_t)b * T * RS + (size_t)(H + Hkv + hk) * kD;
   const int q0 = qb * BM + 32 * w;
   const int qrow = q0 + (lane & 31);
+  // dropout hash pieces (attn_common.h): per-lane seed mix ^ row product, 16-bit threshold
+  const uint32_t drow = DROPOUT ? dropout_seedmix(seed) ^ ((uint32_t)((b * H + h) * T + qrow) * kDropRowMul) : 0u;
+  const uint32_t dthr = dropout_thr(p_drop);
   const float c = scale * kLog2e;
   const float inv_keep = DROPOUT ? 1.f / (1.f - p_drop) : 1.f;
 
@@ -107,6 +110,7 @@ __global__ void __launch_bounds__(256, 2) fa_fwd_kernel(const bf16* __restrict__
   __syncthreads();
   for (int j = 0; j < ntiles; ++j) {
     const int kt0 = j * BN;
+    const uint32_t kpair0 = DROPOUT ? (uint32_t)((kt0 + 4 * hh) >> 1) * kDropKeyMul : 0u;
     if (j + 1 < ntiles) gload(kt0 + BN);
     const char* Kt = smem[j & 1][0];
     const char* Vt = smem[j & 1][1];
@@ -154,10 +158,10 @@ __global__ void __launch_bounds__(256, 2) fa_fwd_kernel(const bf16* __restrict__
           for (int i = 0; i < 16; i += 2) {
             float2_t p = {fexp2(fmaf(s[kh][i], c, negm)), fexp2(fmaf(s[kh][i + 1], c, negm))};
             lsum += p;
-            if constexpr (DROPOUT) {
-              const int key = kt0 + 32 * kh + acc_row(i, lane);
-              p[0] = dropout_keep(seed, b, h, H, T, qrow, key, p_drop) ? p[0] * inv_keep : 0.f;
-              p[1] = dropout_keep(seed, b, h, H, T, qrow, key + 1, p_drop) ? p[1] * inv_keep : 0.f;
+            if constexpr (DROPOUT) {  // keys (and key + 1) kt0 + 32kh + 4hh + (i&3) + 8(i>>2): one hash
+              const uint32_t km = kpair0 + (uint32_t)(16 * kh + 4 * (i >> 2) + ((i & 3) >> 1)) * kDropKeyMul;
+              p[0] = dropout_keep_mixed(drow, km, false, dthr) ? p[0] * inv_keep : 0.f;
+              p[1] = dropout_keep_mixed(drow, km, true, dthr) ? p[1] * inv_keep : 0.f;
             }
             s[kh][i] = p[0];
             s[kh][i + 1] = p[1];
@@ -521,6 +525,9 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv3_kernel(const bf16* __rest
   const size_t ORS = (size_t)H * kD;
   const int kw0 = kb * BK + 32 * w;
   const int key = kw0 + (lane & 31);
+  // dropout hash pieces (attn_common.h): seed mix ^ this lane's key-pair product, threshold
+  const uint32_t dkey = DROPOUT ? dropout_seedmix(seed) ^ ((uint32_t)(key >> 1) * kDropKeyMul) : 0u;
+  const uint32_t dthr = dropout_thr(p_drop);
   const float c = scale * kLog2e;
   const float inv_keep = DROPOUT ? 1.f / (1.f - p_drop) : 1.f;
 
@@ -660,6 +667,7 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv3_kernel(const bf16* __rest
         const char* Qt = stg + half * 32 * 128;
         const char* Dt = stg + TILE + half * 32 * 128;
         const bool need_mask = (kw0 + 31 > qh0) || (qh0 + 32 > T) || (kw0 + 32 > T);
+        const uint32_t drow0 = DROPOUT ? (uint32_t)((b * H + hq) * T + qh0 + 4 * hh) * kDropRowMul : 0u;
         auto grads = [&](auto mask_tag) {
           constexpr bool MASK = decltype(mask_tag)::value;
 #pragma unroll
@@ -674,8 +682,8 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv3_kernel(const bf16* __rest
               const int q = qh0 + r0 + k;
               float p = fexp2(fmaf(sp[half][i], c, -l2[k]));
               if constexpr (MASK) p = (key > q || q >= T || key >= T) ? 0.f : p;
-              if constexpr (DROPOUT) {
-                const bool keep = dropout_keep(seed, b, hq, H, T, q, key, p_drop);
+              if constexpr (DROPOUT) {  // row q = qh0 + 4hh + 8g + k: row product by addition
+                const bool keep = dropout_keep_mixed(drow0 + (uint32_t)(8 * g + k) * kDropRowMul, dkey, key & 1, dthr);
                 sp[half][i] = keep ? p * inv_keep : 0.f;
                 dp[half][i] = p * ((keep ? dp[half][i] * inv_keep : 0.f) - dl[k]);
               } else {
@@ -751,6 +759,9 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dq4_kernel(const bf16* __restri
   const bf16* vbase = qkv + (size_t)b * T * RS + (size_t)(H + Hkv + hk) * kD;
   const int q0 = qb * BM + 32 * w;
   const int qrow = q0 + (lane & 31);
+  // dropout hash pieces (attn_common.h): per-lane seed mix ^ row product, threshold
+  const uint32_t drow = DROPOUT ? dropout_seedmix(seed) ^ ((uint32_t)((b * H + h) * T + qrow) * kDropRowMul) : 0u;
+  const uint32_t dthr = dropout_thr(p_drop);
   const float c = scale * kLog2e;
   const float inv_keep = DROPOUT ? 1.f / (1.f - p_drop) : 1.f;
 
@@ -859,6 +870,7 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dq4_kernel(const bf16* __restri
         }
       }
       const bool need_mask = (kt0 + BN - 1 > q0) || (kt0 + BN > T) || (q0 + 32 > T);
+      const uint32_t kpair0 = DROPOUT ? (uint32_t)((kt0 + 4 * hh) >> 1) * kDropKeyMul : 0u;
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh) {
         auto grads = [&](auto mask_tag) {
@@ -868,8 +880,9 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dq4_kernel(const bf16* __restri
             const int k = kt0 + 32 * kh + acc_row(i, lane);
             float p = fexp2(fmaf(s[kh][i], c, -l2));
             if constexpr (MASK) p = (k > qrow || k >= T || !qok) ? 0.f : p;
-            if constexpr (DROPOUT) {
-              const bool keep = dropout_keep(seed, b, h, H, T, qrow, k, p_drop);
+            if constexpr (DROPOUT) {  // key k = kt0 + 32kh + 4hh + (i&3) + 8(i>>2); pairs share a hash
+              const uint32_t km = kpair0 + (uint32_t)(16 * kh + 4 * (i >> 2) + ((i & 3) >> 1)) * kDropKeyMul;
+              const bool keep = dropout_keep_mixed(drow, km, (i & 1) != 0, dthr);
               s[kh][i] = p * ((keep ? dp[kh][i] * inv_keep : 0.f) - dl);
             } else {
               s[kh][i] = p * dp[kh][i];
