@@ -82,7 +82,21 @@ MODELS = {
     # (reference mappers.py:122-176, neural_net_model.py:222); random init, no download
     "gpt2-hf": dict(V=50257, C=768, L=12, H=12, P=1024, hf=True),
     "tiny": dict(V=512, C=64, L=2, H=2, P=64),  # plumbing rehearsal only
+    # google/gemma-3-1b-pt text shapes through Mapper.from_hf_config (RMSNorm, RoPE, GQA 4:1,
+    # head_dim 256, gated GELU MLP, 262k vocab; random init, no checkpoint): the generic engine
+    # (autograd over the HIP layers: flash attention D=256, RMSNorm, gated activation)
+    "gemma3-1b": dict(V=262144, C=1152, L=26, H=4, P=32768, gemma=True),
 }
+
+
+def gemma3_1b_layers(L: int = 26) -> list[dict]:
+    from types import SimpleNamespace
+    from penroz.models.mapper import Mapper
+    return Mapper.from_hf_config(SimpleNamespace(
+        model_type="gemma3_text", vocab_size=262144, hidden_size=1152, intermediate_size=6912, num_hidden_layers=L,
+        num_attention_heads=4, num_key_value_heads=1, head_dim=256, rms_norm_eps=1e-6, rope_theta=1e6,
+        rope_local_base_freq=10000.0, attention_dropout=0.0, hidden_activation="gelu_pytorch_tanh",
+        query_pre_attn_scalar=256, sliding_window=512))
 
 
 def hf_gpt2_layers(V, C, L, H, P, pdrop=0.1):
@@ -122,7 +136,7 @@ def parse_args(argv=None):
     tiny = args.model == "tiny"
     args.batch = args.batch or (4 if tiny else 64)
     args.seq = args.seq or (32 if tiny else 1024)
-    args.engine = args.engine or ("fused" if args.device == "cuda" else "generic")
+    args.engine = args.engine or ("fused" if args.device == "cuda" and not MODELS[args.model].get("gemma") else "generic")
     if args.device == "cpu" and args.engine == "fused":
         raise SystemExit("the fused engine needs --device cuda")
     return args
@@ -252,14 +266,17 @@ def _build(args, cfg, device, engine, world):
     os.environ["PENROZ_ENGINE"] = engine
     torch.manual_seed(1234)
     dims = {k: cfg[k] for k in ("V", "C", "L", "H", "P")}
-    layers = hf_gpt2_layers(**dims) if cfg.get("hf") else gpt2_layers(**dims)
+    if cfg.get("gemma"):
+        layers = gemma3_1b_layers(cfg["L"])
+    else:
+        layers = hf_gpt2_layers(**dims) if cfg.get("hf") else gpt2_layers(**dims)
     model = NeuralNetworkModel("bench", Mapper(layers, {"adamw": {"lr": 6e-4, "betas": [0.9, 0.95], "eps": 1e-8}}))
     if cfg.get("hf"):
         for mod in model.modules():
             if isinstance(mod, (torch.nn.Linear, torch.nn.Embedding)):
                 torch.nn.init.normal_(mod.weight, 0.0, 0.02)
     model.to(device)
-    if cfg.get("hf") and device.type == "cuda":
+    if (cfg.get("hf") or cfg.get("gemma")) and device.type == "cuda":
         model.to(dtype=torch.bfloat16)  # what /import/ produces
     runner = _make_runner(model, engine, device, distributed=world > 1)
     model.train()
@@ -402,6 +419,7 @@ def run_rank(args):
             print(table, file=sys.stderr)
 
     n_params = sum(p.numel() for p in model.parameters())
+    n_linear = sum(m.weight.numel() for m in model.modules() if isinstance(m, torch.nn.Linear))
     runtime = None
     if args.via_runtime:
         ex = getattr(runner, "exec", None)
@@ -426,7 +444,10 @@ def run_rank(args):
         ref_tok_s = _reference_eager_tok_s(args, cfg, device, pool)
 
     if rank == 0:
-        flops_per_tok = 6 * (n_params - cfg["V"] * cfg["C"] - cfg["P"] * cfg["C"]) + 12 * cfg["L"] * cfg["C"] * T
+        if cfg.get("gemma"):  # matmul weights (tied lm_head counted as the Linear it is) + attention
+            flops_per_tok = 6 * n_linear + 12 * cfg["L"] * cfg["H"] * 256 * T
+        else:
+            flops_per_tok = 6 * (n_params - cfg["V"] * cfg["C"] - cfg["P"] * cfg["C"]) + 12 * cfg["L"] * cfg["C"] * T
         print(json.dumps({
             "metric": METRIC if args.model == "gpt2-124m" else f"tokens/sec (whole node) {args.model} DDP train",
             "value": tok_s, "unit": "tokens/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,

@@ -4,7 +4,8 @@
 //       with 16-B vectors; optionally rewrites the bf16 shadow copy the GEMMs read, so the
 //       master update and the low-precision refresh cost one pass (≈30 B/param of traffic).
 // multi-tensor: one launch over a device chunk table (tensor, offset) for parameter lists
-//       that are not flat (generic models).
+//       that are not flat (generic models); fp32, or bf16 parameters with bf16 state (what
+//       torch.optim keeps for them) updated in fp32 registers.
 // Math = torch.optim.AdamW / Adam single-tensor path: decoupled decay p *= 1 − lr·wd (AdamW)
 // or g += wd·p (Adam); m = lerp(m, g, 1 − β1); v = β2·v + (1 − β2)·g²;
 // p −= (lr / bc1) · m / (sqrt(v) / sqrt(bc2) + eps). Bias corrections come from the host in
@@ -66,25 +67,33 @@ __global__ void __launch_bounds__(256) adam_flat_kernel(float* __restrict__ p, c
 }
 
 struct TensorEntry {
-  float* p;
-  const float* g;
-  float* m;
-  float* v;
+  void* p;
+  const void* g;
+  void* m;
+  void* v;
   int64_t n;
 };
 
 constexpr int kChunk = 8192;
 
+// T = float, or bf16 for bf16 parameters (torch keeps their exp_avg / exp_avg_sq in bf16 too):
+// the update is computed in fp32 and each of p / m / v is rounded once on store (torch's foreach
+// path rounds after every elementwise op)
+template <typename T>
 __global__ void __launch_bounds__(256) adam_multi_kernel(const TensorEntry* __restrict__ tab,
                                                          const int32_t* __restrict__ chunk_tensor,
                                                          const int32_t* __restrict__ chunk_index, AdamHyper h) {
   const TensorEntry e = tab[chunk_tensor[blockIdx.x]];
+  T* P = static_cast<T*>(e.p);
+  const T* Gp = static_cast<const T*>(e.g);
+  T* M = static_cast<T*>(e.m);
+  T* V = static_cast<T*>(e.v);
   const int64_t start = (int64_t)chunk_index[blockIdx.x] * kChunk;
   const int64_t end = min(e.n, start + kChunk);
   for (int64_t i = start + threadIdx.x; i < end; i += blockDim.x) {
-    float pk = e.p[i], mk = e.m[i], vk = e.v[i];
-    adam_elem(pk, e.g[i], mk, vk, h);
-    e.p[i] = pk; e.m[i] = mk; e.v[i] = vk;
+    float pk = to_f(P[i]), mk = to_f(M[i]), vk = to_f(V[i]);
+    adam_elem(pk, to_f(Gp[i]), mk, vk, h);
+    P[i] = from_f<T>(pk); M[i] = from_f<T>(mk); V[i] = from_f<T>(vk);
   }
 }
 
@@ -139,14 +148,15 @@ void multi_tensor_adam(std::vector<torch::Tensor> ps, std::vector<torch::Tensor>
   const size_t nt = ps.size();
   TORCH_CHECK(gs.size() == nt && ms.size() == nt && vs.size() == nt);
   if (nt == 0) return;
+  const auto dt = ps[0].scalar_type();
+  TORCH_CHECK(dt == torch::kFloat32 || dt == torch::kBFloat16, "multi-tensor Adam: fp32 or bf16 tensors");
   std::vector<TensorEntry> tab(nt);
   std::vector<int32_t> ct, ci;
   for (size_t i = 0; i < nt; ++i) {
     for (auto* t : {&ps[i], &gs[i], &ms[i], &vs[i]})
-      TORCH_CHECK(t->is_cuda() && t->is_contiguous() && t->scalar_type() == torch::kFloat32 &&
-                  t->numel() == ps[i].numel(), "multi-tensor Adam needs contiguous fp32 tensors of equal size");
-    tab[i] = {ps[i].data_ptr<float>(), gs[i].data_ptr<float>(), ms[i].data_ptr<float>(), vs[i].data_ptr<float>(),
-              ps[i].numel()};
+      TORCH_CHECK(t->is_cuda() && t->is_contiguous() && t->scalar_type() == dt && t->numel() == ps[i].numel(),
+                  "multi-tensor Adam needs contiguous tensors of one dtype (fp32 or bf16) and equal size");
+    tab[i] = {ps[i].data_ptr(), gs[i].data_ptr(), ms[i].data_ptr(), vs[i].data_ptr(), ps[i].numel()};
     const int64_t chunks = (ps[i].numel() + kChunk - 1) / kChunk;
     for (int64_t c = 0; c < chunks; ++c) {
       ct.push_back((int32_t)i);
@@ -164,7 +174,11 @@ void multi_tensor_adam(std::vector<torch::Tensor> ps, std::vector<torch::Tensor>
   auto dev = host.to(ps[0].device(), /*non_blocking=*/true);
   const uint8_t* base = dev.data_ptr<uint8_t>();
   AdamHyper h = make_hyper(lr, b1, b2, eps, wd, step, grad_scale, maximize, decoupled);
-  hipLaunchKernelGGL(adam_multi_kernel, dim3(nchunks), dim3(256), 0, at::hip::getCurrentHIPStream(),
-                     reinterpret_cast<const TensorEntry*>(base), reinterpret_cast<const int32_t*>(base + tab_bytes),
-                     reinterpret_cast<const int32_t*>(base + tab_bytes + 4 * nchunks), h);
+  auto launch = [&](auto kernel) {
+    hipLaunchKernelGGL(kernel, dim3(nchunks), dim3(256), 0, at::hip::getCurrentHIPStream(),
+                       reinterpret_cast<const TensorEntry*>(base), reinterpret_cast<const int32_t*>(base + tab_bytes),
+                       reinterpret_cast<const int32_t*>(base + tab_bytes + 4 * nchunks), h);
+  };
+  if (dt == torch::kBFloat16) launch(adam_multi_kernel<bf16>);
+  else launch(adam_multi_kernel<float>);
 }

@@ -238,11 +238,15 @@ __global__ void __launch_bounds__(256) fa_gen_bwd_pre_kernel(const bf16* __restr
 // ------------------------------------------------------------------------------------------
 // dK / dV: grid (ceil(T/64) key blocks, B*Hkv); wave w owns keys kb*64 + 32w + (lane&31) and
 // sweeps 32-row query slices (every query head of its KV group) staged in LDS: Q | dO | LSE | δ.
+// Query-head split (part != nullptr, grid y = B*Hkv*G): each workgroup sweeps ONE query head of
+// its group and writes fp32 partial dK / dV ([G][B·T][K | V][Hkv·D]) that fa_gen_kv_reduce sums —
+// at Gemma-3 1B shapes (Hkv = 1, G = 4, B = 8) the unsplit grid is 128 workgroups of 2 waves for
+// 256 CUs.
 template <int D, bool DROPOUT>
 __global__ void __launch_bounds__(128, 1)
     fa_gen_bwd_dkdv_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
-                           const float* __restrict__ delta, bf16* __restrict__ dqkv, int T, int H, int Hkv,
-                           float scale, float p_drop, uint64_t seed) {
+                           const float* __restrict__ delta, bf16* __restrict__ dqkv, float* __restrict__ part, int T,
+                           int H, int Hkv, float scale, float p_drop, uint64_t seed) {
   constexpr int NP = D / 64, NS = D / 16, ND = D / 32;
   constexpr int BK = 64, QS = 32;
   constexpr int TILE = QS * 128 * NP;          // one 32-row slice of Q (or dO)
@@ -252,10 +256,12 @@ __global__ void __launch_bounds__(128, 1)
   constexpr bool KVLDS = D >= 256;
   constexpr int KVT = BK * 128 * NP;           // 64 key rows
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + (KVLDS ? 2 * KVT : 16)];
-  int kb, bh;
-  xcd_head_block(kb, bh);  // key block kb ascending = heaviest first (causal)
-  const int b = bh / Hkv, hk = bh % Hkv;
+  int kb, bhx;
+  xcd_head_block(kb, bhx);  // key block kb ascending = heaviest first (causal)
   const int G = H / Hkv;
+  const int GS = part != nullptr ? G : 1;  // workgroups per KV group (query-head split)
+  const int gi = bhx % GS, bh = bhx / GS;
+  const int b = bh / Hkv, hk = bh % Hkv;
   const int lane = threadIdx.x & 63, w = wave_id(), hh = lane >> 5;
   const size_t RS = (size_t)(H + 2 * Hkv) * D;
   const size_t ORS = (size_t)H * D;
@@ -301,10 +307,11 @@ __global__ void __launch_bounds__(128, 1)
   const int s_first = (kb * BK) / QS;
   const int nslices = (T + QS - 1) / QS;
   const int per_head = nslices - s_first;
-  const int total = G * per_head;
+  const int total = (GS == 1 ? G : 1) * per_head;
+  auto head_of = [&](int it) { return hk * G + (GS == 1 ? it / per_head : gi); };
 
   auto dma = [&](int it) {  // wave 0: Q slice + LSE rows, wave 1: dO slice + δ rows
-    const int hq = hk * G + it / per_head;
+    const int hq = head_of(it);
     const int qs0 = (s_first + it % per_head) * QS;
     const unsigned st = __builtin_amdgcn_readfirstlane(lds_addr_of(smem + (it & 1) * STAGE));
     if (w == 0)
@@ -325,7 +332,7 @@ __global__ void __launch_bounds__(128, 1)
     const char* Dt = stg + TILE;
     const float* lse_s = reinterpret_cast<const float*>(stg + 2 * TILE);
     const float* del_s = lse_s + 64;
-    const int hq = hk * G + it / per_head;
+    const int hq = head_of(it);
     const int qs0 = (s_first + it % per_head) * QS;
     if (qs0 + QS - 1 >= kw0 && kw0 < T && qs0 < T) {
       f32x16 sp, dp;
@@ -387,7 +394,20 @@ __global__ void __launch_bounds__(128, 1)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
-  if (key < T) {
+  if (key < T && part != nullptr) {  // fp32 partials of this query head: [gi][b·T + key][K | V][hk·D + d]
+    const int Bn = gridDim.y / (Hkv * GS);
+    float* prow = part + ((size_t)gi * Bn * T + (size_t)b * T + key) * (2 * Hkv * D) + (size_t)hk * D;
+#pragma unroll
+    for (int dh = 0; dh < ND; ++dh)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = 32 * dh + 8 * g + 4 * hh;
+        *reinterpret_cast<float4*>(prow + d) = float4{dk[dh][4 * g] * scale, dk[dh][4 * g + 1] * scale,
+                                                      dk[dh][4 * g + 2] * scale, dk[dh][4 * g + 3] * scale};
+        *reinterpret_cast<float4*>(prow + (size_t)Hkv * D + d) =
+            float4{dv[dh][4 * g], dv[dh][4 * g + 1], dv[dh][4 * g + 2], dv[dh][4 * g + 3]};
+      }
+  } else if (key < T) {
     bf16* dkrow = dqkv + ((size_t)b * T + key) * RS + (size_t)(H + hk) * D;
     bf16* dvrow = dqkv + ((size_t)b * T + key) * RS + (size_t)(H + Hkv + hk) * D;
 #pragma unroll
@@ -399,6 +419,25 @@ __global__ void __launch_bounds__(128, 1)
                dk[dh][4 * g + 3] * scale);
         store4(dvrow + d, dv[dh][4 * g], dv[dh][4 * g + 1], dv[dh][4 * g + 2], dv[dh][4 * g + 3]);
       }
+  }
+}
+
+// Σ over the G query-head partials -> the K | V columns of dqkv (bf16). One thread per 8 columns.
+__global__ void __launch_bounds__(256) fa_gen_kv_reduce(const float* __restrict__ part, bf16* __restrict__ dqkv,
+                                                        int64_t rows, int W2, int G, int64_t RS, int64_t col0) {
+  const int64_t n8 = rows * (W2 / 8);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / (W2 / 8), c = 8 * (i - r * (W2 / 8));
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int g = 0; g < G; ++g) {
+      const float* src = part + ((size_t)g * rows + r) * W2 + c;
+      const float4 a = *reinterpret_cast<const float4*>(src), bq = *reinterpret_cast<const float4*>(src + 4);
+      acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+      acc[4] += bq.x; acc[5] += bq.y; acc[6] += bq.z; acc[7] += bq.w;
+    }
+    bf16* dst = dqkv + r * RS + col0 + c;
+    store4(dst, acc[0], acc[1], acc[2], acc[3]);
+    store4(dst + 4, acc[4], acc[5], acc[6], acc[7]);
   }
 }
 
@@ -573,14 +612,26 @@ void flash_attn_gen_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out
   const bf16* q = reinterpret_cast<const bf16*>(qkv.data_ptr());
   const bf16* d = reinterpret_cast<const bf16*>(dout.data_ptr());
   bf16* g = reinterpret_cast<bf16*>(dqkv.data_ptr());
-  dim3 gkv((T + 63) / 64, B * Hkv), gq((T + 63) / 64, B * H);
+  // GQA with few KV workgroups: split the dK / dV sweep over the query heads of each group
+  // (fp32 partials + one reduction pass) so the grid covers the chip
+  const int G = (int)(H / Hkv), nkb = (T + 63) / 64;
+  const bool split = G > 1 && (int64_t)B * Hkv * nkb < 1024;
+  torch::Tensor part;
+  if (split) part = torch::empty({(int64_t)G * B * T, 2 * Hkv * D}, qkv.options().dtype(torch::kFloat32));
+  dim3 gkv(nkb, B * Hkv * (split ? G : 1)), gq((T + 63) / 64, B * H);
   FA_GEN_DISPATCH(D, p_drop > 0.0, {
     hipLaunchKernelGGL((fa_gen_bwd_pre_kernel<DD>), dim3(((int64_t)rows * (DD / 8) + 255) / 256), dim3(256), 0,
                        stream, d, reinterpret_cast<const bf16*>(out.data_ptr()), delta.data_ptr<float>(), B, T,
                        (int)H);
     hipLaunchKernelGGL((fa_gen_bwd_dkdv_kernel<DD, DR>), gkv, dim3(128), 0, stream, q, d, lse.data_ptr<float>(),
-                       delta.data_ptr<float>(), g, T, (int)H, (int)Hkv, (float)scale, (float)p_drop,
-                       (uint64_t)seed);
+                       delta.data_ptr<float>(), g, split ? part.data_ptr<float>() : nullptr, T, (int)H, (int)Hkv,
+                       (float)scale, (float)p_drop, (uint64_t)seed);
+    if (split) {
+      const int64_t n8 = (int64_t)B * T * (2 * Hkv * DD / 8);
+      hipLaunchKernelGGL(fa_gen_kv_reduce, dim3((unsigned)std::min<int64_t>((n8 + 255) / 256, 4096)), dim3(256), 0,
+                         stream, part.data_ptr<float>(), g, (int64_t)B * T, (int)(2 * Hkv * DD), G,
+                         (int64_t)(H + 2 * Hkv) * DD, (int64_t)H * DD);
+    }
     hipLaunchKernelGGL((fa_gen_bwd_dq_kernel<DD, DR>), gq, dim3(128), 0, stream, q, d, lse.data_ptr<float>(),
                        delta.data_ptr<float>(), g, T, (int)H, (int)Hkv, (float)scale, (float)p_drop, (uint64_t)seed);
   })

@@ -6,7 +6,8 @@ group), so reference checkpoints load and ours load in the reference.  On GPU:
     (set up by :meth:`FusedAdamW.attach_flat`, used by the fused GPT executor), the step is a
     single grid-stride kernel over (param, grad, m, v) that also rewrites the bf16 shadow
     weights the GEMMs read (``csrc/kernels/adamw.hip``);
-  * *list mode* — otherwise a multi-tensor kernel walks a chunk table of the group's tensors.
+  * *list mode* — otherwise a multi-tensor kernel walks a chunk table of the group's tensors
+    (fp32, or bf16 parameters with bf16 state as torch keeps it, updated in fp32 registers).
 On CPU (or amsgrad / differentiable / capturable options) the stock torch step runs.
 Replaces the reference's ``torch.optim.AdamW`` foreach step (``mappers.py:53-57``,
 ``neural_net_model.py:677``).
@@ -72,7 +73,8 @@ class _FusedMixin:
         if group.get("amsgrad") or group.get("differentiable") or group.get("capturable"):
             return False
         ps = [p for p in group["params"] if p.grad is not None]
-        return bool(ps) and all(p.is_cuda and p.dtype == torch.float32 for p in ps) and _ext.available()
+        return bool(ps) and all(p.is_cuda and p.dtype in (torch.float32, torch.bfloat16) and p.grad.dtype == p.dtype
+                                for p in ps) and _ext.available()
 
     @torch.no_grad()
     def step(self, closure=None, grad_scale: float = 1.0):
@@ -151,9 +153,9 @@ class _FusedMixin:
                 st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
             st["step"] += 1
-            by_step.setdefault(int(st["step"].item()), []).append(p)
+            by_step.setdefault((int(st["step"].item()), p.dtype), []).append(p)
         k = _ext.kernels()
-        for step, ps in by_step.items():
+        for (step, _), ps in by_step.items():
             k.multi_tensor_adam([p.data for p in ps], [p.grad for p in ps],
                                 [self.state[p]["exp_avg"] for p in ps], [self.state[p]["exp_avg_sq"] for p in ps],
                                 lr, b1, b2, eps, wd, step, float(grad_scale), maximize, self._decoupled)

@@ -139,7 +139,9 @@ class _RMSNormFn(torch.autograd.Function):
 
 
 def rms_norm(x: Tensor, w: Tensor, eps: float) -> Tensor:
-    """``(x_f32 * rsqrt(mean(x²) + eps)).to(x.dtype) * w`` — reference semantics."""
-    if use_kernels(x) and x.shape[-1] % 4 == 0 and not torch.is_autocast_enabled("cuda"):
+    """``(x_f32 * rsqrt(mean(x²) + eps)).to(x.dtype) * w`` — reference semantics. Autocast does not
+    change that expression (the statistics are fp32 already; the product follows type promotion),
+    so the HIP kernel (fp32 statistics, output dtype = promote(x, w)) serves both modes."""
+    if use_kernels(x) and x.shape[-1] % 4 == 0:
         return _RMSNormFn.apply(x, w, eps)
     return reference_rms_norm(x, w, eps)

@@ -208,6 +208,33 @@ def test_fused_optimizer_list_mode():
         assert set(o1.state_dict()["state"][0].keys()) == set(o2.state_dict()["state"][0].keys())
 
 
+def test_fused_optimizer_list_mode_bf16_params():
+    """bf16 parameters (HF / Gemma imports on the generic engine): bf16 state like torch keeps, the
+    update done in fp32 and rounded once — within bf16 rounding of an fp32 AdamW on the same
+    values, and closer to it than torch's own bf16 foreach step."""
+    from penroz.models.optim import FusedAdamW
+    torch.manual_seed(0)
+    shapes = ((33, 17), (5,), (70000,))
+    ps = [torch.randn(s, device=DEV).to(torch.bfloat16).requires_grad_() for s in shapes]
+    f32 = [p.detach().float().clone().requires_grad_() for p in ps]
+    tb = [p.detach().clone().requires_grad_() for p in ps]
+    o1 = FusedAdamW(ps, lr=3e-3, weight_decay=0.05)
+    o2 = torch.optim.AdamW(f32, lr=3e-3, weight_decay=0.05)
+    o3 = torch.optim.AdamW(tb, lr=3e-3, weight_decay=0.05)
+    for _ in range(3):
+        for p, r, t in zip(ps, f32, tb):
+            g = torch.randn(p.shape, device=DEV).to(torch.bfloat16)
+            p.grad, r.grad, t.grad = g.clone(), g.float(), g.clone()
+        o1.step()
+        o2.step()
+        o3.step()
+    for p, r, t in zip(ps, f32, tb):
+        assert p.dtype == torch.bfloat16 and o1.state[p]["exp_avg"].dtype == torch.bfloat16
+        err = (p.float() - r).abs().max().item()
+        assert err <= 0.02 * r.abs().max().item() + 1e-2, err
+        assert err <= (t.float() - r).abs().max().item() + 1e-2
+
+
 def _qkv(B, T, H, Hkv, D=64, scale=1.0):
     return (torch.randn(B, T, (H + 2 * Hkv) * D, device=DEV) * scale).to(torch.bfloat16)
 
@@ -500,11 +527,16 @@ def test_sampling_wide_rows(dt, V):
     assert torch.allclose(freq, probs, atol=0.03), (freq, probs)
 
 
-@pytest.mark.parametrize("xdt,wdt", [(torch.float32, torch.float32), (torch.bfloat16, torch.bfloat16)])
-def test_rmsnorm(xdt, wdt):
+@pytest.mark.parametrize("autocast", [False, True])
+@pytest.mark.parametrize("xdt,wdt", [(torch.float32, torch.float32), (torch.bfloat16, torch.bfloat16),
+                                     (torch.float32, torch.bfloat16)])
+def test_rmsnorm(xdt, wdt, autocast):
+    """HIP RMSNorm (also under bf16 autocast, as the generic engine runs it) vs the reference expression."""
     x = torch.randn(100, 640, device=DEV).to(xdt)
     w = torch.randn(640, device=DEV).to(wdt)
-    y = Nm.rms_norm(x, w, 1e-6)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+        y = Nm.rms_norm(x, w, 1e-6)
+    assert y.dtype == torch.promote_types(xdt, wdt)
     _close(y, Nm.reference_rms_norm(x, w, 1e-6), 0.03, 0.01)
     xr, wr = x.detach().float().clone().requires_grad_(), w.detach().float().clone().requires_grad_()
     dy = torch.randn(100, 640, device=DEV)

@@ -59,6 +59,18 @@ def test_bench_cli_help():
         assert flag in r.stdout
 
 
+def test_bench_gemma_config_uses_generic_engine_and_gemma_layers():
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    args = bench.parse_args(["--model", "gemma3-1b"])
+    assert args.engine == "generic" and args.batch == 64 and args.seq == 1024
+    assert bench.parse_args([]).engine == "fused"
+    layers = bench.gemma3_1b_layers(2)
+    names = [next(iter(l)) for l in layers]
+    assert names.count("transformerblock") == 2 or "rmsnorm" in names, names
+
+
 def _run_bench(args, env_extra=None, timeout=300):
     import subprocess
     import sys
