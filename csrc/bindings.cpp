@@ -32,7 +32,8 @@ torch::Tensor rope_qkv(torch::Tensor qkv, torch::Tensor cosv, torch::Tensor sinv
 void kv_quantize(torch::Tensor x, torch::Tensor q, torch::Tensor scale, int64_t pos);
 std::vector<torch::Tensor> tensor_stats(torch::Tensor x, int64_t bins);
 // cross_entropy.hip
-torch::Tensor cross_entropy_fwd_bwd(torch::Tensor logits, torch::Tensor targets, double scale, int64_t ignore_index);
+torch::Tensor cross_entropy_fwd_bwd(torch::Tensor logits, torch::Tensor targets, double scale, int64_t ignore_index,
+                                    c10::optional<torch::Tensor> grad_out);
 // adamw.hip
 void adamw_step(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, c10::optional<torch::Tensor> shadow,
                 double lr, double b1, double b2, double eps, double wd, int64_t step, double grad_scale, bool maximize);
@@ -113,7 +114,8 @@ PYBIND11_MODULE(penroz_kernels, m) {
   m.def("rope_qkv", &rope_qkv);
   m.def("kv_quantize", &kv_quantize);
   m.def("tensor_stats", &tensor_stats);
-  m.def("cross_entropy_fwd_bwd", &cross_entropy_fwd_bwd);
+  m.def("cross_entropy_fwd_bwd", &cross_entropy_fwd_bwd, pybind11::arg("logits"), pybind11::arg("targets"),
+        pybind11::arg("scale"), pybind11::arg("ignore_index"), pybind11::arg("grad_out") = pybind11::none());
   m.def("adamw_step", &adamw_step);
   m.def("adam_step", &adam_step);
   m.def("multi_tensor_adam", &multi_tensor_adam);

@@ -34,10 +34,11 @@ __device__ __forceinline__ float block_reduce(float v, float* sh, bool is_max) {
 template <int CPT, typename T>
 __global__ void __launch_bounds__(kCEThreads) ce_kernel(T* __restrict__ logits, const int64_t* __restrict__ targets,
                                                         float* __restrict__ loss, int V, int ld, float scale,
-                                                        int64_t ignore_index) {
+                                                        int64_t ignore_index, T* __restrict__ gout) {
   __shared__ float sh[16];
   const int row = blockIdx.x;
   T* rp = logits + (size_t)row * ld;
+  T* gp = gout ? gout + (size_t)row * ld : rp;  // gradient destination (in place by default)
   const int64_t tgt = targets[row];
   PZ_DEVICE_CHECK(tgt == ignore_index || (tgt >= 0 && tgt < V));
   const int t = threadIdx.x;
@@ -86,7 +87,7 @@ __global__ void __launch_bounds__(kCEThreads) ce_kernel(T* __restrict__ logits, 
       float g[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) g[j] = fmaf(v[k][j], ps, c + j == tgt ? -sc : 0.f);
-      Vec8<T>::store(rp + c, g);
+      Vec8<T>::store(gp + c, g);
     }
   }
 }
@@ -96,10 +97,11 @@ template <typename T>
 __global__ void __launch_bounds__(kCEThreads) ce_loop_kernel(T* __restrict__ logits,
                                                              const int64_t* __restrict__ targets,
                                                              float* __restrict__ loss, int V, int ld, float scale,
-                                                             int64_t ignore_index) {
+                                                             int64_t ignore_index, T* __restrict__ gout) {
   __shared__ float sh[16];
   const int row = blockIdx.x;
   T* rp = logits + (size_t)row * ld;
+  T* gp = gout ? gout + (size_t)row * ld : rp;
   const int64_t tgt = targets[row];
   PZ_DEVICE_CHECK(tgt == ignore_index || (tgt >= 0 && tgt < V));
   float m = -INFINITY;
@@ -129,7 +131,7 @@ __global__ void __launch_bounds__(kCEThreads) ce_loop_kernel(T* __restrict__ log
     Vec8<T>::load(rp + c, v);
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = c + j < V ? (__expf(v[j] - lse) - (c + j == tgt ? 1.f : 0.f)) * sc : 0.f;
-    Vec8<T>::store(rp + c, v);
+    Vec8<T>::store(gp + c, v);
   }
 }
 
@@ -137,7 +139,10 @@ __global__ void __launch_bounds__(kCEThreads) ce_loop_kernel(T* __restrict__ log
 
 using namespace penroz;
 
-torch::Tensor cross_entropy_fwd_bwd(torch::Tensor logits, torch::Tensor targets, double scale, int64_t ignore_index) {
+// grad_out (optional, same shape / row stride / dtype as logits): the gradient goes there and the
+// logits stay intact (autograd callers); default: in place over the logits.
+torch::Tensor cross_entropy_fwd_bwd(torch::Tensor logits, torch::Tensor targets, double scale, int64_t ignore_index,
+                                    c10::optional<torch::Tensor> grad_out) {
   TORCH_CHECK(logits.is_cuda() && logits.dim() == 2 && logits.stride(1) == 1, "logits: [N, V] with unit column stride");
   TORCH_CHECK(targets.scalar_type() == torch::kInt64 && targets.numel() == logits.size(0));
   const int N = logits.size(0), V = logits.size(1);
@@ -151,6 +156,14 @@ torch::Tensor cross_entropy_fwd_bwd(torch::Tensor logits, torch::Tensor targets,
   auto loss = torch::empty({N}, logits.options().dtype(torch::kFloat32));
   if (N == 0) return loss;
   auto tg = targets.contiguous();
+  void* gptr = nullptr;
+  if (grad_out.has_value() && grad_out->defined()) {
+    TORCH_CHECK(grad_out->is_cuda() && grad_out->scalar_type() == logits.scalar_type() &&
+                    grad_out->sizes() == logits.sizes() && grad_out->strides() == logits.strides() &&
+                    reinterpret_cast<uintptr_t>(grad_out->data_ptr()) % 16 == 0,
+                "grad_out must match the logits' shape, strides and dtype (16-B aligned)");
+    gptr = grad_out->data_ptr();
+  }
   auto stream = at::hip::getCurrentHIPStream();
   const int chunks = ((V + 7) / 8 + kCEThreads - 1) / kCEThreads;
   auto launch = [&](auto tag) {
@@ -159,16 +172,17 @@ torch::Tensor cross_entropy_fwd_bwd(torch::Tensor logits, torch::Tensor targets,
     const int64_t* tp = tg.data_ptr<int64_t>();
     float* op = loss.data_ptr<float>();
     const float sc = (float)scale;
+    T* gp = reinterpret_cast<T*>(gptr);
     switch (chunks) {
-      case 1: hipLaunchKernelGGL((ce_kernel<1, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index); break;
-      case 2: hipLaunchKernelGGL((ce_kernel<2, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index); break;
-      case 3: hipLaunchKernelGGL((ce_kernel<3, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index); break;
-      case 4: hipLaunchKernelGGL((ce_kernel<4, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index); break;
-      case 5: hipLaunchKernelGGL((ce_kernel<5, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index); break;
-      case 6: hipLaunchKernelGGL((ce_kernel<6, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index); break;
-      case 7: hipLaunchKernelGGL((ce_kernel<7, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index); break;
-      case 8: hipLaunchKernelGGL((ce_kernel<8, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index); break;
-      default: hipLaunchKernelGGL((ce_loop_kernel<T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index);
+      case 1: hipLaunchKernelGGL((ce_kernel<1, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index, gp); break;
+      case 2: hipLaunchKernelGGL((ce_kernel<2, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index, gp); break;
+      case 3: hipLaunchKernelGGL((ce_kernel<3, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index, gp); break;
+      case 4: hipLaunchKernelGGL((ce_kernel<4, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index, gp); break;
+      case 5: hipLaunchKernelGGL((ce_kernel<5, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index, gp); break;
+      case 6: hipLaunchKernelGGL((ce_kernel<6, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index, gp); break;
+      case 7: hipLaunchKernelGGL((ce_kernel<7, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index, gp); break;
+      case 8: hipLaunchKernelGGL((ce_kernel<8, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index, gp); break;
+      default: hipLaunchKernelGGL((ce_loop_kernel<T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index, gp);
     }
   };
   if (logits.scalar_type() == torch::kBFloat16) launch(bf16{});

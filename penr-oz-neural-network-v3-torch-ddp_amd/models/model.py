@@ -42,6 +42,7 @@ from penroz.models.kv_cache import KVCache, create_kv_cache
 from penroz.models.layers import CausalSelfAttention, PositionEmbedding, SoftmaxOnLast
 from penroz.models.mapper import Mapper
 from penroz.ops import sampling as samp_ops
+from penroz.ops import fused as fused_ops
 from penroz.parallel import dist as ddp
 from penroz.parallel.launcher import maybe_inject_fault
 from penroz.utils import checkpoint as ckpt
@@ -245,7 +246,7 @@ class NeuralNetworkModel(nn.Module):
             if logits.ndim > 2 and target.ndim > 1:
                 logits = logits.reshape(-1, logits.size(-1))
                 target = target.reshape(-1)
-            cost = nn.functional.cross_entropy(logits, target)
+            cost = fused_ops.cross_entropy(logits, target)  # F.cross_entropy semantics; fused HIP on GPU bf16
         else:
             cost = nn.functional.mse_loss(x, target)
         return activations, cost

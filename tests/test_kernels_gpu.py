@@ -106,6 +106,27 @@ def test_gelu(approx):
     _close(dbias, out.float().sum(0), 0.05, 1e-3)
 
 
+@pytest.mark.parametrize("N,V", [(64, 50304), (37, 262144), (5, 1000)])
+def test_fused_cross_entropy_autograd_matches_torch(N, V):
+    """fused_ops.cross_entropy (bf16 logits, separate gradient buffer, device-side mean over the
+    non-ignored rows) == F.cross_entropy on the fp32 logits; the logits are left intact."""
+    torch.manual_seed(0)
+    logits = (torch.randn(N, V, device=DEV) * 3).to(torch.bfloat16).requires_grad_()
+    tg = torch.randint(0, V, (N,), device=DEV)
+    tg[1] = -100  # ignored row
+    keep = logits.detach().clone()
+    loss = Fu.cross_entropy(logits, tg)
+    (loss * 0.5).backward()
+    assert torch.equal(logits.detach(), keep)
+    ref = logits.detach().float().requires_grad_()
+    rl = F.cross_entropy(ref, tg)
+    (rl * 0.5).backward()
+    assert abs(loss.item() - rl.item()) < 2e-3 * max(1.0, abs(rl.item()))
+    rel = ((logits.grad.float() - ref.grad).norm() / ref.grad.norm()).item()
+    assert rel < 0.01, rel
+    assert logits.grad[1].abs().max().item() == 0.0
+
+
 def test_colsum():
     x = torch.randn(4099, 2304, device=DEV).to(torch.bfloat16)
     out = torch.full((2304,), 2.0, device=DEV)
