@@ -1,0 +1,7 @@
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace -d gpurun_out/prof_gemma2 -o run -- python3 bench.py --model gemma3-1b --batch 8 --steps 3 --warmup 1 --ref-steps 0 > gpurun_out/prof_gemma_bench.log 2>&1 || { tail -20 gpurun_out/prof_gemma_bench.log; exit 1; }
+DB=$(find gpurun_out/prof_gemma2 -name 'run_results.db' | head -n1)
+python3 bench/prof_summary.py $DB --steps 4 > gpurun_out/prof_gemma_summary.txt
+head -n 30 gpurun_out/prof_gemma_summary.txt | cut -c1-140

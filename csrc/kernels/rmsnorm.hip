@@ -3,6 +3,7 @@
 // dtype = promote(x, w). One wave per row (any width % 4), 4 rows per workgroup; dγ partials
 // accumulate per workgroup in LDS and are finished by a column reduction (no global atomics).
 #include "common.h"
+#include "deferred.h"
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 
@@ -58,14 +59,6 @@ __global__ void __launch_bounds__(256) rms_bwd_kernel(const TDY* __restrict__ dy
   for (int c = threadIdx.x; c < C; c += blockDim.x) part[(size_t)blockIdx.x * C + c] = dwl[c];
 }
 
-__global__ void __launch_bounds__(256) rms_finish_kernel(const float* __restrict__ part, int G, int C,
-                                                         float* __restrict__ out) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
-  float s = 0.f;
-  for (int g = 0; g < G; ++g) s += part[(size_t)g * C + c];
-  out[c] = s;
-}
 
 
 // Decode-step fusion for Gemma blocks: residual add + post-norm + the next norm in one pass.
@@ -177,17 +170,20 @@ std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor dy, torch::Tensor x, torch:
   auto dx = torch::empty_like(x);
   const int G = std::max(1, std::min((N + 3) / 4, 512));
   auto part = torch::empty({G, C}, x.options().dtype(torch::kFloat32));
-  auto dw = torch::empty({C}, x.options().dtype(torch::kFloat32));
+  auto dw = torch::zeros({C}, x.options().dtype(torch::kFloat32));
   auto wc = w.contiguous();
   auto stream = at::hip::getCurrentHIPStream();
-  if (N == 0) return {dx, dw.zero_()};
+  if (N == 0) return {dx, dw};
   RMS_TYPES(x.scalar_type(), TX, RMS_TYPES(w.scalar_type(), TW, RMS_TYPES(dy.scalar_type(), TDY,
     hipLaunchKernelGGL((rms_bwd_kernel<TX, TW, TDY>), dim3(G), dim3(256), C * sizeof(float), stream,
                        reinterpret_cast<const TDY*>(dy.data_ptr()), reinterpret_cast<const TX*>(x.data_ptr()),
                        reinterpret_cast<const TW*>(wc.data_ptr()), rstd.data_ptr<float>(),
                        reinterpret_cast<TX*>(dx.data_ptr()), part.data_ptr<float>(), N, C))))
-  hipLaunchKernelGGL(rms_finish_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, part.data_ptr<float>(), G, C,
-                     dw.data_ptr<float>());
+  // dγ = Σ of the G partial rows: the sliced two-stage column reduction (reduce.h). A single
+  // 256-thread block walking all G rows per column (the former finish kernel) was latency-bound:
+  // 120 µs per call at Gemma's head_dim-256 q/k norms (G = 512)
+  float* outs[1] = {dw.data_ptr<float>()};
+  reduce_partials_auto(part, 1, G, C, outs, stream);
   return {dx, dw};
 }
 
