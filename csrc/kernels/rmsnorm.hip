@@ -4,6 +4,7 @@
 // accumulate per workgroup in LDS and are finished by a column reduction (no global atomics).
 #include "common.h"
 #include "deferred.h"
+#include <type_traits>
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 
@@ -30,33 +31,53 @@ __global__ void __launch_bounds__(256) rms_fwd_kernel(const TX* __restrict__ x, 
   if (lane == 0) rstd_out[row] = r;
 }
 
-template <typename TX, typename TW, typename TDY>
+// One wave per row; lane l owns columns l + 64·k (k < NPL), so each row's x / dy stay in registers
+// between the two passes and the dγ partial sums accumulate in registers across the wave's rows
+// (no LDS atomics); the 4 waves' partials are combined through LDS into one row of `part`.
+template <int NPL, typename TX, typename TW, typename TDY>
 __global__ void __launch_bounds__(256) rms_bwd_kernel(const TDY* __restrict__ dy, const TX* __restrict__ x,
                                                       const TW* __restrict__ w, const float* __restrict__ rstd,
                                                       TX* __restrict__ dx, float* __restrict__ part, int N, int C) {
-  extern __shared__ __attribute__((aligned(16))) float dwl[];
-  for (int c = threadIdx.x; c < C; c += blockDim.x) dwl[c] = 0.f;
-  __syncthreads();
+  extern __shared__ __attribute__((aligned(16))) float dwl[];  // [4 waves][C]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float wv[NPL], dwa[NPL];
+#pragma unroll
+  for (int k = 0; k < NPL; ++k) {
+    const int c = lane + 64 * k;
+    wv[k] = c < C ? to_f(w[c]) : 0.f;
+    dwa[k] = 0.f;
+  }
   for (int row = blockIdx.x * 4 + wid; row < N; row += gridDim.x * 4) {
     const size_t base = (size_t)row * C;
     const float r = rstd[row];
+    float xv[NPL], gv[NPL];
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      const int c = lane + 64 * k;
+      xv[k] = c < C ? to_f(x[base + c]) : 0.f;
+      gv[k] = c < C ? to_f(dy[base + c]) : 0.f;
+    }
     float dot = 0.f;
-    for (int c = lane; c < C; c += 64) {
-      const float xv = to_f(x[base + c]);
-      const float g = to_f(dy[base + c]);
-      dot += g * to_f(w[c]) * xv;
-      atomicAdd(&dwl[c], g * to_f(from_f<TX>(xv * r)));
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      dot += gv[k] * wv[k] * xv[k];
+      dwa[k] += gv[k] * to_f(from_f<TX>(xv[k] * r));
     }
     dot = wave_sum(dot) / C;
-    for (int c = lane; c < C; c += 64) {
-      const float xv = to_f(x[base + c]);
-      const float g = to_f(dy[base + c]) * to_f(w[c]);
-      dx[base + c] = from_f<TX>(r * g - xv * r * r * r * dot);
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      const int c = lane + 64 * k;
+      if (c < C) dx[base + c] = from_f<TX>(r * gv[k] * wv[k] - xv[k] * r * r * r * dot);
     }
   }
+#pragma unroll
+  for (int k = 0; k < NPL; ++k) {
+    const int c = lane + 64 * k;
+    if (c < C) dwl[wid * C + c] = dwa[k];
+  }
   __syncthreads();
-  for (int c = threadIdx.x; c < C; c += blockDim.x) part[(size_t)blockIdx.x * C + c] = dwl[c];
+  for (int c = threadIdx.x; c < C; c += blockDim.x)
+    part[(size_t)blockIdx.x * C + c] = dwl[c] + dwl[C + c] + dwl[2 * C + c] + dwl[3 * C + c];
 }
 
 
@@ -166,19 +187,27 @@ std::vector<torch::Tensor> rmsnorm_fwd(torch::Tensor x, torch::Tensor w, double 
 std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor w, torch::Tensor rstd) {
   TORCH_CHECK(x.is_cuda() && x.is_contiguous() && dy.is_contiguous() && dy.numel() == x.numel());
   const int N = x.size(0), C = x.size(1);
-  TORCH_CHECK((size_t)C * 4 <= 160 * 1024, "RMSNorm width too large for the LDS dγ accumulator");
+  TORCH_CHECK(C <= 64 * 32, "RMSNorm backward: width <= 2048");
   auto dx = torch::empty_like(x);
-  const int G = std::max(1, std::min((N + 3) / 4, 512));
+  const int G = std::max(1, std::min((N + 3) / 4, 2048));
   auto part = torch::empty({G, C}, x.options().dtype(torch::kFloat32));
   auto dw = torch::zeros({C}, x.options().dtype(torch::kFloat32));
   auto wc = w.contiguous();
   auto stream = at::hip::getCurrentHIPStream();
   if (N == 0) return {dx, dw};
-  RMS_TYPES(x.scalar_type(), TX, RMS_TYPES(w.scalar_type(), TW, RMS_TYPES(dy.scalar_type(), TDY,
-    hipLaunchKernelGGL((rms_bwd_kernel<TX, TW, TDY>), dim3(G), dim3(256), C * sizeof(float), stream,
-                       reinterpret_cast<const TDY*>(dy.data_ptr()), reinterpret_cast<const TX*>(x.data_ptr()),
-                       reinterpret_cast<const TW*>(wc.data_ptr()), rstd.data_ptr<float>(),
-                       reinterpret_cast<TX*>(dx.data_ptr()), part.data_ptr<float>(), N, C))))
+  auto launch = [&](auto npl) {
+    constexpr int NPL = decltype(npl)::value;
+    RMS_TYPES(x.scalar_type(), TX, RMS_TYPES(w.scalar_type(), TW, RMS_TYPES(dy.scalar_type(), TDY,
+      hipLaunchKernelGGL((rms_bwd_kernel<NPL, TX, TW, TDY>), dim3(G), dim3(256), 4 * C * sizeof(float), stream,
+                         reinterpret_cast<const TDY*>(dy.data_ptr()), reinterpret_cast<const TX*>(x.data_ptr()),
+                         reinterpret_cast<const TW*>(wc.data_ptr()), rstd.data_ptr<float>(),
+                         reinterpret_cast<TX*>(dx.data_ptr()), part.data_ptr<float>(), N, C))))
+  };
+  const int npl = (C + 63) / 64;
+  if (npl <= 4) launch(std::integral_constant<int, 4>{});
+  else if (npl <= 8) launch(std::integral_constant<int, 8>{});
+  else if (npl <= 18) launch(std::integral_constant<int, 18>{});
+  else launch(std::integral_constant<int, 32>{});
   // dγ = Σ of the G partial rows: the sliced two-stage column reduction (reduce.h). A single
   // 256-thread block walking all G rows per column (the former finish kernel) was latency-bound:
   // 120 µs per call at Gemma's head_dim-256 q/k norms (G = 512)
