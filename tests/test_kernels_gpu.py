@@ -568,9 +568,18 @@ def test_rmsnorm(xdt, wdt, autocast):
     _close(wg.grad, wr.grad, 0.5, 0.02)
 
 
-def test_rope():
-    H, Hkv, D = 4, 2, 64
-    qkv = torch.randn(2, 33, (H + 2 * Hkv) * D, device=DEV)
+@pytest.mark.parametrize("H,Hkv,D,dt", [(4, 2, 64, torch.float32), (4, 1, 256, torch.bfloat16),
+                                         (3, 3, 24, torch.float32), (2, 1, 128, torch.bfloat16)])
+def test_rope(H, Hkv, D, dt):
+    """Vectorised (D % 16 == 0) and scalar RoPE kernels vs the torch reference, fwd + bwd."""
+    qkv = torch.randn(2, 33, (H + 2 * Hkv) * D, device=DEV).to(dt).float() if dt == torch.float32 else \
+        torch.randn(2, 33, (H + 2 * Hkv) * D, device=DEV).to(dt)
+    if dt == torch.bfloat16:
+        inv = 1.0 / (10000 ** (torch.arange(0, D, 2, device=DEV).float() / D))
+        out = Ro.apply_rope_qkv(qkv, H, Hkv, D, inv, 7)
+        ref = Ro.reference_apply_rope_qkv(qkv.float(), H, Hkv, D, inv, 7)
+        _close(out, ref, 0.02, 0.01)
+        return
     inv = 1.0 / (10000 ** (torch.arange(0, D, 2, device=DEV).float() / D))
     out = Ro.apply_rope_qkv(qkv, H, Hkv, D, inv, 7)
     ref = Ro.reference_apply_rope_qkv(qkv, H, Hkv, D, inv, 7)
