@@ -26,9 +26,17 @@ Extra fields (outside the timed region):
     steps with the gradient all-reduce switched off (the part of the collective NOT hidden
     behind the backward), and ``probe_busbw_GBps`` = ring bus bandwidth of bare all-reduces of
     one default-size bucket (RCCL over xGMI at N > 1; compare 7 links × ≈153 GB/s);
+  * ``comm`` at N > 1 also holds the first-contact record made before the model is built
+    (``penroz.parallel.commtune``): ``devices`` (every rank's PCI id; duplicate devices abort
+    the run), ``sweep`` (bare all-reduce ms / busbw over bucket sizes 16-256 MB x fp32/bf16 wire x
+    c10d/native transport, each result checked for the exact average), ``choice`` (the transport
+    the gradient reducer then uses, unless ``PENROZ_COMM`` is set) and ``rccl.coll_channels``
+    (parsed from RCCL's INIT log). The process group has an explicit timeout
+    (``PENROZ_DIST_TIMEOUT``, 300 s), so a stuck rank fails the run instead of hanging it;
   * ``vs_reference_eager_same_gpu``: the same config through the ``reference`` engine (stock
     PyTorch eager + autocast + foreach AdamW, the reference's semantics) measured in this same
-    process right after (1 GPU only; ``--ref-steps 0`` skips it).
+    process right after with the headline's own warmup / step counts (1 GPU only; ``--ref-steps
+    0`` skips it).
 ``--device cpu`` (gloo, generic engine, pair it with ``--model tiny``) is the plumbing rehearsal
 used by the CPU tests; the headline is always ``--device cuda``.
 """
@@ -118,14 +126,17 @@ def parse_args(argv=None):
                     help="default: fused on cuda, generic on cpu")
     ap.add_argument("--model", default="gpt2-124m", choices=list(MODELS))
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"])
-    ap.add_argument("--ref-steps", type=int, default=4,
+    ap.add_argument("--ref-steps", type=int, default=-1,
                     help="steps of the reference engine measured after the run for vs_reference_eager_same_gpu "
-                         "(1 GPU, gpt2-124m only; 0 = skip)")
+                         "(1 GPU, gpt2-124m only; default -1 = the headline's --steps after its --warmup; 0 = skip)")
     ap.add_argument("--comm-probe-iters", type=int, default=5,
                     help="world > 1: time this many bare all-reduces of one gradient bucket after the timed "
                          "run and report the bus bandwidth in comm (0 = skip)")
     ap.add_argument("--nocomm-steps", type=int, default=4,
                     help="steps without the gradient all-reduce, for allreduce_exposed_ms (world > 1; 0 = skip)")
+    ap.add_argument("--no-comm-sweep", dest="comm_sweep", action="store_false",
+                    help="world > 1: skip the first-contact all-reduce sweep (bucket size x wire x transport) "
+                         "that picks the gradient transport before the timed run")
     ap.add_argument("--via-runtime", action="store_true",
                     help="also time the same config through NeuralNetworkModel.train_model (Loader over synthetic "
                          "shards, per-epoch diagnostics, checkpoints) and report its tokensPerSec progress figure")
@@ -241,6 +252,33 @@ def _allreduce_probe(device, world: int, iters: int) -> dict:
             "probe_busbw_GBps": buf.numel() * 4 * 2 * (world - 1) / world / t / 1e9}
 
 
+def _first_contact(args, device, world: int, rccl_log) -> dict:
+    """World > 1, before the model is built (outside the timed region): every rank's device
+    identity (N distinct PCI devices, or fail), the all-reduce sweep over bucket size × wire dtype
+    × transport (``penroz.parallel.commtune``), the transport the reducer will use (unless
+    ``PENROZ_COMM`` was set) and the channel count RCCL picked."""
+    from penroz.parallel import commtune
+    from penroz.parallel.reducer import DEFAULT_BUCKET_MB
+    devices = commtune.gather_identities(device)
+    if device.type == "cuda" and "PENROZ_BENCH_DEVICE" not in os.environ:
+        pcis = [d.get("pci") for d in devices]
+        if len(set(pcis)) != len(pcis):
+            raise SystemExit(f"bench.py: ranks share devices {pcis}; refusing to report a {world}-GPU number")
+    out = {"devices": [d.get("pci", d.get("host")) for d in devices]}
+    if args.comm_sweep:
+        sizes = commtune.SWEEP_SIZES_MB if device.type == "cuda" else (1, 4)
+        rows = commtune.sweep(device, sizes_mb=sizes, iters=args.comm_probe_iters or 3)
+        out["sweep"] = rows
+        choice = commtune.choose(rows, DEFAULT_BUCKET_MB)
+        if "PENROZ_COMM" in os.environ:
+            choice = {"transport": os.environ["PENROZ_COMM"], "reason": "PENROZ_COMM set"}
+        else:
+            os.environ["PENROZ_COMM"] = choice["transport"]
+        out["choice"] = choice
+    out["rccl"] = commtune.rccl_channels(rccl_log)
+    return out
+
+
 def _timed(step, n, world, device):
     if world > 1:
         dist.barrier()
@@ -300,11 +338,12 @@ def _reference_eager_tok_s(args, cfg, device, pool) -> float | None:
     try:
         model, runner = _build(args, cfg, device, "reference", 1)
         step = _make_step(runner, pool, device)
-        for i in range(2):
+        steps = args.steps if args.ref_steps < 0 else args.ref_steps
+        for i in range(args.warmup):  # the headline's own warmup / step counts
             step(i)
-        dt, _ = _timed(step, args.ref_steps, 1, device)
+        dt, _ = _timed(step, steps, 1, device)
         del model, runner
-        return args.batch * args.seq * args.ref_steps / dt
+        return args.batch * args.seq * steps / dt
     except torch.OutOfMemoryError:
         return None
     finally:
@@ -376,12 +415,14 @@ def run_rank(args):
         device = torch.device("cuda", local)
     else:
         device = torch.device("cpu")
+    first_contact = {}
     if world > 1:
+        from penroz.parallel import commtune
+        from penroz.parallel.dist import init_group
         backend = os.environ.get("PENROZ_DIST_BACKEND", "nccl" if args.device == "cuda" else "gloo")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=device)
-        else:
-            dist.init_process_group(backend)
+        rccl_log = commtune.enable_rccl_init_log(rank) if backend == "nccl" else None
+        init_group(backend, device)  # explicit timeout: a stuck rank fails the run, no silent hang
+        first_contact = _first_contact(args, device, world, rccl_log)
 
     cfg = MODELS[args.model]
     B, T, V = args.batch, args.seq, cfg["V"]
@@ -402,6 +443,7 @@ def run_rank(args):
     final_loss = float(loss.item())
 
     comm = _comm_info(runner, world)
+    comm.update(first_contact)
     if world > 1 and args.nocomm_steps > 0:  # outside the timed region
         dt0, _ = _timed(_make_step(runner, pool, device, sync_grads=False), args.nocomm_steps, world, device)
         comm["ms_per_step_without_allreduce"] = dt0 / args.nocomm_steps * 1e3
@@ -433,7 +475,7 @@ def run_rank(args):
         if runtime.get("tokensPerSec_mean"):
             runtime["ratio_vs_executor"] = runtime["tokensPerSec_mean"] / tok_s
     ref_tok_s = None
-    if (world == 1 and device.type == "cuda" and args.engine == "fused" and args.ref_steps > 0
+    if (world == 1 and device.type == "cuda" and args.engine == "fused" and args.ref_steps != 0
             and args.model == "gpt2-124m"):
         if not args.via_runtime:
             ex = getattr(runner, "exec", None)

@@ -1,0 +1,187 @@
+"""First-contact communicator tuning for the gradient all-reduce (RCCL over xGMI, or gloo).
+
+The reference hands gradient synchronisation to DDP's C++ Reducer with fixed 25 MB buckets over
+ProcessGroupNCCL (``/root/reference/neural_net_model.py:609``). Here the transport, the bucket
+size and the wire dtype are choices, and the right ones depend on the node: an MI355X has seven
+point-to-point xGMI links (≈153 GB/s each), so a ring collective's bus bandwidth depends on how
+many channels RCCL spreads over them and on the message size. This module measures that on the
+job's own group, outside any timed region:
+
+* :func:`sweep` — bare in-place AVG all-reduces of one gradient bucket for every (transport,
+  wire dtype, bucket size), each checked for the correct average (rank-valued input), reporting
+  ``ms``, ``algbw`` and ``busbw`` (= algbw · 2(n−1)/n, the per-rank link traffic of a ring);
+* :func:`choose` — the transport for training: the C++ communicator (``csrc/comm/rccl_comm.cpp``)
+  only when it reduced correctly and beat torch's ProcessGroupNCCL by a margin at the bucket size
+  the reducer will use; otherwise c10d;
+* :func:`rccl_channels` — the channel count RCCL picked, parsed from its INIT/GRAPH log
+  (``enable_rccl_init_log`` must run before the first communicator is created);
+* :func:`gather_identities` — every rank's device PCI id, proving N distinct devices.
+"""
+from __future__ import annotations
+
+import glob
+import os
+import re
+import time
+
+import torch
+import torch.distributed as dist
+
+SWEEP_SIZES_MB = (16, 32, 64, 128, 256)
+_LOG_DIR = "/tmp"
+
+
+def enable_rccl_init_log(rank: int) -> str | None:
+    """Route RCCL's INIT/GRAPH info log to a per-rank file (only if the user set no NCCL_DEBUG).
+
+    Must run before the first RCCL communicator of the process is created (RCCL reads these
+    once). Returns the file pattern, or None when the user's own settings are kept."""
+    if "NCCL_DEBUG" in os.environ:
+        return None
+    pattern = os.path.join(_LOG_DIR, f"penroz_rccl_r{rank}_{os.getpid()}.log")
+    os.environ["NCCL_DEBUG"] = "INFO"
+    os.environ["NCCL_DEBUG_SUBSYS"] = "INIT,GRAPH"
+    os.environ["NCCL_DEBUG_FILE"] = pattern
+    return pattern
+
+
+_CHAN_RE = [re.compile(r"(\d+) coll channels"), re.compile(r"Channel \d+/(\d+)")]
+
+
+def rccl_channels(pattern: str | None) -> dict:
+    """{'coll_channels': n | None, 'log': path} from the INIT log written under ``pattern``."""
+    if not pattern:
+        return {"coll_channels": None, "log": None}
+    files = sorted(glob.glob(pattern + "*")) or ([pattern] if os.path.exists(pattern) else [])
+    n = None
+    for f in files:
+        try:
+            text = open(f, errors="replace").read()
+        except OSError:
+            continue
+        for rx in _CHAN_RE:
+            vals = [int(v) for v in rx.findall(text)]
+            if vals:
+                n = max(vals)
+                break
+        if n is not None:
+            break
+    return {"coll_channels": n, "log": files[0] if files else None}
+
+
+def gather_identities(device: torch.device) -> list[dict]:
+    from penroz.parallel.dist import device_identity
+    me = device_identity(device)
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, me)
+    return out
+
+
+def _sync(device):
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+
+
+def _native_or_none(device):
+    """The C++ communicator on every rank, or None on every rank (agreed over the c10d group)."""
+    ok = torch.zeros(1, device=device)
+    native = None
+    if device.type == "cuda" and os.environ.get("PENROZ_COMM_SWEEP_NATIVE", "1") != "0":
+        try:
+            from penroz.parallel import rccl
+            rccl.load_module()
+            ok += 1
+        except Exception:  # module missing on this rank: nobody builds a communicator
+            pass
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if ok.item() > 0:
+        import threading
+        from penroz.parallel import rccl
+        from penroz.parallel.dist import dist_timeout_s
+        # ncclCommInitRank blocks until every rank has joined and has no timeout of its own:
+        # a rank that never gets there must end the job, not hang it
+        guard = threading.Timer(dist_timeout_s(), lambda: os._exit(124))
+        guard.daemon = True
+        guard.start()
+        try:
+            native = rccl.NativeComm.get()
+        finally:
+            guard.cancel()
+    return native
+
+
+def sweep(device: torch.device, sizes_mb=SWEEP_SIZES_MB, wires=("fp32", "bf16"), transports=("c10d", "native"),
+          iters: int = 3, warmup: int = 1) -> list[dict]:
+    """Time every (transport, wire, bucket size); max over ranks; correctness-checked.
+
+    The input on rank r is r + 1 everywhere, so the average is (n + 1) / 2 exactly in fp32 and
+    bf16 (n ≤ 255); ``ok`` records whether the result matched on every rank."""
+    world, rank = dist.get_world_size(), dist.get_rank()
+    gloo = dist.get_backend() != "nccl"
+    native = _native_or_none(device) if "native" in transports else None
+    expect = (world + 1) / 2.0
+    rows = []
+    for wire in wires:
+        dt = {"fp32": torch.float32, "bf16": torch.bfloat16}[wire]
+        for mb in sizes_mb:
+            n = int(mb * 2**20) // 4  # elements of an fp32 gradient bucket of that size
+            buf = torch.empty(n, device=device, dtype=dt)
+            for tr in transports:
+                if tr == "native" and native is None:
+                    continue
+
+                def one():
+                    if tr == "native":
+                        native.all_reduce_avg_async(buf)
+                        native.wait_all()
+                    elif gloo:
+                        dist.all_reduce(buf)
+                        buf.div_(world)
+                    else:
+                        dist.all_reduce(buf, op=dist.ReduceOp.AVG)
+
+                buf.fill_(rank + 1)
+                one()
+                _sync(device)
+                good = torch.tensor([1.0 if bool((buf == expect).all()) else 0.0], device=device)
+                for _ in range(max(0, warmup - 1)):
+                    one()
+                _sync(device)
+                dist.barrier()
+                t0 = time.perf_counter()
+                for _ in range(iters):
+                    one()
+                _sync(device)
+                dist.barrier()
+                t = torch.tensor([(time.perf_counter() - t0) / iters], dtype=torch.float64, device=device)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                dist.all_reduce(good, op=dist.ReduceOp.MIN)
+                sec = float(t.item())
+                nbytes = buf.numel() * buf.element_size()
+                alg = nbytes / sec / 1e9
+                rows.append({"transport": tr, "wire": wire, "bucket_mb": mb, "ms": round(sec * 1e3, 4),
+                             "algbw_GBps": round(alg, 2), "busbw_GBps": round(alg * 2 * (world - 1) / world, 2),
+                             "ok": bool(good.item() > 0)})
+            del buf
+    return rows
+
+
+def choose(rows: list[dict], bucket_mb: float, margin: float = 1.03) -> dict:
+    """Transport for the fp32 gradient all-reduce at ``bucket_mb`` (the nearest swept size):
+    native only if it was correct and ≥ ``margin`` × c10d's bus bandwidth there."""
+    fp = [r for r in rows if r["wire"] == "fp32"]
+    if not fp:
+        return {"transport": "c10d", "reason": "no sweep"}
+    size = min({r["bucket_mb"] for r in fp}, key=lambda s: abs(s - bucket_mb))
+    at = {r["transport"]: r for r in fp if r["bucket_mb"] == size}
+    c, n = at.get("c10d"), at.get("native")
+    if c is None:
+        return {"transport": "c10d", "reason": "c10d not swept"}
+    if n is None:
+        return {"transport": "c10d", "reason": "native communicator unavailable", "at_mb": size}
+    if not n["ok"]:
+        return {"transport": "c10d", "reason": "native all-reduce result wrong", "at_mb": size}
+    if n["busbw_GBps"] >= margin * c["busbw_GBps"]:
+        return {"transport": "native", "reason": f"native {n['busbw_GBps']} vs c10d {c['busbw_GBps']} GB/s",
+                "at_mb": size}
+    return {"transport": "c10d", "reason": f"native {n['busbw_GBps']} vs c10d {c['busbw_GBps']} GB/s", "at_mb": size}

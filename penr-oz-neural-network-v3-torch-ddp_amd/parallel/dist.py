@@ -40,15 +40,46 @@ def use_ddp(device: str) -> bool:
     return is_ddp()
 
 
+def dist_timeout_s() -> float:
+    """Collective / rendezvous timeout (``PENROZ_DIST_TIMEOUT`` seconds, default 300).
+
+    torch's default is 10 min for NCCL (30 for gloo); a dead or stuck rank should instead fail
+    the job with a non-zero exit well inside a benchmark driver's budget. On the nccl (RCCL)
+    backend the ProcessGroupNCCL watchdog aborts the communicator and tears the process down
+    when a collective exceeds it (``TORCH_NCCL_ASYNC_ERROR_HANDLING=1``, set here unless the
+    caller chose otherwise); on gloo the blocked collective raises."""
+    return float(os.environ.get("PENROZ_DIST_TIMEOUT", "300"))
+
+
+def init_group(backend: str, device: torch.device | None = None, timeout_s: float | None = None):
+    """``dist.init_process_group`` with an explicit timeout (and ``device_id`` binding on nccl)."""
+    import datetime
+    if not (dist.is_available() and not dist.is_initialized()):
+        return dist.group.WORLD
+    timeout = datetime.timedelta(seconds=timeout_s if timeout_s is not None else dist_timeout_s())
+    kwargs = {"timeout": timeout}
+    if backend == "nccl":
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        if device is not None:
+            kwargs["device_id"] = device
+    dist.init_process_group(backend=backend, **kwargs)
+    return dist.group.WORLD
+
+
 def init_process_group(device: str):
     """Initialise the default group once (env:// rendezvous on MASTER_ADDR/PORT)."""
-    if dist.is_available() and not dist.is_initialized():
-        backend = backend_for(device)
-        kwargs = {}
-        if backend == "nccl":
-            kwargs["device_id"] = torch.device(f"cuda:{ddp_local_rank()}")
-        dist.init_process_group(backend=backend, **kwargs)
-    return dist.group.WORLD
+    backend = backend_for(device)
+    return init_group(backend, torch.device(f"cuda:{ddp_local_rank()}") if backend == "nccl" else None)
+
+
+def device_identity(device: torch.device) -> dict:
+    """What identifies this rank's device: PCI domain:bus:device and UUID (GPU), or the host."""
+    if device.type != "cuda":
+        import socket
+        return {"device": "cpu", "host": socket.gethostname(), "pid": os.getpid()}
+    p = torch.cuda.get_device_properties(device)
+    pci = f"{getattr(p, 'pci_domain_id', 0):04x}:{getattr(p, 'pci_bus_id', 0):02x}:{getattr(p, 'pci_device_id', 0):02x}"
+    return {"device": str(device), "pci": pci, "uuid": str(getattr(p, "uuid", "")), "name": p.name}
 
 
 def ddp_all_reduce(tensor: torch.Tensor):

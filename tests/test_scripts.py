@@ -102,6 +102,13 @@ def test_bench_self_launches_ranks_cpu_gloo():
     assert d["comm"]["allreduce_exposed_ms"] >= 0.0
     assert d["comm"]["probe_allreduce_mb"] == 4 and d["comm"]["probe_busbw_GBps"] > 0
     assert d["steps"] == 2 and d["warmup"] == 1 and d["value"] > 0
+    # first-contact record: both ranks' devices, the checked sweep, the transport choice
+    assert len(d["comm"]["devices"]) == 2
+    sweep = d["comm"]["sweep"]
+    assert {r["bucket_mb"] for r in sweep} == {1, 4} and {r["wire"] for r in sweep} == {"fp32", "bf16"}
+    assert all(r["ok"] and r["busbw_GBps"] > 0 and r["transport"] == "c10d" for r in sweep)
+    assert d["comm"]["choice"]["transport"] == "c10d"
+    assert set(d["comm"]["rccl"]) == {"coll_channels", "log"}
 
 
 def test_bench_refuses_more_gpus_than_visible():
@@ -110,6 +117,58 @@ def test_bench_refuses_more_gpus_than_visible():
     assert r.returncode != 0
     assert "GPU(s) are visible" in r.stderr
     assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def test_comm_choice_rules():
+    from penroz.parallel.commtune import choose
+    row = lambda tr, bw, ok=True, mb=64, wire="fp32": {"transport": tr, "wire": wire, "bucket_mb": mb,
+                                                        "busbw_GBps": bw, "ok": ok}
+    assert choose([row("c10d", 100), row("native", 120)], 64)["transport"] == "native"
+    assert choose([row("c10d", 100), row("native", 101)], 64)["transport"] == "c10d"   # inside the margin
+    assert choose([row("c10d", 100), row("native", 200, ok=False)], 64)["transport"] == "c10d"  # wrong sum
+    assert choose([row("c10d", 100)], 64)["transport"] == "c10d"
+    # nearest swept size to the reducer's bucket decides
+    rows = [row("c10d", 100, mb=32), row("native", 90, mb=32), row("c10d", 100, mb=128), row("native", 150, mb=128)]
+    assert choose(rows, 100)["transport"] == "native" and choose(rows, 40)["transport"] == "c10d"
+
+
+def test_init_group_passes_timeout(monkeypatch):
+    import datetime
+    import torch.distributed as dist
+    from penroz.parallel import dist as pdist
+    seen = {}
+    monkeypatch.setattr(dist, "is_initialized", lambda: False)
+    monkeypatch.setattr(dist, "init_process_group", lambda **kw: seen.update(kw))
+    monkeypatch.setenv("PENROZ_DIST_TIMEOUT", "42")
+    monkeypatch.delenv("TORCH_NCCL_ASYNC_ERROR_HANDLING", raising=False)
+    import torch
+    pdist.init_group("nccl", torch.device("cuda", 0))
+    assert seen["timeout"] == datetime.timedelta(seconds=42) and seen["backend"] == "nccl"
+    assert seen["device_id"] == torch.device("cuda", 0)
+    assert os.environ["TORCH_NCCL_ASYNC_ERROR_HANDLING"] == "1"
+    seen.clear()
+    pdist.init_process_group("cpu")
+    assert seen["backend"] == "gloo" and "device_id" not in seen and seen["timeout"].total_seconds() == 42
+
+
+@pytest.mark.slow
+def test_stalled_rank_fails_within_timeout():
+    """A rank stuck outside a collective makes its peer fail after PENROZ_DIST_TIMEOUT, and the
+    supervising launcher ends the whole group with a nonzero code: no hang."""
+    import subprocess
+    import sys
+    import time
+    code = ("import sys, types, bench; sys.exit(bench.launch_ranks(types.SimpleNamespace(gpus=2, device='cpu'), [], "
+            f"script={os.path.join(ROOT, 'tests', 'stall_rank_helper.py')!r}))")
+    env = dict(os.environ, PENROZ_DIST_TIMEOUT="3")
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    t0 = time.time()
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=90, env=env)
+    took = time.time() - t0
+    assert r.returncode != 0, r.stdout + r.stderr
+    assert "rank0 collective failed" in r.stdout, r.stdout + r.stderr
+    assert took < 60, took
 
 
 @pytest.mark.slow
