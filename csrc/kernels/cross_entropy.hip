@@ -150,9 +150,11 @@ torch::Tensor cross_entropy_fwd_bwd(torch::Tensor logits, torch::Tensor targets,
   TORCH_CHECK(ld % 8 == 0 && ld >= ((V + 7) & ~7) && reinterpret_cast<uintptr_t>(logits.data_ptr()) % 16 == 0,
               "logits rows must start 16-B aligned with a row stride that is a multiple of 8 and >= V rounded up to "
               "8 (pad the buffer: [N, ld][:, :V])");
-  TORCH_CHECK(N <= 1 || logits.storage().nbytes() >= (size_t)(logits.storage_offset() + (int64_t)(N - 1) * ld +
-                                                              ((V + 7) & ~7)) * logits.element_size(),
-              "logits: the last row's padding must be allocated");
+  // every row's 16-B chunks (the last one padded up to 8 elements) must be allocated — N == 1
+  // included, where the row stride says nothing about the padding
+  TORCH_CHECK(logits.storage().nbytes() >= (size_t)(logits.storage_offset() + (int64_t)(N > 0 ? N - 1 : 0) * ld +
+                                                    ((V + 7) & ~7)) * logits.element_size(),
+              "logits: the last row's padding must be allocated (pad the buffer: [N, ld][:, :V])");
   auto loss = torch::empty({N}, logits.options().dtype(torch::kFloat32));
   if (N == 0) return loss;
   auto tg = targets.contiguous();

@@ -3,12 +3,14 @@
 // dtype = promote(x, w). One wave per row (any width % 4), 4 rows per workgroup; dγ partials
 // accumulate per workgroup in LDS and are finished by a column reduction (no global atomics).
 #include "common.h"
-#include "deferred.h"
+#include "reduce.h"
 #include <type_traits>
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 
 namespace penroz {
+
+constexpr int RMS_BWD_MAX_C = 10240;  // rms_bwd_wide_kernel: 4 waves x C fp32 partials in LDS (160 KiB)
 
 template <typename TX, typename TW, typename TY>
 __global__ void __launch_bounds__(256) rms_fwd_kernel(const TX* __restrict__ x, const TW* __restrict__ w,
@@ -74,6 +76,34 @@ __global__ void __launch_bounds__(256) rms_bwd_kernel(const TDY* __restrict__ dy
   for (int k = 0; k < NPL; ++k) {
     const int c = lane + 64 * k;
     if (c < C) dwl[wid * C + c] = dwa[k];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x)
+    part[(size_t)blockIdx.x * C + c] = dwl[c] + dwl[C + c] + dwl[2 * C + c] + dwl[3 * C + c];
+}
+
+// Widths past the register-resident kernel (C > 2048: Gemma-3 4B 2560, 12B 3840, 27B 5376): one
+// wave per row in two lane-strided (coalesced) passes over the row (dot, then dx); each wave's dγ partials live in its own LDS row [C] (no atomics), combined per
+// workgroup exactly like rms_bwd_kernel. LDS = 16·C bytes, so C ≤ 10240.
+template <typename TX, typename TW, typename TDY>
+__global__ void __launch_bounds__(256) rms_bwd_wide_kernel(const TDY* __restrict__ dy, const TX* __restrict__ x,
+                                                           const TW* __restrict__ w, const float* __restrict__ rstd,
+                                                           TX* __restrict__ dx, float* __restrict__ part, int N, int C) {
+  extern __shared__ __attribute__((aligned(16))) float dwl[];  // [4 waves][C]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float* my = dwl + wid * C;
+  for (int c = lane; c < C; c += 64) my[c] = 0.f;
+  for (int row = blockIdx.x * 4 + wid; row < N; row += gridDim.x * 4) {
+    const size_t base = (size_t)row * C;
+    const float r = rstd[row];
+    float dot = 0.f;
+    for (int c = lane; c < C; c += 64) dot += to_f(dy[base + c]) * to_f(w[c]) * to_f(x[base + c]);
+    dot = wave_sum(dot) / C;
+    for (int c = lane; c < C; c += 64) {
+      const float xv = to_f(x[base + c]), gv = to_f(dy[base + c]);
+      my[c] += gv * to_f(from_f<TX>(xv * r));  // each lane owns its columns: no race
+      dx[base + c] = from_f<TX>(r * gv * to_f(w[c]) - xv * r * r * r * dot);
+    }
   }
   __syncthreads();
   for (int c = threadIdx.x; c < C; c += blockDim.x)
@@ -187,7 +217,7 @@ std::vector<torch::Tensor> rmsnorm_fwd(torch::Tensor x, torch::Tensor w, double 
 std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor w, torch::Tensor rstd) {
   TORCH_CHECK(x.is_cuda() && x.is_contiguous() && dy.is_contiguous() && dy.numel() == x.numel());
   const int N = x.size(0), C = x.size(1);
-  TORCH_CHECK(C <= 64 * 32, "RMSNorm backward: width <= 2048");
+  TORCH_CHECK(C <= RMS_BWD_MAX_C, "RMSNorm backward: width <= ", RMS_BWD_MAX_C);
   auto dx = torch::empty_like(x);
   const int G = std::max(1, std::min((N + 3) / 4, 2048));
   auto part = torch::empty({G, C}, x.options().dtype(torch::kFloat32));
@@ -207,12 +237,24 @@ std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor dy, torch::Tensor x, torch:
   if (npl <= 4) launch(std::integral_constant<int, 4>{});
   else if (npl <= 8) launch(std::integral_constant<int, 8>{});
   else if (npl <= 18) launch(std::integral_constant<int, 18>{});
-  else launch(std::integral_constant<int, 32>{});
-  // dγ = Σ of the G partial rows: the sliced two-stage column reduction (reduce.h). A single
-  // 256-thread block walking all G rows per column (the former finish kernel) was latency-bound:
-  // 120 µs per call at Gemma's head_dim-256 q/k norms (G = 512)
+  else if (npl <= 32) launch(std::integral_constant<int, 32>{});
+  else {
+    RMS_TYPES(x.scalar_type(), TX, RMS_TYPES(w.scalar_type(), TW, RMS_TYPES(dy.scalar_type(), TDY,
+      auto kern = rms_bwd_wide_kernel<TX, TW, TDY>;
+      hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          4 * C * (int)sizeof(float));
+      hipLaunchKernelGGL(kern, dim3(G), dim3(256), 4 * C * sizeof(float), stream,
+                         reinterpret_cast<const TDY*>(dy.data_ptr()), reinterpret_cast<const TX*>(x.data_ptr()),
+                         reinterpret_cast<const TW*>(wc.data_ptr()), rstd.data_ptr<float>(),
+                         reinterpret_cast<TX*>(dx.data_ptr()), part.data_ptr<float>(), N, C))))
+  }
+  // dγ = Σ of the G partial rows: the sliced two-stage column reduction (reduce.h), on the CURRENT
+  // stream — dw goes straight back to autograd, so it must not be finished on the executor's
+  // deferred side stream (nothing would order the caller's reads after it)
+  const int S = reduce_slices(G);
+  auto mid = torch::empty({1, S, C}, part.options());
   float* outs[1] = {dw.data_ptr<float>()};
-  reduce_partials_auto(part, 1, G, C, outs, stream);
+  reduce_partials_add(part.data_ptr<float>(), 1, G, C, outs, mid.data_ptr<float>(), S, stream);
   return {dx, dw};
 }
 

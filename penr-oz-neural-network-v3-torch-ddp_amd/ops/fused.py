@@ -70,16 +70,20 @@ def cross_entropy_fwd_bwd(logits: Tensor, targets: Tensor, grad_scale: float, ig
 
 
 class _FusedCrossEntropyFn(torch.autograd.Function):
-    """Mean cross-entropy over the non-ignored rows of bf16/fp16 logits [N, V]: one kernel pass
-    computes the per-row loss (fp32 statistics) and the gradient of the summed loss into a separate
-    buffer; backward scales it by grad_output / n_valid on the device (no host sync)."""
+    """Mean cross-entropy over the non-ignored rows of bf16 logits [N, V]: one kernel pass computes
+    the per-row loss (fp32 statistics) and, when a gradient will be needed, the gradient of the
+    summed loss into a separate buffer; backward scales it by grad_output / n_valid on the device
+    (no host sync). Every target ignored gives NaN, as ``F.cross_entropy`` does (0 / 0)."""
 
     @staticmethod
     def forward(ctx, logits, targets, ignore_index):
+        n_valid = (targets != ignore_index).sum().to(torch.float32)
+        if not ctx.needs_input_grad[0]:  # no_grad / eval (evaluate_model, /output): loss only
+            rows = kernels().cross_entropy_fwd_bwd(logits, targets, 0.0, int(ignore_index))
+            return rows.sum() / n_valid
         grad = torch.empty_like(logits)
         rows = kernels().cross_entropy_fwd_bwd(logits, targets, 1.0, int(ignore_index), grad)
-        n_valid = (targets != ignore_index).sum().clamp_min(1).to(torch.float32)
-        ctx.save_for_backward(grad, n_valid)
+        ctx.save_for_backward(grad, n_valid.clamp_min(1))
         return rows.sum() / n_valid
 
     @staticmethod
@@ -89,10 +93,12 @@ class _FusedCrossEntropyFn(torch.autograd.Function):
 
 
 def cross_entropy(logits: Tensor, targets: Tensor, ignore_index: int = -100) -> Tensor:
-    """``F.cross_entropy(logits, targets)`` (mean over non-ignored rows). GPU bf16/fp16 logits whose
-    rows are 16-B aligned take the fused HIP kernel (replaces autocast's fp32 cast + log_softmax +
-    nll + their backward: ~60 GB of traffic at a 262k vocabulary, B·T = 8k); anything else runs torch."""
-    if (use_kernels(logits) and logits.dim() == 2 and logits.dtype in (torch.bfloat16, torch.float16)
+    """``F.cross_entropy(logits, targets)`` (mean over non-ignored rows). GPU bf16 logits whose rows
+    are 16-B aligned take the fused HIP kernel (replaces autocast's fp32 cast + log_softmax + nll +
+    their backward: ~60 GB of traffic at a 262k vocabulary, B·T = 8k); anything else runs torch —
+    fp16 logits included: under fp16 + GradScaler the gradient must be scaled in fp32 before it is
+    rounded to fp16 (small probabilities would flush), which torch's autocast CE does."""
+    if (use_kernels(logits) and logits.dim() == 2 and logits.dtype == torch.bfloat16
             and logits.stride(1) == 1 and logits.shape[1] % 8 == 0 and logits.is_contiguous()
             and targets.dtype == torch.int64 and targets.dim() == 1):
         return _FusedCrossEntropyFn.apply(logits, targets, ignore_index)

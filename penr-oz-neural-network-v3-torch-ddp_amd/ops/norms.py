@@ -142,6 +142,9 @@ def rms_norm(x: Tensor, w: Tensor, eps: float) -> Tensor:
     """``(x_f32 * rsqrt(mean(x²) + eps)).to(x.dtype) * w`` — reference semantics. Autocast does not
     change that expression (the statistics are fp32 already; the product follows type promotion),
     so the HIP kernel (fp32 statistics, output dtype = promote(x, w)) serves both modes."""
-    if use_kernels(x) and x.shape[-1] % 4 == 0:
+    if use_kernels(x) and x.shape[-1] % 4 == 0 and x.shape[-1] <= RMS_BWD_MAX_C:
         return _RMSNormFn.apply(x, w, eps)
     return reference_rms_norm(x, w, eps)
+
+
+RMS_BWD_MAX_C = 10240  # the HIP backward keeps 4 waves x C fp32 dγ partials in LDS (rmsnorm.hip)

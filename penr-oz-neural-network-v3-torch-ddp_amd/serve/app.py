@@ -214,6 +214,68 @@ def serving_lock(model: NeuralNetworkModel) -> threading.Lock:
     return lk
 
 
+def _lock_timeout_s() -> float:
+    return float(os.environ.get("PENROZ_SERVE_LOCK_TIMEOUT", "120"))
+
+
+class _Held:
+    """``with _Held(model):`` — the model's serving lock, waited for at most
+    ``PENROZ_SERVE_LOCK_TIMEOUT`` seconds (then 503: busy), never indefinitely."""
+
+    def __init__(self, model):
+        self.lock = serving_lock(model)
+
+    def __enter__(self):
+        if not self.lock.acquire(timeout=_lock_timeout_s()):
+            raise HTTPException(status_code=503, detail="Model is busy serving another request; retry later.")
+        return self
+
+    def __exit__(self, *exc):
+        self.lock.release()
+
+
+class _LockedStream:
+    """A token stream that owns the model's serving lock from before the response starts until
+    the stream is finished OR abandoned. The response's background task (run by Starlette after
+    the body, also when the client disconnected mid-stream) closes the generator — retrying
+    while a threadpool thread is still inside it producing a token — so its ``finally`` releases
+    the lock at once instead of whenever the abandoned generator is garbage-collected."""
+
+    def __init__(self, model, tokens):
+        self.lock = serving_lock(model)
+        if not self.lock.acquire(timeout=_lock_timeout_s()):
+            raise HTTPException(status_code=503, detail="Model is busy serving another request; retry later.")
+        self._released = False
+        self._guard = threading.Lock()
+        self.gen = self._run(tokens)
+
+    def _release(self):
+        with self._guard:
+            if not self._released:
+                self._released = True
+                self.lock.release()
+
+    def _run(self, tokens):
+        try:
+            for token in tokens:
+                yield f"{token}\n"
+        finally:
+            self._release()
+
+    def close(self):
+        import time
+        deadline = time.monotonic() + _lock_timeout_s()
+        while True:
+            try:
+                self.gen.close()  # suspended at a yield (or finished): runs the finally now
+                break
+            except ValueError:  # "generator already executing" on a threadpool thread
+                if time.monotonic() > deadline:
+                    return
+                time.sleep(0.005)
+        self._release()  # never started: the finally never ran
+
+
 def _checkpoint_mtime(model_id: str) -> float | None:
     p = os.path.join(NeuralNetworkModel.SHM_PATH, NeuralNetworkModel.get_model_path(model_id))
     if not os.path.exists(p):
@@ -320,7 +382,7 @@ def tokenize_text(body: TokenizeTextRequest = Body(...)):
 @app.post("/output/")
 def compute_model_output(body: OutputRequest = Body(...)):
     model = load_for_serving(body.model_id)
-    with serving_lock(model):
+    with _Held(model):
         output, cost = model.compute_output(body.input, body.target)
     return {"output": output, "cost": cost}
 
@@ -328,7 +390,7 @@ def compute_model_output(body: OutputRequest = Body(...)):
 @app.post("/evaluate/")
 def evaluate_model(body: EvaluateRequest = Body(...)):
     model = load_for_serving(body.model_id)
-    with serving_lock(model):
+    with _Held(model):
         cost = model.evaluate_model(body.dataset_id, body.target_dataset_id, body.shard, body.epochs,
                                     body.batch_size, body.block_size, body.step_size)
     return {"cost": cost}
@@ -338,15 +400,13 @@ def evaluate_model(body: EvaluateRequest = Body(...)):
 def model_generate(body: GenerateRequest = Body(...)):
     model = load_for_serving(body.model_id)
     if body.stream:
-        def token_stream():
-            # held for the stream's whole lifetime (the KV cache stays attached between chunks);
-            # a disconnected client's generator is closed on collection, which releases it
-            with serving_lock(model):
-                for token in model.generate_tokens_stream(body.input, body.block_size, body.max_new_tokens,
-                                                          body.temperature, body.top_k, body.stop_token):
-                    yield f"{token}\n"
-        return StreamingResponse(token_stream(), media_type="text/plain")
-    with serving_lock(model):
+        # the lock is held for the stream's whole lifetime (the KV cache stays attached between
+        # chunks) and released by the background task even when the client goes away mid-stream
+        from starlette.background import BackgroundTask
+        st = _LockedStream(model, model.generate_tokens_stream(body.input, body.block_size, body.max_new_tokens,
+                                                              body.temperature, body.top_k, body.stop_token))
+        return StreamingResponse(st.gen, media_type="text/plain", background=BackgroundTask(st.close))
+    with _Held(model):
         tokens = model.generate_tokens(body.input, body.block_size, body.max_new_tokens, body.temperature,
                                        body.top_k, body.stop_token)
     return {"tokens": tokens}

@@ -127,6 +127,36 @@ def test_fused_cross_entropy_autograd_matches_torch(N, V):
     assert logits.grad[1].abs().max().item() == 0.0
 
 
+def test_fused_cross_entropy_no_grad_and_all_ignored():
+    """Under no_grad the fused CE computes the loss only (no gradient buffer, logits untouched);
+    every target ignored gives NaN like F.cross_entropy; fp16 logits run torch's CE."""
+    logits = (torch.randn(16, 1000, device=DEV) * 3).to(torch.bfloat16)
+    tg = torch.randint(0, 1000, (16,), device=DEV)
+    keep = logits.clone()
+    with torch.no_grad():
+        loss = Fu.cross_entropy(logits, tg)
+    assert torch.equal(logits, keep)
+    assert abs(loss.item() - F.cross_entropy(logits.float(), tg).item()) < 2e-3
+    allign = torch.full((16,), -100, device=DEV, dtype=torch.long)
+    assert torch.isnan(Fu.cross_entropy(logits, allign)) and torch.isnan(F.cross_entropy(logits.float(), allign))
+    h = logits.half().requires_grad_()
+    lh = Fu.cross_entropy(h, tg)
+    lh.backward()
+    assert lh.grad_fn.name() != "_FusedCrossEntropyFnBackward" and torch.isfinite(h.grad).all()
+
+
+def test_cross_entropy_single_unpadded_row_is_refused():
+    """A lone [1, V] row with V % 8 != 0 and no allocated padding: the kernel's last 16-B chunk
+    would run past the allocation, so the call is refused instead (pad the buffer)."""
+    logits = torch.randn(1, 50257, device=DEV).to(torch.bfloat16)
+    with pytest.raises(RuntimeError, match="padding"):
+        Fu.cross_entropy_fwd_bwd(logits, torch.tensor([5], device=DEV), 1.0)
+    buf = torch.zeros(1, 50264, device=DEV, dtype=torch.bfloat16)
+    buf[:, :50257] = logits
+    loss = Fu.cross_entropy_fwd_bwd(buf[:, :50257], torch.tensor([5], device=DEV), 0.0)
+    assert abs(loss.item() - F.cross_entropy(logits.float(), torch.tensor([5], device=DEV)).item()) < 2e-3
+
+
 def test_colsum():
     x = torch.randn(4099, 2304, device=DEV).to(torch.bfloat16)
     out = torch.full((2304,), 2.0, device=DEV)
@@ -551,16 +581,19 @@ def test_sampling_wide_rows(dt, V):
 @pytest.mark.parametrize("autocast", [False, True])
 @pytest.mark.parametrize("xdt,wdt", [(torch.float32, torch.float32), (torch.bfloat16, torch.bfloat16),
                                      (torch.float32, torch.bfloat16)])
-def test_rmsnorm(xdt, wdt, autocast):
-    """HIP RMSNorm (also under bf16 autocast, as the generic engine runs it) vs the reference expression."""
-    x = torch.randn(100, 640, device=DEV).to(xdt)
-    w = torch.randn(640, device=DEV).to(wdt)
+@pytest.mark.parametrize("C", [640, 2560, 5376, 1100])
+def test_rmsnorm(xdt, wdt, autocast, C):
+    """HIP RMSNorm (also under bf16 autocast, as the generic engine runs it) vs the reference
+    expression; widths past the register kernel (Gemma-3 4B 2560, 27B 5376) and one that is not a
+    multiple of 64 take the wide backward kernel / the masked lanes."""
+    x = torch.randn(100, C, device=DEV).to(xdt)
+    w = torch.randn(C, device=DEV).to(wdt)
     with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
         y = Nm.rms_norm(x, w, 1e-6)
     assert y.dtype == torch.promote_types(xdt, wdt)
     _close(y, Nm.reference_rms_norm(x, w, 1e-6), 0.03, 0.01)
     xr, wr = x.detach().float().clone().requires_grad_(), w.detach().float().clone().requires_grad_()
-    dy = torch.randn(100, 640, device=DEV)
+    dy = torch.randn(100, C, device=DEV)
     Nm.reference_rms_norm(xr, wr, 1e-6).backward(dy)
     xg, wg = x.detach().clone().requires_grad_(), w.detach().clone().requires_grad_()
     Nm.rms_norm(xg, wg, 1e-6).backward(dy.to(y.dtype))

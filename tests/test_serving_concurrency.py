@@ -138,3 +138,40 @@ def test_stats_served_from_sidecar(served_model, monkeypatch):
         AssertionError("/stats must not load the checkpoint"))))
     client = TestClient(main.app, raise_server_exceptions=True)
     assert client.get("/stats/?model_id=conc").json() == {"layers": [], "weights": []}
+
+
+def test_abandoned_stream_releases_the_model(served_model, monkeypatch):
+    """A client that reads one chunk of a streaming /generate and goes away: the response's
+    background task closes the token generator, which releases the serving lock at once (not at
+    garbage collection), so the next request runs; a request that cannot get the lock within
+    PENROZ_SERVE_LOCK_TIMEOUT gets 503 instead of queueing forever."""
+    import asyncio
+    from penroz.serve.app import GenerateRequest
+    model = A.load_for_serving("conc")
+    resp = A.model_generate(GenerateRequest(model_id="conc", input=[[1, 2, 3]], block_size=16, max_new_tokens=24,
+                                            temperature=0.0, stream=True))
+    lock = A.serving_lock(model)
+
+    async def one_chunk_then_drop():
+        it = resp.body_iterator.__aiter__()
+        first = await it.__anext__()
+        assert first.strip().isdigit()
+        assert lock.locked()  # held while the stream is open
+        await resp.background()  # what Starlette runs after a disconnect
+
+    asyncio.run(one_chunk_then_drop())
+    assert not lock.locked()
+    client = TestClient(main.app, raise_server_exceptions=True)
+    r = client.post("/generate/", json={"model_id": "conc", "input": [[1, 2, 3]], "block_size": 16,
+                                        "max_new_tokens": 4, "temperature": 0.0})
+    assert r.status_code == 200
+    monkeypatch.setenv("PENROZ_SERVE_LOCK_TIMEOUT", "0.2")
+    assert lock.acquire(timeout=1)
+    try:
+        r = client.post("/generate/", json={"model_id": "conc", "input": [[1, 2, 3]], "block_size": 16,
+                                            "max_new_tokens": 4, "temperature": 0.0, "stream": True})
+        assert r.status_code == 503
+        r = client.post("/output/", json={"model_id": "conc", "input": [[1, 2, 3]]})
+        assert r.status_code == 503
+    finally:
+        lock.release()
