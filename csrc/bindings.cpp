@@ -58,9 +58,10 @@ void set_deferred_reduce_stream(int64_t stream, int64_t device);
 // decode_attn.hip
 void kv_append(torch::Tensor k, torch::Tensor v, torch::Tensor kc, torch::Tensor vc, c10::optional<torch::Tensor> ks,
                c10::optional<torch::Tensor> vs, c10::optional<torch::Tensor> pos_dev, int64_t pos);
-// gemm.hip
-void gemm_bf16(torch::Tensor a, torch::Tensor b, bool b_kn, c10::optional<torch::Tensor> bias, torch::Tensor out,
-               c10::optional<torch::Tensor> act, int64_t gelu_approx, int64_t ablate);
+// gemm8.hip
+void gemm8_bf16(torch::Tensor a, torch::Tensor b, c10::optional<torch::Tensor> bias, torch::Tensor out,
+                c10::optional<torch::Tensor> act, int64_t gelu_approx, int64_t ablate);
+torch::Tensor gemm8_dma_probe(torch::Tensor src, int64_t bytes, int64_t lds_off, int64_t soff);
 // skinny_gemm.hip
 int64_t skinny_gemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> bias, torch::Tensor out,
                     torch::Tensor ws, torch::Tensor cnt, int64_t splitk);
@@ -130,9 +131,10 @@ PYBIND11_MODULE(penroz_kernels, m) {
   m.def("kv_append", &kv_append, pybind11::arg("k"), pybind11::arg("v"), pybind11::arg("kc"), pybind11::arg("vc"),
         pybind11::arg("ks") = pybind11::none(), pybind11::arg("vs") = pybind11::none(),
         pybind11::arg("pos_dev") = pybind11::none(), pybind11::arg("pos") = 0);
-  m.def("gemm_bf16", &gemm_bf16, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("b_kn"),
-        pybind11::arg("bias") = pybind11::none(), pybind11::arg("out"), pybind11::arg("act") = pybind11::none(),
-        pybind11::arg("gelu_approx") = 0, pybind11::arg("ablate") = 0);
+  m.def("gemm8_bf16", &gemm8_bf16, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("bias") = pybind11::none(),
+        pybind11::arg("out"), pybind11::arg("act") = pybind11::none(), pybind11::arg("gelu_approx") = 0, pybind11::arg("ablate") = 0,
+        "out = a·bᵀ (+bias) (act = GELU(out)), 8-phase 256x256 MFMA GEMM, K % 128 == 0");
+  m.def("gemm8_dma_probe", &gemm8_dma_probe);
   m.def("skinny_gemm", &skinny_gemm, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("bias"),
         pybind11::arg("out"), pybind11::arg("ws"), pybind11::arg("cnt"), pybind11::arg("splitk") = 0,
         "decode-shaped out[M<=64, N] = x·wᵀ (+bias), bf16; returns the split-K factor used");

@@ -74,25 +74,27 @@ def load_tuned_gemms() -> bool:
     return ok
 
 
-# ---- forward / dgrad GEMMs (csrc/kernels/gemm.hip) ------------------------------------------
-# EXPERIMENTAL native path: persistent 256×256-tile MFMA kernel (LDS-DMA double-buffered 64-deep
-# chunks, ping-pong wave groups) with fused bias / bias+GELU epilogues. Measured slower than
-# hipBLASLt on every GPT-2 shape (profiles/gemm_native_r1.log: 0.78-0.92× fwd, 0.85-0.95× dgrad),
-# so it is OFF by default; PENROZ_NATIVE_GEMM=1 routes linear_fwd / linear_dgrad through it.
+# ---- forward / dgrad GEMMs (csrc/kernels/gemm8.hip) -----------------------------------------
+# EXPERIMENTAL native path: persistent 256×256-tile MFMA kernel on the 8-phase ping-pong schedule
+# (one LDS-DMA unit per phase behind one counted wait, buffer-resource DMA with range-checked edges,
+# bias / bias+GELU epilogues). Measured at 0.79-1.00× hipBLASLt per GPT-2 shape, 0.87× summed over a
+# layer (profiles/gemm8_r3.md: the K = 768 tiles lose ~25 % to the lock-step epilogue store burst),
+# so the forward / dgrad GEMMs stay on hipBLASLt; PENROZ_NATIVE_GEMM=1 routes linear_fwd /
+# linear_dgrad through it.
 NATIVE_GEMM = os.environ.get("PENROZ_NATIVE_GEMM", "0")
 
 
-def _gemm_ok(a: Tensor, b: Tensor, n: int) -> bool:
+def _gemm_ok(a: Tensor, b: Tensor) -> bool:
     return (NATIVE_GEMM == "1" and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16
-            and a.shape[1] % 32 == 0 and a.shape[1] >= 128 and n % 8 == 0 and a.stride(1) == 1 and b.stride(1) == 1
+            and a.shape[1] % 128 == 0 and b.shape[0] % 8 == 0 and a.stride(1) == 1 and b.stride(1) == 1
             and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0)
 
 
 def linear_fwd(x: Tensor, w: Tensor, bias: Tensor | None, out: Tensor, act: Tensor | None = None,
                gelu_approx: str = "none") -> Tensor:
     """out = x·wᵀ (+ bias); with ``act``: out = pre-activation, act = GELU(out) (one pass)."""
-    if use_kernels(x) and _gemm_ok(x, w, w.shape[0]):
-        kernels().gemm_bf16(x, w, False, bias, out, act, 1 if gelu_approx == "tanh" else 0)
+    if use_kernels(x) and _gemm_ok(x, w):
+        kernels().gemm8_bf16(x, w, bias, out, act, 1 if gelu_approx == "tanh" else 0)
         return out
     if bias is not None:
         torch.addmm(bias, x, w.t(), out=out)
@@ -103,12 +105,13 @@ def linear_fwd(x: Tensor, w: Tensor, bias: Tensor | None, out: Tensor, act: Tens
     return out
 
 
-def linear_dgrad(dy: Tensor, w: Tensor, out: Tensor) -> Tensor:
-    """out = dy·w (input gradient of y = x·wᵀ)."""
-    if use_kernels(dy) and _gemm_ok(dy, w, w.shape[1]):
-        kernels().gemm_bf16(dy, w, True, None, out)
+def linear_dgrad(dy: Tensor, wt: Tensor, out: Tensor) -> Tensor:
+    """out = dy·w, the input gradient of y = x·wᵀ, from the transposed weight ``wt`` = wᵀ [in, out]
+    (the executor's copy: both operands reduction-contiguous)."""
+    if use_kernels(dy) and _gemm_ok(dy, wt):
+        kernels().gemm8_bf16(dy, wt, None, out)
         return out
-    return torch.mm(dy, w, out=out)
+    return torch.mm(dy, wt.t(), out=out)
 
 
 # ---- decode-shaped GEMMs (csrc/kernels/skinny_gemm.hip) --------------------------------------

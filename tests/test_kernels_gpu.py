@@ -648,28 +648,6 @@ def test_wgrad_gemm(K, M, N, tile, variant):
     assert rel < 1e-4, rel
 
 
-@pytest.mark.parametrize("kn", [False, True])
-@pytest.mark.parametrize("M,K,N,epi", [(4096, 768, 2304, "bias"), (1000, 128, 200, "none"), (2048, 3072, 768, "bias"),
-                                       (777, 256, 1032, "gelu"), (512, 768, 50304, "none")])
-def test_native_gemm(M, K, N, epi, kn):
-    """Experimental fwd/dgrad GEMM (csrc/kernels/gemm.hip, off by default) vs an fp32 reference."""
-    if kn and epi == "gelu":
-        pytest.skip("GELU epilogue is TN only")
-    torch.manual_seed(0)
-    a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
-    b = (torch.randn(K, N, device=DEV) if kn else torch.randn(N, K, device=DEV)).to(torch.bfloat16)
-    bias = torch.randn(N, device=DEV).to(torch.bfloat16) if epi != "none" else None
-    out = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
-    act = torch.full_like(out, float("nan")) if epi == "gelu" else None
-    _ext.kernels().gemm_bf16(a, b, kn, bias, out, act, 0)
-    ref = a.float() @ (b.float() if kn else b.float().t())
-    if bias is not None:
-        ref = ref + bias.float()
-    _close(out, ref, 0.02 * ref.abs().max().item(), msg="gemm")
-    if act is not None:
-        _close(act, F.gelu(out.float()), 0.02, msg="gelu epilogue")
-
-
 @pytest.mark.parametrize("M,K,N", [(64, 768, 2304), (64, 768, 768), (64, 3072, 768), (64, 768, 3072), (1, 768, 50304),
                                    (17, 96, 40), (33, 768, 2304), (64, 768, 50257), (5, 4096, 1024)])
 @pytest.mark.parametrize("with_bias", [True, False])
