@@ -458,12 +458,12 @@ class GPTExecutor:
         return self._full_logits().view(idx.shape[0], idx.shape[1], -1)
 
     def setup_training(self, distributed: bool):
-        from penroz.parallel.reducer import GradReducer, plan_buckets, DEFAULT_BUCKET_MB
+        from penroz.parallel.reducer import GradReducer, plan_buckets, default_bucket_mb
         import torch.distributed as dist
         self.refresh_shadow()
         self.reducer = None
         if distributed and dist.is_initialized() and dist.get_world_size() > 1:
-            buckets = plan_buckets(self.segments, DEFAULT_BUCKET_MB * 2**20)
+            buckets = plan_buckets(self.segments, default_bucket_mb(dist.get_backend()) * 2**20)
             self.reducer = GradReducer(self.flat_grad, buckets)
             self.reducer.broadcast_params(self.flat)
             self.refresh_shadow()

@@ -36,6 +36,14 @@ import torch.distributed as dist
 log = logging.getLogger(__name__)
 
 DEFAULT_BUCKET_MB = float(os.environ.get("PENROZ_BUCKET_MB", "64"))
+# gloo (CPU plumbing config): the reference DDP's 25 MB, so the first buckets' TCP transfers start
+# early in the backward (64 MB buckets left ≈ 500 ms of a 1.9 s CPU step exposed, 25 MB ≈ 310 ms:
+# profiles/bench_r3_cpu_gloo_ws2_t64.log)
+GLOO_BUCKET_MB = float(os.environ.get("PENROZ_BUCKET_MB", "25"))
+
+
+def default_bucket_mb(backend: str | None) -> float:
+    return GLOO_BUCKET_MB if backend == "gloo" else DEFAULT_BUCKET_MB
 WIRE_DTYPES = {"fp32": None, "bf16": torch.bfloat16}
 
 
@@ -176,7 +184,9 @@ class HookedReducer:
     (≈ backward order); a bucket launches when all its parameters have accumulated.
     """
 
-    def __init__(self, params: list[torch.nn.Parameter], bucket_mb: float = DEFAULT_BUCKET_MB, group=None):
+    def __init__(self, params: list[torch.nn.Parameter], bucket_mb: float | None = None, group=None):
+        if bucket_mb is None:
+            bucket_mb = default_bucket_mb(dist.get_backend(group) if dist.is_initialized() else None)
         self.params = [p for p in params if p.requires_grad]
         order = list(reversed(self.params))
         total = sum(p.numel() for p in order)

@@ -53,7 +53,7 @@ def _worker(rank, world, port, out, bucket_mb, overlap):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import penroz.parallel.reducer as R
-    R.DEFAULT_BUCKET_MB = bucket_mb  # several buckets for this small model
+    R.DEFAULT_BUCKET_MB = R.GLOO_BUCKET_MB = bucket_mb  # several buckets for this small model
     from penroz.models.executor import GPTExecutor
     dev = torch.device("cuda", 0)
     model = _model(dev)
