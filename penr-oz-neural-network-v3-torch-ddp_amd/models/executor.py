@@ -213,7 +213,6 @@ class GPTExecutor:
         self._reduce_pending = False
         import os
         self._overlap_opt = os.environ.get("PENROZ_OVERLAP_OPT", "1") != "0"
-        self._fused_qkv_bias = os.environ.get("PENROZ_FUSED_QKV_BIAS", "1") != "0"
         self._side_init()
 
     def _param_order(self):
@@ -511,12 +510,9 @@ class GPTExecutor:
     # before the step returns. PENROZ_WGRAD_STREAM=0 runs everything on one stream (A/B).
     def _side_init(self):
         import os
-        self._side = self._hi = None
+        self._side = None
         if self.device.type == "cuda" and os.environ.get("PENROZ_WGRAD_STREAM", "1") != "0":
             self._side = torch.cuda.Stream(device=self.device)
-            if os.environ.get("PENROZ_HI_PRIO", "0") == "1":  # measured neutral (66.9 vs 67.0 ms)
-                lo, hi = torch.cuda.Stream.priority_range()
-                self._hi = torch.cuda.Stream(device=self.device, priority=hi)
         self._buf_free = {}
 
     def _side_call(self, operand: Tensor, fn):
@@ -558,21 +554,8 @@ class GPTExecutor:
     def train_micro_step(self, idx: Tensor, targets: Tensor, scale: float, sync: bool = True,
                          capture: bool = False) -> Tensor:
         """Forward + backward of one micro-batch; gradients accumulate into the flat buffer.
-
-        Returns the (scaled) mean loss as a device scalar. With the side stream enabled, the
-        critical path (forward, dgrad chain) runs on a HIGH-priority stream so the side stream's
-        gradient-only kernels fill in behind it instead of competing with it as equals.
-        """
-        hi = getattr(self, "_hi", None)
-        if hi is None:
-            return self._train_micro_step(idx, targets, scale, sync, capture)
-        cur = torch.cuda.current_stream(self.device)
-        hi.wait_stream(cur)
-        with torch.cuda.stream(hi):
-            loss = self._train_micro_step(idx, targets, scale, sync, capture)
-        cur.wait_stream(hi)
-        loss.record_stream(cur)
-        return loss
+        Returns the (scaled) mean loss as a device scalar."""
+        return self._train_micro_step(idx, targets, scale, sync, capture)
 
     def _train_micro_step(self, idx: Tensor, targets: Tensor, scale: float, sync: bool, capture: bool) -> Tensor:
         s = self.spec
@@ -641,14 +624,10 @@ class GPTExecutor:
             torch.mm(dres_bf, self._dgrad_w(b.proj.weight), out=self.d_c)
             self._wgrad(dres_bf, self.att[l], b.proj.weight)
             # the qkv bias gradient comes out of the attention-backward epilogues (partials finished
-            # on the side stream by the deferred reduction); PENROZ_FUSED_QKV_BIAS=0: a column-sum
-            # pass over dqkv on the side stream instead (A/B)
-            fused_bias = self._fused_qkv_bias
+            # on the side stream by the deferred reduction)
             attn_ops.flash_bwd(self.d_c.view(B, T, C), self.qkv[l].view(B, T, 3 * C), self.att[l].view(B, T, C),
                                self.lse[l], s.H, s.H, s.D, b.attn.dropout, seed + l, dqkv=dqkv.view(B, T, 3 * C),
-                               dbias=self.grad(b.qkv.bias) if fused_bias else None)
-            if not fused_bias:
-                self._side_call(dqkv, lambda: fused_ops.colsum(dqkv, self.grad(b.qkv.bias)))
+                               dbias=self.grad(b.qkv.bias))
             torch.mm(dqkv, self._dgrad_w(b.qkv.weight), out=self.d_c)
             self._wgrad(dqkv, self.ln1[l], b.qkv.weight)
             mean, rstd, _, _ = self.stats[l]
