@@ -68,6 +68,11 @@ int64_t skinny_gemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tenso
 void decode_ln_linear(torch::Tensor rin, c10::optional<torch::Tensor> delta, c10::optional<torch::Tensor> dbias,
                       c10::optional<torch::Tensor> rout, torch::Tensor gamma, torch::Tensor beta, double eps,
                       torch::Tensor w, c10::optional<torch::Tensor> bias, torch::Tensor out, int64_t act);
+// decode_linear.hip
+void decode_ln_gemm(torch::Tensor resid, torch::Tensor gamma, torch::Tensor beta, double eps, torch::Tensor w,
+                    c10::optional<torch::Tensor> bias, torch::Tensor out, int64_t act, int64_t flags);
+void decode_gemm_acc(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> bias, torch::Tensor resid,
+                     int64_t flags);
 // gemm_wgrad.hip
 void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad, int64_t tile, int64_t variant);
 // flash_attn.hip
@@ -143,6 +148,12 @@ PYBIND11_MODULE(penroz_kernels, m) {
         pybind11::arg("eps"), pybind11::arg("w"), pybind11::arg("bias"), pybind11::arg("out"), pybind11::arg("act") = 0,
         "decode step: out = act(LN(resid_in + delta + dbias)·wᵀ + bias) for M <= 64 rows, K <= 1024; "
         "resid_out receives the residual sum");
+  m.def("decode_ln_gemm", &decode_ln_gemm, pybind11::arg("resid"), pybind11::arg("gamma"), pybind11::arg("beta"),
+        pybind11::arg("eps"), pybind11::arg("w"), pybind11::arg("bias"), pybind11::arg("out"), pybind11::arg("act") = 0,
+        pybind11::arg("flags") = 0, "batched decode: out = act(LayerNorm(resid)·wᵀ + bias), fp32 resid [M, K <= 1024]");
+  m.def("decode_gemm_acc", &decode_gemm_acc, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("bias"),
+        pybind11::arg("resid"), pybind11::arg("flags") = 0,
+        "batched decode: resid += x·wᵀ + bias (fp32 residual, in place)");
   m.def("wgrad_gemm", &wgrad_gemm, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("grad"),
         pybind11::arg("tile") = 256, pybind11::arg("variant") = 8);
   m.def("flash_attn_fwd", &flash_attn_fwd);

@@ -36,22 +36,38 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){lo, hi}, bf16x2_t));
 }
 
+// Whole-wave reductions (all 64 lanes active; every lane gets the result). Within each 16-lane
+// row the lanes combine through DPP (quad_perm [1,0,3,2], [2,3,0,1], then row_ror 4 and 8: no
+// LDS traffic, a few cycles each), then the four row results are read into scalar registers
+// (v_readlane) and combined in a fixed order. The former __shfl_xor butterfly issued six
+// ds_bpermute round trips through the LDS crossbar per reduction (~100 cycles each, serially
+// dependent): in the decode LayerNorm prologues that alone was microseconds per kernel.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float lane_f32(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+template <typename Op>
+__device__ __forceinline__ float wave_reduce(float v, Op op) {
+  v = op(v, dpp_f32<0xB1>(v));   // quad_perm [1,0,3,2]
+  v = op(v, dpp_f32<0x4E>(v));   // quad_perm [2,3,0,1]
+  v = op(v, dpp_f32<0x124>(v));  // row_ror:4
+  v = op(v, dpp_f32<0x128>(v));  // row_ror:8
+  return op(op(lane_f32(v, 0), lane_f32(v, 16)), op(lane_f32(v, 32), lane_f32(v, 48)));
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  return wave_reduce(v, [](float a, float b) { return a + b; });
 }
 
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  return wave_reduce(v, [](float a, float b) { return fmaxf(a, b); });
 }
 
 __device__ __forceinline__ float wave_min(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
-  return v;
+  return wave_reduce(v, [](float a, float b) { return fminf(a, b); });
 }
 
 // Load 8 consecutive elements (16 B for bf16, 32 B for fp32) as floats.

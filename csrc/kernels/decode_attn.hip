@@ -423,7 +423,8 @@ torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c
   const int Hkv = kc.size(1), cap = kc.size(2);
   TORCH_CHECK(kc.size(0) == B && kc.size(3) == D && H % Hkv == 0 && H / Hkv <= kMaxGroup);
   TORCH_CHECK(S <= cap && q_offset >= 0 && q_offset + Tq <= S, "bad cache extent");
-  TORCH_CHECK(D == 64 || D == 128 || D == 256, "decode attention supports head_dim 64/128/256");
+  TORCH_CHECK(D == 32 || D == 64 || D == 128 || D == 256 || D == 512,
+              "decode attention supports head_dim 32/64/128/256/512");
   const bool quant = kc.scalar_type() == torch::kInt8;
   TORCH_CHECK(!quant || (k_scale.has_value() && v_scale.has_value()), "int8 cache needs scales");
   TORCH_CHECK(quant || kc.scalar_type() == q.scalar_type(), "cache dtype must match q");
@@ -485,7 +486,9 @@ torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c
   }
     if (D == 64) PENROZ_DECODE_G(64)
     else if (D == 128) PENROZ_DECODE_G(128)
-    else PENROZ_DECODE_G(256)  // Gemma
+    else if (D == 256) PENROZ_DECODE_G(256)  // Gemma
+    else if (D == 32) PENROZ_DECODE(32, 0);  // small GPT-style models (any group size)
+    else PENROZ_DECODE(512, 0);              // Gemma-4 full-attention layers (global_head_dim)
 #undef PENROZ_DECODE_G
 #undef PENROZ_DECODE
     if (splits > 1) {

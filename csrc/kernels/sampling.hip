@@ -7,7 +7,8 @@
 //   the per-thread sums finds the owning thread, which walks its own elements.
 // The whole decision stays on the device (no sort, no host round trip per token).
 // sample_reg_kernel (default for V % 8 == 0, V <= 64 Ki) keeps the row in registers; wider rows
-// (greedy / top-k <= 64, V <= 256 Ki) go through the two-stage sample_part_kernel + sample_merge_kernel.
+// and batches of >= 16 rows (greedy / top-k <= 64, V <= 256 Ki) go through the two-stage
+// sample_part_kernel + sample_merge_kernel.
 #include "common.h"
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
@@ -744,7 +745,9 @@ static void launch_sample(const torch::Tensor& logits, const SampleIO& io, doubl
   const bool fits = chunks <= (logits.scalar_type() == torch::kBFloat16 ? 16 : 8);
   const float tt = (float)temperature;
   const int kk = (int)top_k;
-  if (V % 8 == 0 && !fits && logits.scalar_type() != torch::kFloat16 &&
+  // the two-stage form for rows too wide for registers, and for many rows (a batch-64 decode
+  // step: P x B part workgroups fill the chip where B one-row workgroups leave most CUs idle)
+  if (V % 8 == 0 && (!fits || B >= 16) && logits.scalar_type() != torch::kFloat16 &&
       V <= kPartMaxP * kPartN && (temperature == 0.0 || (top_k > 0 && top_k <= kPartK))) {
     const int P = (V + kPartN - 1) / kPartN;
     const bool topk = temperature != 0.0;

@@ -33,8 +33,10 @@ with a cos/sin table computed on the device from ``pos_t`` once per step
 """
 from __future__ import annotations
 
+import gc
 import logging
 import os
+import weakref
 
 import torch
 from torch import Tensor
@@ -69,6 +71,10 @@ FUSED_LN_LINEAR = os.environ.get("PENROZ_DECODE_FUSED", "1") != "0"
 # while the rows are few (batch 1 / 4 / 8: -8 / -10 / -3 %) and loses from 16 rows on (+14 % at 16,
 # +69 % at 64): profiles/decode_fused_rows_r2.log
 FUSED_MAX_ROWS = int(os.environ.get("PENROZ_DECODE_FUSED_MAX_ROWS", "8"))
+# ... above that: the batched block (csrc/kernels/decode_linear.hip) — 5 kernels per block, the
+# fp32 residual updated in place by the proj / fc2 epilogues, LayerNorm recomputed per 16-row
+# block inside the QKV / fc GEMMs; "0": add+LN, GEMM, GELU kernels (8 per block)
+BATCHED_BLOCK = os.environ.get("PENROZ_DECODE_BATCHED", "1") != "0"
 
 
 class _GraphMode:
@@ -170,11 +176,19 @@ class GPTDecodeProgram:
         return (FUSED_LN_LINEAR and 1 <= rows <= min(64, FUSED_MAX_ROWS) and sp.C % 32 == 0 and sp.C <= 1024
                 and sp.gelu_approx in ("none", "tanh") and _ext.available())
 
+    def _batched_ok(self, rows: int) -> bool:
+        sp = self.spec
+        return (BATCHED_BLOCK and rows > FUSED_MAX_ROWS and sp.C % 32 == 0 and sp.C <= 1024
+                and sp.blocks[0].fc.out_features % 32 == 0 and sp.gelu_approx in ("none", "tanh")
+                and _ext.available())
+
     def forward(self, idx: Tensor, cache) -> Tensor:
         """idx [rows, 1] -> logits [rows, V] (bf16); appends this step's K/V at cache.pos_t."""
         sp = self.spec
         rows, C, H, D = idx.shape[0], sp.C, sp.H, sp.D
         x = fused_ops.embedding_fwd(idx, sp.wte.weight, sp.wpe.weight, 0, pos_dev=cache.pos_t)  # fp32 [rows, C]
+        if self._batched_ok(rows):
+            return self._forward_batched(x, rows, cache)
         x2 = torch.empty_like(x)  # the residual stream ping-pongs between x and x2 (no aliasing)
         if self._fused_ok(rows):
             return self._forward_fused(x, x2, rows, cache)
@@ -235,6 +249,32 @@ class GPTDecodeProgram:
             delta, dbias = self._linear(h, blk.fc2, bias=False), fb
         wf, bf, ef = self.lnf
         y, _, _ = norm_ops.add_ln_fwd(x, delta, x2, wf, bf, ef, delta_bias=dbias)
+        return self._linear(y, sp.head)
+
+
+    def _forward_batched(self, x: Tensor, rows: int, cache) -> Tensor:
+        """Per block: [LN1 + QKV GEMM + bias] → decode attention (K/V append fused) → [proj GEMM +
+        bias, added into the fp32 residual in place] → [LN2 + fc GEMM + bias + GELU] → [fc2 GEMM +
+        bias, added into the residual]: 5 kernels instead of 8."""
+        sp = self.spec
+        K = _ext.kernels()
+        C, H, D = sp.C, sp.H, sp.D
+        act = 2 if sp.gelu_approx == "tanh" else 1
+        for l, blk in enumerate(sp.blocks):
+            w1, b1, e1, w2, b2, e2 = self.ln[l]
+            qkv = torch.empty(rows, 3 * C, dtype=torch.bfloat16, device=x.device)
+            K.decode_ln_gemm(x, w1, b1, e1, blk.qkv.weight, blk.qkv.bias, qkv, 0)
+            qkv = qkv.view(rows, 1, 3 * C)
+            q = qkv[:, :, :C].view(rows, 1, H, D)
+            k = qkv[:, :, C:2 * C].view(rows, 1, H, D)
+            v = qkv[:, :, 2 * C:].view(rows, 1, H, D)
+            o = cache._attend_graph(l, q, k, v)
+            K.decode_gemm_acc(o.view(rows, C), blk.proj.weight, blk.proj.bias, x)
+            h = torch.empty(rows, blk.fc.out_features, dtype=torch.bfloat16, device=x.device)
+            K.decode_ln_gemm(x, w2, b2, e2, blk.fc.weight, blk.fc.bias, h, act)
+            K.decode_gemm_acc(h, blk.fc2.weight, blk.fc2.bias, x)
+        wf, bf, ef = self.lnf
+        y, _, _ = norm_ops.ln_fwd(x, wf, bf, ef)
         return self._linear(y, sp.head)
 
 
@@ -361,16 +401,32 @@ def applicable(model) -> bool:
     if p is None or not p.is_cuda:
         return False
     attn = model._find_attention_layers()
-    # RoPE layers rotate with a device-offset table; their decode attention must be the HIP kernel
-    # (head_dim known up front: the HF Gemma builders set it)
-    return bool(attn) and all(a.rope_theta is None or a.head_dim in attn_ops.DECODE_HEAD_DIMS for a in attn)
+    if not attn:
+        return False
+    # the captured step appends K/V and attends inside the decode kernel, so every layer's head_dim
+    # must have one (HF Gemma builders set head_dim; GPT-pattern models derive it from C / H)
+    gpt_d = None
+    if any(a.head_dim is None for a in attn):
+        from penroz.models.executor import GPTExecutor
+        spec = GPTExecutor.match(model)
+        gpt_d = spec.D if spec is not None else None
+    for a in attn:
+        d = a.head_dim if a.head_dim is not None else gpt_d
+        if d is not None and d not in attn_ops.DECODE_HEAD_DIMS:
+            return False
+        if d is None and a.rope_theta is not None:
+            return False
+    return True
 
 
 class GraphDecoder:
     """Static decode state + the captured step graph for ``rows`` sequences."""
 
     def __init__(self, model, rows: int, capacity: int, temperature: float, top_k: int | None):
-        self.model = model
+        # weak: the model caches its decoders (model.__dict__), so a strong reference would make a
+        # cycle that only the cyclic GC frees — and a collection that runs while ANOTHER graph is
+        # being captured destroys this one's graph mid-capture (a hard abort)
+        self._model = weakref.ref(model)
         self.device = next(model.parameters()).device
         self.attn = model._find_attention_layers()
         self.pos_layers = model._find_position_embeddings()
@@ -410,8 +466,9 @@ class GraphDecoder:
             if self.program is not None:
                 last = self.program.forward(self.idx, self.cache)
             else:
-                with gemm_ops.decode_gemms(self.model, max_rows=SKINNY_MAX_ROWS):
-                    acts, _ = self.model(self.idx, skip_softmax=True)
+                model = self._model()
+                with gemm_ops.decode_gemms(model, max_rows=SKINNY_MAX_ROWS):
+                    acts, _ = model(self.idx, skip_softmax=True)
                 logits = acts[-1]
                 last = logits[:, -1, :] if logits.ndim == 3 else logits
             if _ext.available() and last.is_cuda:
@@ -470,8 +527,16 @@ class GraphDecoder:
         torch.cuda.current_stream(self.device).wait_stream(side)
         self._set_state(last_tok, cache_len, start)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self._step()
+        # no cyclic GC inside the capture: a collection there can free objects that own HIP
+        # resources (another decoder's graph, events), which is illegal while capturing
+        gc_on = gc.isenabled()
+        gc.disable()
+        try:
+            with torch.cuda.graph(g):
+                self._step()
+        finally:
+            if gc_on:
+                gc.enable()
         self.graph = g
         self._set_state(last_tok, cache_len, start)  # capture does not execute; state is as before
         log.info(f"captured decode graph: rows={self.rows} block={self.capacity} "

@@ -30,10 +30,22 @@ import torch.nn.functional as F
 from penroz.ops._ext import use_kernels, kernels
 
 # head dims with a native kernel: prefill / training flash attention (flash_attn.hip: 64;
-# flash_attn_gen.hip: 128, 256) and decode attention (csrc/kernels/decode_attn.hip). Other head
-# dims run torch SDPA on the GPU.
+# flash_attn_gen.hip: 128, 256) and decode attention (csrc/kernels/decode_attn.hip: also 32 and
+# Gemma-4's global_head_dim 512). Prefill / training at any other head dim <= 256 runs the next
+# wider kernel on zero-padded heads (see _padded_dim); wider heads (512: Gemma-4 full-attention
+# layers) run torch SDPA for prefill / training — their O accumulator alone (32 query rows × 512
+# fp32 per wave) would fill a wave's whole 512-entry register file — and the native kernel for
+# decode.
 SUPPORTED_HEAD_DIMS = (64, 128, 256)
-DECODE_HEAD_DIMS = (64, 128, 256)
+DECODE_HEAD_DIMS = (32, 64, 128, 256, 512)
+
+
+def _padded_dim(D: int) -> int | None:
+    """The native flash-attention width that serves head_dim ``D`` (None: no native kernel)."""
+    for n in SUPPORTED_HEAD_DIMS:
+        if D <= n:
+            return n
+    return None
 
 
 def reference_causal_attention_qkv(qkv: Tensor, H: int, Hkv: int, D: int, dropout_p: float = 0.0) -> Tensor:
@@ -133,10 +145,55 @@ class _FlashAttnFn(torch.autograd.Function):
         return dqkv.to(in_dtype), None, None, None, None
 
 
+class _PaddedFlashAttnFn(torch.autograd.Function):
+    """Head dim D without its own kernel: every head zero-padded to the kernel width Dp. The
+    scores are unchanged (the padded columns contribute 0 to Q·Kᵀ; the scale stays 1/√D), the
+    output's padded columns are P·0 = 0, and in the backward dQ, dK, dV vanish on them (dO is
+    padded with zeros), so slicing them off is exact."""
+
+    @staticmethod
+    def forward(ctx, qkv, H, Hkv, D, Dp, dropout_p):
+        in_dtype = qkv.dtype
+        B, T, _ = qkv.shape
+        x = torch.zeros(B, T, H + 2 * Hkv, Dp, dtype=torch.bfloat16, device=qkv.device)
+        x[..., :D] = qkv.view(B, T, H + 2 * Hkv, D)
+        x = x.view(B, T, -1)
+        seed = new_seed() if dropout_p > 0 else 0
+        out = torch.empty(B, T, H * Dp, dtype=torch.bfloat16, device=qkv.device)
+        lse = torch.empty(B, H, T, dtype=torch.float32, device=qkv.device)
+        fn = kernels().flash_attn_fwd if Dp == 64 else kernels().flash_attn_gen_fwd
+        fn(x, out, lse, H, Hkv, Dp, 1.0 / math.sqrt(D), float(dropout_p), int(seed))
+        ctx.save_for_backward(x, out, lse)
+        ctx.meta = (H, Hkv, D, Dp, dropout_p, seed, in_dtype)
+        o = out.view(B, T, H, Dp)[..., :D].reshape(B, T, H * D)
+        return o.to(in_dtype)
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, out, lse = ctx.saved_tensors
+        H, Hkv, D, Dp, p, seed, in_dtype = ctx.meta
+        B, T, _ = x.shape
+        dp = torch.zeros(B, T, H, Dp, dtype=torch.bfloat16, device=x.device)
+        dp[..., :D] = dout.view(B, T, H, D)
+        dqkv = torch.empty_like(x)
+        scale = 1.0 / math.sqrt(D)
+        dpv = dp.view(B, T, H * Dp)
+        if Dp == 64:
+            kernels().flash_attn_bwd(dpv, x, out, lse, dqkv, H, Hkv, Dp, scale, float(p), int(seed), None)
+        else:
+            kernels().flash_attn_gen_bwd(dpv, x, out, lse, dqkv, H, Hkv, Dp, scale, float(p), int(seed))
+        g = dqkv.view(B, T, H + 2 * Hkv, Dp)[..., :D].reshape(B, T, (H + 2 * Hkv) * D)
+        return g.to(in_dtype), None, None, None, None, None
+
+
 def causal_attention_qkv(qkv: Tensor, H: int, Hkv: int, D: int, dropout_p: float = 0.0) -> Tensor:
     """Causal attention of a fused-QKV tensor ``[B, T, (H + 2·Hkv)·D]`` -> ``[B, T, H·D]``."""
-    if use_kernels(qkv) and D in SUPPORTED_HEAD_DIMS:
-        return _FlashAttnFn.apply(qkv, H, Hkv, D, dropout_p)
+    if use_kernels(qkv):
+        if D in SUPPORTED_HEAD_DIMS:
+            return _FlashAttnFn.apply(qkv, H, Hkv, D, dropout_p)
+        Dp = _padded_dim(D)
+        if Dp is not None and D % 8 == 0:
+            return _PaddedFlashAttnFn.apply(qkv, H, Hkv, D, Dp, dropout_p)
     return reference_causal_attention_qkv(qkv, H, Hkv, D, dropout_p)
 
 

@@ -82,10 +82,11 @@ class _EagerGraph:
         self.dec._step()
 
 
-def test_decode_program_graph_replay_matches_eager_program(monkeypatch):
+@pytest.mark.parametrize("rows", [3, 40])
+def test_decode_program_graph_replay_matches_eager_program(monkeypatch, rows):
     m = _model(torch.bfloat16)
     assert gd.GPTDecodeProgram.build(m) is not None, "GPT pattern must select the decode program"
-    ctx = torch.randint(0, 256, (3, 5), generator=torch.Generator().manual_seed(2)).tolist()
+    ctx = torch.randint(0, 256, (rows, 5), generator=torch.Generator().manual_seed(2)).tolist()
     graphed = m.generate_batch(ctx, 16, 40, temperature=0.0)  # through the sliding window too
     assert all(d.program is not None and isinstance(d.graph, torch.cuda.CUDAGraph) for d in m._graph_decoders.values())
     m.__dict__.pop("_graph_decoders")
@@ -99,9 +100,12 @@ def test_decode_program_graph_replay_matches_eager_program(monkeypatch):
     assert graphed == eager
 
 
-def test_decode_program_step_matches_module_step():
+@pytest.mark.parametrize("rows", [3, 24, 64])
+def test_decode_program_step_matches_module_step(rows):
+    """One decode-program step vs the module forward: rows 3 run the fused LN-linear path, 24 and
+    64 the batched block (decode_ln_gemm / decode_gemm_acc)."""
     m = _model(torch.bfloat16)
-    rows, cap = 3, 32
+    cap = 32
     dec = gd.GraphDecoder(m, rows, cap, 0.0, None)
     assert dec.program is not None
     idx = torch.randint(0, 256, (rows, 7), device="cuda", generator=torch.Generator("cuda").manual_seed(3))

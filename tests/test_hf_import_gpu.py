@@ -31,7 +31,7 @@ def test_import_then_generate_on_gpu_matches_hf_greedy(workdir, monkeypatch):
     n_new = 40
     r = client.post("/generate/", json={"model_id": "gpu-gpt2", "input": prompt, "block_size": 128,
                                         "max_new_tokens": n_new, "temperature": 0.0})
-    assert r.status_code == 200
+    assert r.status_code == 200, r.text
     got = r.json()["tokens"]
     ref = hf.to("cuda", torch.bfloat16).eval()
     with torch.no_grad():

@@ -435,6 +435,31 @@ def test_flash_gen_fwd_bwd(D, B, T, H, Hkv):
         assert rel < 0.02, f"D={D} {name} relative error {rel}"
 
 
+@pytest.mark.parametrize("D", [32, 80, 96, 160])
+@pytest.mark.parametrize("B,T,H,Hkv,p", [(2, 130, 4, 2, 0.0), (1, 300, 3, 3, 0.0), (2, 64, 4, 1, 0.1)])
+def test_flash_padded_head_dims(D, B, T, H, Hkv, p):
+    """Head dims without their own kernel run the next wider one on zero-padded heads: forward
+    and input gradient vs the fp32 reference (with dropout: finite output and gradient)."""
+    torch.manual_seed(D + T)
+    qkv = _qkv(B, T, H, Hkv, D, scale=1.1).requires_grad_()
+    if p == 0.0:
+        out = A.causal_attention_qkv(qkv, H, Hkv, D)
+        x = qkv.detach().float().requires_grad_()
+        ro, _ = A.reference_attention_lse(x, H, Hkv, D)
+        _close(out, ro, 0.02, 0.01, "out")
+        dout = torch.randn_like(out)
+        out.backward(dout)
+        (ro * dout.float()).sum().backward()
+        rel = (qkv.grad.float() - x.grad).norm() / x.grad.norm()
+        assert rel < 0.02, rel
+    else:
+        torch.manual_seed(5)
+        out = A.causal_attention_qkv(qkv, H, Hkv, D, dropout_p=p)
+        assert torch.isfinite(out.float()).all()
+        out.float().sum().backward()
+        assert torch.isfinite(qkv.grad.float()).all() and qkv.grad.abs().sum() > 0
+
+
 @pytest.mark.parametrize("D", [128, 256])
 def test_flash_gen_rescale_branch(D):
     """One key spiking far above the rest at a late tile forces the online-softmax rescale."""
@@ -482,7 +507,7 @@ def test_flash_gen_dropout_matches_masked_reference(D):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32, torch.float16])
-@pytest.mark.parametrize("D", [64, 128, 256])
+@pytest.mark.parametrize("D", [32, 64, 128, 256, 512])
 @pytest.mark.parametrize("B,H,Hkv,S,Tq", [(2, 4, 4, 300, 1), (1, 8, 2, 1024, 1), (3, 4, 4, 64, 5), (64, 12, 12, 600, 1),
                                           (2, 16, 1, 777, 1), (1, 12, 12, 1, 1)])
 def test_decode_attention(dtype, D, B, H, Hkv, S, Tq):
@@ -682,7 +707,8 @@ def test_transpose_bf16(R, C):
 @pytest.mark.parametrize("dtype,int8", [(torch.bfloat16, False), (torch.float32, False), (torch.float16, False),
                                         (torch.bfloat16, True)])
 @pytest.mark.parametrize("D,H,Hkv,S", [(64, 12, 12, 100), (128, 8, 2, 300), (64, 4, 1, 1), (128, 4, 4, 257),
-                                       (256, 8, 1, 300), (256, 4, 2, 65)])  # Gemma head_dim 256
+                                       (256, 8, 1, 300), (256, 4, 2, 65),  # Gemma head_dim 256
+                                       (32, 4, 4, 77), (512, 8, 1, 130), (512, 16, 2, 33)])  # 32; Gemma-4 global 512
 def test_decode_attention_fused_append(dtype, int8, D, H, Hkv, S):
     """Decode attention that appends this step's K/V itself (slot S-1, read from the fused QKV
     rows) == kv_append followed by decode attention: same output, same cache contents."""
@@ -929,3 +955,46 @@ def test_decode_ln_linear(M, K, N, act, with_delta):
     _close(out, ref, 2e-2, 2e-2, "out")
     if with_delta:
         _close(rout, s, 1e-6, 1e-6, "resid_out")
+
+
+@pytest.mark.parametrize("M,K,N", [(64, 768, 2304), (64, 768, 3072), (37, 1024, 320), (16, 256, 64), (9, 96, 1040)])
+@pytest.mark.parametrize("act", [0, 2])
+def test_decode_ln_gemm(M, K, N, act):
+    """Batched decode LN-GEMM: out = act(LN(resid)·Wᵀ + b) vs fp32 torch; rows past M and the
+    partial last column tile (N % 64 != 0) are never written."""
+    torch.manual_seed(0)
+    rin = torch.randn(M, K, device=DEV) * 3 + 1
+    gamma, beta = torch.randn(K, device=DEV), torch.randn(K, device=DEV)
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, device=DEV).to(torch.bfloat16)
+    big = torch.full((M + 1, N + 16), 7.0, device=DEV, dtype=torch.bfloat16)
+    out = big[:M, :N]  # strided rows; the guard column / row must stay untouched
+    _ext.kernels().decode_ln_gemm(rin, gamma, beta, 1e-5, w, b, out, act)
+    y = F.layer_norm(rin, (K,), gamma, beta, 1e-5).to(torch.bfloat16).float()
+    ref = y @ w.float().t() + b.float()
+    if act:
+        ref = F.gelu(ref.to(torch.bfloat16).float(), approximate="tanh")
+    _close(out, ref, 2e-2, 2e-2, "out")
+    assert (big[M] == 7).all() and (big[:, N:] == 7).all()
+
+
+@pytest.mark.parametrize("M,K,N", [(64, 768, 768), (64, 3072, 768), (23, 160, 48), (1, 32, 16), (50, 4096, 1600)])
+@pytest.mark.parametrize("with_bias", [True, False])
+def test_decode_gemm_acc(M, K, N, with_bias):
+    """Batched decode accumulate-GEMM: resid += x·Wᵀ + b in place (fp32) vs torch; repeated calls
+    accumulate (one owner per element: deterministic)."""
+    torch.manual_seed(1)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, device=DEV).to(torch.bfloat16) if with_bias else None
+    r0 = torch.randn(M, N, device=DEV)
+    r = r0.clone()
+    kk = _ext.kernels()
+    kk.decode_gemm_acc(x, w, b, r)
+    step = x.float() @ w.float().t() + (b.float() if with_bias else 0)
+    _close(r, r0 + step, 1e-3, 1e-4, "resid")
+    r1 = r.clone()
+    kk.decode_gemm_acc(x, w, b, r)
+    kk.decode_gemm_acc(x, w, b, r1)
+    assert torch.equal(r, r1), "not deterministic"
+    _close(r, r0 + 2 * step, 2e-3, 1e-4, "resid x2")
