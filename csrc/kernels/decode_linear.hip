@@ -34,7 +34,7 @@ typedef float dl_f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t dl_u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kDlMaxSteps = 32;  // decode_ln_gemm: K <= 1024 (32 k-steps of 32)
-constexpr int kDlGroup = 16;     // decode_gemm_acc: k-steps whose loads are issued together
+constexpr int kDlGroup = 32;     // decode_gemm_acc: k-steps per wave whose loads are issued together
 
 // (row block, column tile) of a workgroup: the nrb row blocks of column tile ct share
 // blockIdx % 8 (one XCD) for the full groups of 8 tiles; the tail is row-block-major.
@@ -75,6 +75,15 @@ __global__ void __launch_bounds__(256) decode_ln_gemm_kernel(const float* __rest
 #pragma unroll
     for (int s = 0; s < kDlMaxSteps; ++s)
       if (s < steps && live && !(flags & 2)) wa[s] = *reinterpret_cast<const dl_u32x4*>(wp + s * 32);
+  }
+
+  // the epilogue's bias terms, fetched now (not a memory round trip after the MFMAs)
+  const int m = rb * 16 + r16, n = n0 + 4 * (lane >> 4);
+  float bv[4] = {0.f, 0.f, 0.f, 0.f};
+  if (bias && live) {
+    const uint2 u = *reinterpret_cast<const uint2*>(bias + n);
+    bv[0] = __uint_as_float(u.x << 16); bv[1] = __uint_as_float(u.x & 0xffff0000u);
+    bv[2] = __uint_as_float(u.y << 16); bv[3] = __uint_as_float(u.y & 0xffff0000u);
   }
 
   // 2. LayerNorm of rows rb*16 + wid + 4i (fp32 two-pass on the register copy) -> bf16 LDS
@@ -154,12 +163,11 @@ __global__ void __launch_bounds__(256) decode_ln_gemm_kernel(const float* __rest
   }
 
   // 4. bias (+ GELU on the bf16-rounded linear output, the unfused pair's rounding point)
-  const int m = rb * 16 + r16, n = n0 + 4 * (lane >> 4);
   if (m >= M || (flags & 4)) return;
   float y[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    y[r] = acc[r] + (bias ? bf2f(bias[n + r]) : 0.f);
+    y[r] = acc[r] + bv[r];
     if (act) y[r] = gelu_f(bf2f(from_f<bf16>(y[r])), act - 1);
   }
   *reinterpret_cast<uint2*>(out + (size_t)m * o_rs + n) = uint2{pack_bf16x2(y[0], y[1]), pack_bf16x2(y[2], y[3])};
@@ -180,14 +188,29 @@ __global__ void __launch_bounds__(256) decode_gemm_acc_kernel(const bf16* __rest
   const bf16* wp = w + (size_t)(n0 + r16) * K + kq;
   const int mx = rb * 16 + r16;
   const bf16* xp = x + (size_t)(mx < M ? mx : 0) * x_rs + kq;  // rows past M feed unstored outputs
+  // the epilogue's operands (this lane's 4 residual values and bias terms, wave 0 only) are
+  // fetched now, so the tail is LDS reduce + one store instead of two more memory round trips
+  const int m = rb * 16 + r16, n = n0 + 4 * (lane >> 4);
+  const bool owner = wid == 0 && m < M && !(flags & 4);
+  float4_t cur = {0.f, 0.f, 0.f, 0.f}, bv = {0.f, 0.f, 0.f, 0.f};
+  if (owner) {
+    cur = *reinterpret_cast<const float4_t*>(resid + (size_t)m * N + n);
+    if (bias) {
+      const uint2 u = *reinterpret_cast<const uint2*>(bias + n);
+      bv = float4_t{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                    __uint_as_float(u.y & 0xffff0000u)};
+    }
+  }
   dl_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int s = s0; s < s1; s += kDlGroup) {
+  for (int s = s0; s < s1; s += kDlGroup) {  // one pass for K <= 4096: every load in flight at once
     dl_u32x4 wa[kDlGroup], xb[kDlGroup];
 #pragma unroll
     for (int u = 0; u < kDlGroup; ++u) {
-      const size_t ko = (size_t)min(s + u, s1 - 1) * 32;  // clamped: no per-load branch
-      wa[u] = (flags & 2) ? dl_u32x4{0u, 0u, 0u, 0u} : *reinterpret_cast<const dl_u32x4*>(wp + ko);
-      xb[u] = (flags & 1) ? dl_u32x4{0u, 0u, 0u, 0u} : *reinterpret_cast<const dl_u32x4*>(xp + ko);
+      if (s + u < s1) {
+        const size_t ko = (size_t)(s + u) * 32;
+        wa[u] = (flags & 2) ? dl_u32x4{0u, 0u, 0u, 0u} : *reinterpret_cast<const dl_u32x4*>(wp + ko);
+        xb[u] = (flags & 1) ? dl_u32x4{0u, 0u, 0u, 0u} : *reinterpret_cast<const dl_u32x4*>(xp + ko);
+      }
     }
 #pragma unroll
     for (int u = 0; u < kDlGroup; ++u)
@@ -197,14 +220,11 @@ __global__ void __launch_bounds__(256) decode_gemm_acc_kernel(const bf16* __rest
   }
   if (wid) red[(wid - 1) * 64 + lane] = acc;
   __syncthreads();
-  if (wid) return;
+  if (!owner) return;
   acc += red[lane] + red[64 + lane] + red[128 + lane];
-  const int m = rb * 16 + r16, n = n0 + 4 * (lane >> 4);
-  if (m >= M || (flags & 4)) return;
   float4_t* rp = reinterpret_cast<float4_t*>(resid + (size_t)m * N + n);
-  float4_t cur = *rp;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) cur[r] += acc[r] + (bias ? bf2f(bias[n + r]) : 0.f);
+  for (int r = 0; r < 4; ++r) cur[r] += acc[r] + bv[r];
   *rp = cur;
 }
 
@@ -220,8 +240,9 @@ static void dl_check_w(const torch::Tensor& w, int K, const char* who) {
 
 static const bf16* dl_bias(const c10::optional<torch::Tensor>& bias, int N, const char* who) {
   if (!bias.has_value() || !bias->defined()) return nullptr;
-  TORCH_CHECK(bias->scalar_type() == torch::kBFloat16 && bias->is_contiguous() && bias->numel() == N, who,
-              ": bf16 bias [N]");
+  TORCH_CHECK(bias->scalar_type() == torch::kBFloat16 && bias->is_contiguous() && bias->numel() == N &&
+                  reinterpret_cast<uintptr_t>(bias->data_ptr()) % 8 == 0,
+              who, ": bf16 bias [N], 8-B aligned");
   return reinterpret_cast<const bf16*>(bias->data_ptr());
 }
 
