@@ -147,7 +147,7 @@ def parse_args(argv=None):
     tiny = args.model == "tiny"
     args.batch = args.batch or (4 if tiny else 64)
     args.seq = args.seq or (32 if tiny else 1024)
-    args.engine = args.engine or ("fused" if args.device == "cuda" and not MODELS[args.model].get("gemma") else "generic")
+    args.engine = args.engine or ("fused" if args.device == "cuda" else "generic")
     if args.device == "cpu" and args.engine == "fused":
         raise SystemExit("the fused engine needs --device cuda")
     return args

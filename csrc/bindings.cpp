@@ -20,15 +20,25 @@ void gelu_fwd(torch::Tensor x, int64_t approx, torch::Tensor y);
 void gelu_bwd(torch::Tensor dy, torch::Tensor x, int64_t approx, c10::optional<torch::Tensor> dbias, torch::Tensor out);
 void colsum(torch::Tensor x, torch::Tensor out);
 torch::Tensor gated_act_fwd(torch::Tensor g, torch::Tensor u, int64_t kind);
-torch::Tensor gated_act_packed(torch::Tensor gu, int64_t kind);
+torch::Tensor gated_act_packed(torch::Tensor gu, int64_t kind, c10::optional<torch::Tensor> out);
 std::vector<torch::Tensor> gated_act_bwd(torch::Tensor dy, torch::Tensor g, torch::Tensor u, int64_t kind);
+void gated_act_bwd_packed(torch::Tensor dy, torch::Tensor gu, torch::Tensor dgu, int64_t kind);
+// gemma_train.hip
+void gemma_combine_fwd(int64_t mode, torch::Tensor x, c10::optional<torch::Tensor> a, c10::optional<torch::Tensor> w1,
+                       torch::Tensor w2, double eps1, double eps2, c10::optional<torch::Tensor> h_out, torch::Tensor y_out,
+                       c10::optional<torch::Tensor> s_save, c10::optional<torch::Tensor> r1, torch::Tensor r2);
+void gemma_combine_bwd(int64_t mode, torch::Tensor dy, c10::optional<torch::Tensor> dh_in, torch::Tensor h,
+                       c10::optional<torch::Tensor> s_save, c10::optional<torch::Tensor> a_save,
+                       c10::optional<torch::Tensor> r1, torch::Tensor r2, c10::optional<torch::Tensor> w1,
+                       torch::Tensor w2, torch::Tensor dx, c10::optional<torch::Tensor> da,
+                       c10::optional<torch::Tensor> dw1, torch::Tensor dw2, c10::optional<torch::Tensor> dh_save);
 void transpose_bf16(torch::Tensor in, torch::Tensor out);
 void embedding_fwd(torch::Tensor idx, torch::Tensor wte, torch::Tensor wpe, int64_t off, torch::Tensor out,
                    c10::optional<torch::Tensor> off_dev, double dropout_p, int64_t dropout_seed);
 void embedding_bwd(torch::Tensor dout, torch::Tensor idx, torch::Tensor dwte, torch::Tensor dwpe, int64_t off,
                    double dropout_p, int64_t dropout_seed);
 torch::Tensor rope_qkv(torch::Tensor qkv, torch::Tensor cosv, torch::Tensor sinv, int64_t H, int64_t Hkv, int64_t D,
-                       bool inverse);
+                       bool inverse, c10::optional<torch::Tensor> out);
 void kv_quantize(torch::Tensor x, torch::Tensor q, torch::Tensor scale, int64_t pos);
 std::vector<torch::Tensor> tensor_stats(torch::Tensor x, int64_t bins);
 // cross_entropy.hip
@@ -108,8 +118,19 @@ PYBIND11_MODULE(penroz_kernels, m) {
   m.def("gelu_bwd", &gelu_bwd);
   m.def("colsum", &colsum);
   m.def("gated_act_fwd", &gated_act_fwd);
-  m.def("gated_act_packed", &gated_act_packed);
+  m.def("gated_act_packed", &gated_act_packed, pybind11::arg("gu"), pybind11::arg("kind"),
+        pybind11::arg("out") = pybind11::none());
   m.def("gated_act_bwd", &gated_act_bwd);
+  m.def("gated_act_bwd_packed", &gated_act_bwd_packed, "dgu [N, 2I] from dy [N, I] and the packed gu [N, 2I]");
+  m.def("gemma_combine_fwd", &gemma_combine_fwd, pybind11::arg("mode"), pybind11::arg("x"), pybind11::arg("a"),
+        pybind11::arg("w1"), pybind11::arg("w2"), pybind11::arg("eps1"), pybind11::arg("eps2"), pybind11::arg("h_out"),
+        pybind11::arg("y_out"), pybind11::arg("s_save"), pybind11::arg("r1"), pybind11::arg("r2"),
+        "Gemma residual combine + post-norm + next RMSNorm (modes 0: Gemma3+, 1: Gemma2, 2: Gemma1, 3: norm only)");
+  m.def("gemma_combine_bwd", &gemma_combine_bwd, pybind11::arg("mode"), pybind11::arg("dy"), pybind11::arg("dh_in"),
+        pybind11::arg("h"), pybind11::arg("s_save"), pybind11::arg("a_save"), pybind11::arg("r1"), pybind11::arg("r2"),
+        pybind11::arg("w1"), pybind11::arg("w2"), pybind11::arg("dx"), pybind11::arg("da"), pybind11::arg("dw1"),
+        pybind11::arg("dw2"), pybind11::arg("dh_save") = pybind11::none(),
+        "backward of gemma_combine_fwd (dw1 / dw2 accumulated; dh_save: dL/dh for diagnostics)");
   m.def("transpose_bf16", &transpose_bf16, "out [C, R] = in [R, C]^T (bf16, dims % 64 == 0)");
   m.def("embedding_fwd", &embedding_fwd, pybind11::arg("idx"), pybind11::arg("wte"), pybind11::arg("wpe"),
         pybind11::arg("off"), pybind11::arg("out"), pybind11::arg("off_dev") = pybind11::none(),
@@ -117,7 +138,8 @@ PYBIND11_MODULE(penroz_kernels, m) {
   m.def("embedding_bwd", &embedding_bwd, pybind11::arg("dout"), pybind11::arg("idx"), pybind11::arg("dwte"),
         pybind11::arg("dwpe"), pybind11::arg("off"), pybind11::arg("dropout_p") = 0.0,
         pybind11::arg("dropout_seed") = 0);
-  m.def("rope_qkv", &rope_qkv);
+  m.def("rope_qkv", &rope_qkv, pybind11::arg("qkv"), pybind11::arg("cosv"), pybind11::arg("sinv"), pybind11::arg("H"),
+        pybind11::arg("Hkv"), pybind11::arg("D"), pybind11::arg("inverse"), pybind11::arg("out") = pybind11::none());
   m.def("kv_quantize", &kv_quantize);
   m.def("tensor_stats", &tensor_stats);
   m.def("cross_entropy_fwd_bwd", &cross_entropy_fwd_bwd, pybind11::arg("logits"), pybind11::arg("targets"),

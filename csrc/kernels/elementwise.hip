@@ -138,6 +138,28 @@ __global__ void __launch_bounds__(256) gated_bwd_kernel(const T* __restrict__ dy
   }
 }
 
+// packed form of the backward: gu = [gate | up] per row (I8 chunks of 8 each), dgu likewise —
+// the layout one GEMM over the concatenated [gate; up] weight consumes (fused Gemma executor)
+template <typename T>
+__global__ void __launch_bounds__(256) gated_bwd_packed_kernel(const T* __restrict__ dy, const T* __restrict__ gu,
+                                                               T* __restrict__ dgu, int64_t n8, int I8, int kind) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / I8, c = i - r * I8;
+    const int64_t go = 8 * (r * 2 * I8 + c), uo = go + 8 * (int64_t)I8;
+    float d[8], gv[8], uv[8], o1[8], o2[8];
+    Vec8<T>::load(dy + 8 * i, d);
+    Vec8<T>::load(gu + go, gv);
+    Vec8<T>::load(gu + uo, uv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      o1[k] = d[k] * uv[k] * act_grad_f(gv[k], kind);
+      o2[k] = d[k] * act_f(gv[k], kind);
+    }
+    Vec8<T>::store(dgu + go, o1);
+    Vec8<T>::store(dgu + uo, o2);
+  }
+}
+
 // ------------------------------------------------------------------------------ embedding
 // out[n, :] = wte[idx[n], :] + wpe[off + n % T, :]   (one wave per token row, 16-B lanes)
 template <typename TW>
@@ -496,11 +518,19 @@ torch::Tensor gated_act_fwd(torch::Tensor g, torch::Tensor u, int64_t kind) {
   return y;
 }
 
-torch::Tensor gated_act_packed(torch::Tensor gu, int64_t kind) {
+torch::Tensor gated_act_packed(torch::Tensor gu, int64_t kind, c10::optional<torch::Tensor> out) {
   TORCH_CHECK(gu.is_cuda() && gu.is_contiguous() && gu.dim() == 2 && gu.size(1) % 16 == 0, "gu: [N, 2I], I % 8 == 0");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(gu.data_ptr()) % 16 == 0);
   const int64_t N = gu.size(0), I = gu.size(1) / 2;
-  auto y = torch::empty({N, I}, gu.options());
+  torch::Tensor y;
+  if (out.has_value() && out->defined()) {
+    y = *out;
+    TORCH_CHECK(y.is_contiguous() && y.numel() == N * I && y.scalar_type() == gu.scalar_type() &&
+                    reinterpret_cast<uintptr_t>(y.data_ptr()) % 16 == 0,
+                "gated_act_packed: out must be a contiguous 16-B aligned [N, I] tensor of gu's dtype");
+  } else {
+    y = torch::empty({N, I}, gu.options());
+  }
   const int64_t n8 = N * I / 8;
   if (n8 == 0) return y;
   auto stream = at::hip::getCurrentHIPStream();
@@ -524,6 +554,23 @@ std::vector<torch::Tensor> gated_act_bwd(torch::Tensor dy, torch::Tensor g, torc
                        reinterpret_cast<const T*>(u.data_ptr()), reinterpret_cast<T*>(dg.data_ptr()),
                        reinterpret_cast<T*>(du.data_ptr()), n8, (int)kind))
   return {dg, du};
+}
+
+// dgu [N, 2I] (packed [d gate | d up]) from dy [N, I] and the packed forward input gu [N, 2I]
+void gated_act_bwd_packed(torch::Tensor dy, torch::Tensor gu, torch::Tensor dgu, int64_t kind) {
+  check_vec8(dy);
+  check_vec8(gu);
+  check_vec8(dgu);
+  TORCH_CHECK(gu.dim() == 2 && gu.size(1) % 16 == 0 && dy.dim() == 2 && dy.size(0) == gu.size(0) &&
+                  2 * dy.size(1) == gu.size(1) && dgu.sizes() == gu.sizes() && dy.scalar_type() == gu.scalar_type() &&
+                  dgu.scalar_type() == gu.scalar_type(),
+              "gated_act_bwd_packed: dy [N, I], gu / dgu [N, 2I], I % 8 == 0, one dtype");
+  const int64_t I = dy.size(1), n8 = dy.numel() / 8;
+  auto stream = at::hip::getCurrentHIPStream();
+  FOR_FLOAT_TYPES(gu.scalar_type(), T,
+    hipLaunchKernelGGL(gated_bwd_packed_kernel<T>, dim3(grid_for(n8)), dim3(256), 0, stream,
+                       reinterpret_cast<const T*>(dy.data_ptr()), reinterpret_cast<const T*>(gu.data_ptr()),
+                       reinterpret_cast<T*>(dgu.data_ptr()), n8, (int)(I / 8), (int)kind))
 }
 
 void embedding_fwd(torch::Tensor idx, torch::Tensor wte, torch::Tensor wpe, int64_t off, torch::Tensor out,
@@ -580,12 +627,22 @@ void embedding_bwd(torch::Tensor dout, torch::Tensor idx, torch::Tensor dwte, to
                      B, T, C, (int)off, (uint64_t)dropout_seed, (float)dropout_p);
 }
 
+// out (optional): a preallocated contiguous tensor of qkv's shape and dtype (not aliasing qkv)
 torch::Tensor rope_qkv(torch::Tensor qkv, torch::Tensor cosv, torch::Tensor sinv, int64_t H, int64_t Hkv, int64_t D,
-                       bool inverse) {
+                       bool inverse, c10::optional<torch::Tensor> out_opt) {
   TORCH_CHECK(qkv.is_cuda() && qkv.is_contiguous() && qkv.dim() == 3);
   const int64_t B = qkv.size(0), T = qkv.size(1);
   TORCH_CHECK(qkv.size(2) == (H + 2 * Hkv) * D && cosv.size(0) == T && cosv.size(1) == D / 2);
-  auto out = torch::empty_like(qkv);
+  torch::Tensor out;
+  if (out_opt.has_value() && out_opt->defined()) {
+    out = *out_opt;
+    TORCH_CHECK(out.is_contiguous() && out.numel() == qkv.numel() && out.scalar_type() == qkv.scalar_type() &&
+                    out.data_ptr() != qkv.data_ptr() && reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
+                "rope_qkv: out must be a contiguous 16-B aligned tensor like qkv, not aliasing it");
+    out = out.view(qkv.sizes());
+  } else {
+    out = torch::empty_like(qkv);
+  }
   const int64_t rows = B * T;
   auto stream = at::hip::getCurrentHIPStream();
   const bool vec = D % 16 == 0 && cosv.is_contiguous() && sinv.is_contiguous() &&

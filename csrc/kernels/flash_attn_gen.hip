@@ -251,9 +251,16 @@ __global__ void __launch_bounds__(128, 1)
   constexpr int BK = 64, QS = 32;
   constexpr int TILE = QS * 128 * NP;          // one 32-row slice of Q (or dO)
   constexpr int STAGE = 2 * TILE + 2 * 256;    // Q | dO | LSE[64] | δ[64] (64-lane DMA pieces)
-  // D = 256: K and V fragments (128 registers) would not fit beside the dKᵀ / dVᵀ accumulators
-  // (256): the workgroup's 64 keys of K and V sit in LDS and are read per slice instead
-  constexpr bool KVLDS = D >= 256;
+  // D = 256: the K / V fragments (128 registers) and the full dKᵀ / dVᵀ accumulators (256) do
+  // not fit one wave's register file together. Each workgroup accumulates dK / dV for HALF of D
+  // (grid z = the half) — S and dP, which need all of D, are computed by both halves — so K / V
+  // stay in registers: no per-slice K / V LDS reads, and 65 KB of LDS per workgroup lets two
+  // workgroups (all four SIMDs) share a CU. (Keeping K / V in LDS for one workgroup per CU left
+  // two SIMDs idle, spilled 72 registers and was LDS-bandwidth-bound at 87 TF.)
+  constexpr bool DSPLIT = D >= 256;
+  constexpr int NDH = DSPLIT ? ND / 2 : ND;  // dKᵀ / dVᵀ column blocks of 32 owned here
+  const int dh0 = DSPLIT ? (int)blockIdx.z * NDH : 0;
+  constexpr bool KVLDS = false;
   constexpr int KVT = BK * 128 * NP;           // 64 key rows
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + (KVLDS ? 2 * KVT : 16)];
   int kb, bhx;
@@ -298,9 +305,9 @@ __global__ void __launch_bounds__(128, 1)
     if constexpr (KVLDS) return row_frag(panel(KVs + KVT, BK, s >> 2), 32 * w, s & 3, lane);
     else return vf[s];
   };
-  f32x16 dk[ND], dv[ND];
+  f32x16 dk[NDH], dv[NDH];
 #pragma unroll
-  for (int dh = 0; dh < ND; ++dh)
+  for (int dh = 0; dh < NDH; ++dh)
 #pragma unroll
     for (int i = 0; i < 16; ++i) dk[dh][i] = dv[dh][i] = 0.f;
 
@@ -384,10 +391,11 @@ __global__ void __launch_bounds__(128, 1)
       for (int ss = 0; ss < 2; ++ss) {
         const uint4 pf = acc_frag(sp, ss), sf = acc_frag(dp, ss);
 #pragma unroll
-        for (int dh = 0; dh < ND; ++dh) {
-          dv[dh] = mfma32(tr_frag(panel(Dt, QS, dh >> 1), 16 * ss, 32 * (dh & 1), lane), pf, dv[dh]);
-          dk[dh] = mfma32(tr_frag(panel(Qt, QS, dh >> 1), 16 * ss, 32 * (dh & 1), lane), sf, dk[dh]);
-          if (dh & 1) d_fence<D>();
+        for (int j = 0; j < NDH; ++j) {
+          const int dh = dh0 + j;
+          dv[j] = mfma32(tr_frag(panel(Dt, QS, dh >> 1), 16 * ss, 32 * (dh & 1), lane), pf, dv[j]);
+          dk[j] = mfma32(tr_frag(panel(Qt, QS, dh >> 1), 16 * ss, 32 * (dh & 1), lane), sf, dk[j]);
+          if (j & 1) d_fence<D>();
         }
       }
     }
@@ -398,26 +406,26 @@ __global__ void __launch_bounds__(128, 1)
     const int Bn = gridDim.y / (Hkv * GS);
     float* prow = part + ((size_t)gi * Bn * T + (size_t)b * T + key) * (2 * Hkv * D) + (size_t)hk * D;
 #pragma unroll
-    for (int dh = 0; dh < ND; ++dh)
+    for (int j = 0; j < NDH; ++j)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int d = 32 * dh + 8 * g + 4 * hh;
-        *reinterpret_cast<float4*>(prow + d) = float4{dk[dh][4 * g] * scale, dk[dh][4 * g + 1] * scale,
-                                                      dk[dh][4 * g + 2] * scale, dk[dh][4 * g + 3] * scale};
+        const int d = 32 * (dh0 + j) + 8 * g + 4 * hh;
+        *reinterpret_cast<float4*>(prow + d) = float4{dk[j][4 * g] * scale, dk[j][4 * g + 1] * scale,
+                                                      dk[j][4 * g + 2] * scale, dk[j][4 * g + 3] * scale};
         *reinterpret_cast<float4*>(prow + (size_t)Hkv * D + d) =
-            float4{dv[dh][4 * g], dv[dh][4 * g + 1], dv[dh][4 * g + 2], dv[dh][4 * g + 3]};
+            float4{dv[j][4 * g], dv[j][4 * g + 1], dv[j][4 * g + 2], dv[j][4 * g + 3]};
       }
   } else if (key < T) {
     bf16* dkrow = dqkv + ((size_t)b * T + key) * RS + (size_t)(H + hk) * D;
     bf16* dvrow = dqkv + ((size_t)b * T + key) * RS + (size_t)(H + Hkv + hk) * D;
 #pragma unroll
-    for (int dh = 0; dh < ND; ++dh)
+    for (int j = 0; j < NDH; ++j)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int d = 32 * dh + 8 * g + 4 * hh;
-        store4(dkrow + d, dk[dh][4 * g] * scale, dk[dh][4 * g + 1] * scale, dk[dh][4 * g + 2] * scale,
-               dk[dh][4 * g + 3] * scale);
-        store4(dvrow + d, dv[dh][4 * g], dv[dh][4 * g + 1], dv[dh][4 * g + 2], dv[dh][4 * g + 3]);
+        const int d = 32 * (dh0 + j) + 8 * g + 4 * hh;
+        store4(dkrow + d, dk[j][4 * g] * scale, dk[j][4 * g + 1] * scale, dk[j][4 * g + 2] * scale,
+               dk[j][4 * g + 3] * scale);
+        store4(dvrow + d, dv[j][4 * g], dv[j][4 * g + 1], dv[j][4 * g + 2], dv[j][4 * g + 3]);
       }
   }
 }
@@ -618,7 +626,7 @@ void flash_attn_gen_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out
   const bool split = G > 1 && (int64_t)B * Hkv * nkb < 1024;
   torch::Tensor part;
   if (split) part = torch::empty({(int64_t)G * B * T, 2 * Hkv * D}, qkv.options().dtype(torch::kFloat32));
-  dim3 gkv(nkb, B * Hkv * (split ? G : 1)), gq((T + 63) / 64, B * H);
+  dim3 gkv(nkb, B * Hkv * (split ? G : 1), D >= 256 ? 2 : 1), gq((T + 63) / 64, B * H);  // z: the D halves
   FA_GEN_DISPATCH(D, p_drop > 0.0, {
     hipLaunchKernelGGL((fa_gen_bwd_pre_kernel<DD>), dim3(((int64_t)rows * (DD / 8) + 255) / 256), dim3(256), 0,
                        stream, d, reinterpret_cast<const bf16*>(out.data_ptr()), delta.data_ptr<float>(), B, T,

@@ -8,9 +8,10 @@ delete / from_huggingface``, ``forward(input, target, skip_softmax) -> (activati
 ``train_model_on_device`` (distributed worker entry) and ``train_model``.
 
 Training engines (``PENROZ_ENGINE``, default ``auto``):
-  * ``fused`` — GPT-2-pattern models on GPU lower to :class:`penroz.models.executor.GPTExecutor`
-    (hand-written HIP kernels + hipBLASLt GEMMs, explicit backward, flat fp32 master/grad
-    buffers, fused AdamW, bucketed RCCL all-reduce overlapped with backward);
+  * ``fused`` — GPT-2-pattern models on GPU lower to :class:`penroz.models.executor.GPTExecutor`,
+    Gemma-pattern models to :class:`penroz.models.gemma_executor.GemmaExecutor` (hand-written HIP
+    kernels + hipBLASLt GEMMs, explicit backward, flat fp32 master/grad buffers, fused AdamW,
+    bucketed RCCL all-reduce overlapped with backward);
   * ``generic`` — any layer list: module forward (HIP kernels through autograd), bf16 autocast
     on GPU, our bucketed reducer for DDP;
   * ``reference`` — stock PyTorch eager + autocast + ``torch.nn.parallel.DDP`` + foreach AdamW
@@ -559,16 +560,26 @@ class NeuralNetworkModel(nn.Module):
         if self.amp_dtype(device) == torch.float16:
             return "reference" if eng == "reference" else "generic"  # the fused executor is bf16-only
         if eng == "auto":
-            from penroz.models.executor import GPTExecutor
-            return "fused" if device.type == "cuda" and GPTExecutor.match(self) is not None else "generic"
+            return "fused" if device.type == "cuda" and self._executor_class() is not None else "generic"
         return eng
+
+    def _executor_class(self):
+        """The fused executor this layer list lowers to (GPT-2 or Gemma pattern), or None."""
+        from penroz.models.executor import GPTExecutor
+        from penroz.models.gemma_executor import GemmaExecutor
+        for cls in (GPTExecutor, GemmaExecutor):
+            if cls.match(self) is not None:
+                return cls
+        return None
 
     def _get_executor(self, device):
         if device.type != "cuda" or self._engine(device) != "fused":
             return None
-        from penroz.models.executor import GPTExecutor
         if self._executor is None or self._executor.device != device:
-            self._executor = GPTExecutor(self, device)
+            cls = self._executor_class()
+            if cls is None:
+                raise ValueError("PENROZ_ENGINE=fused needs a GPT-2 or Gemma pattern layer list")
+            self._executor = cls(self, device)
         return self._executor
 
     def train_model(self, dataset_id: str, shard: int, epochs: int, batch_size: int, block_size: int,

@@ -54,3 +54,24 @@ def test_head_chunk_policy(monkeypatch):
     assert _head_chunk_rows(65536, 50304) == 8192
     monkeypatch.setenv("PENROZ_HEAD_CHUNK", "0")
     assert _head_chunk_rows(4 * 65536, 50304) == 4 * 65536
+
+
+def test_gemma_executor_pattern_match_modes():
+    """The fused Gemma executor's pattern match (CPU): Gemma 3 / 2 / 1 layer lists map to the
+    combine modes 0 / 1 / 2; a tied head or a GPT layer list does not match."""
+    from types import SimpleNamespace
+    from penroz.models.gemma_executor import GemmaExecutor
+    from penroz.models.mapper import Mapper
+    from penroz.models.model import NeuralNetworkModel
+    for mt, mode in (("gemma3_text", 0), ("gemma2", 1), ("gemma", 2)):
+        cfg = SimpleNamespace(model_type=mt, vocab_size=64, hidden_size=64, intermediate_size=128, num_hidden_layers=2,
+                              num_attention_heads=2, num_key_value_heads=1, head_dim=64, rms_norm_eps=1e-6,
+                              rope_theta=10000.0, attention_dropout=0.0, hidden_activation="gelu_pytorch_tanh")
+        m = NeuralNetworkModel("g", Mapper(Mapper.from_hf_config(cfg), {"adamw": {"lr": 1e-3}}))
+        spec = GemmaExecutor.match(m)
+        assert spec is not None and spec.mode == mode and spec.F == 128 and spec.act == 1
+        m.layers[-2].weight = m.layers[0].weight  # tied head: not lowered
+        assert GemmaExecutor.match(m) is None
+    import bench
+    g = NeuralNetworkModel("t", Mapper(bench.gpt2_layers(V=64, C=64, L=1, H=1, P=32), {"adamw": {"lr": 1e-3}}))
+    assert GemmaExecutor.match(g) is None
