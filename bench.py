@@ -275,6 +275,15 @@ def _first_contact(args, device, world: int, rccl_log) -> dict:
         else:
             os.environ["PENROZ_COMM"] = choice["transport"]
         out["choice"] = choice
+        # the gradient bucket size from the same table (RCCL only: the gloo plumbing config keeps
+        # the reference DDP's 25 MB, whose TCP transfers the sweep's sizes do not model)
+        if device.type == "cuda":
+            bucket = commtune.choose_bucket(rows, "native" if choice["transport"] == "native" else "c10d")
+            if "PENROZ_BUCKET_MB" in os.environ:
+                bucket = {"bucket_mb": float(os.environ["PENROZ_BUCKET_MB"]), "rule": "PENROZ_BUCKET_MB set"}
+            elif bucket is not None:
+                os.environ["PENROZ_BUCKET_MB"] = str(bucket["bucket_mb"])
+            out["bucket"] = bucket
     out["rccl"] = commtune.rccl_channels(rccl_log)
     return out
 

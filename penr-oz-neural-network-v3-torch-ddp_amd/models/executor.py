@@ -213,6 +213,7 @@ class GPTExecutor:
         self._reduce_pending = False
         import os
         self._overlap_opt = os.environ.get("PENROZ_OVERLAP_OPT", "1") != "0"
+        self._opt_apply, self._opt_done = None, False
         self._side_init()
 
     def _param_order(self):
@@ -482,6 +483,19 @@ class GPTExecutor:
         self._captured = None
 
     def _segment_done(self, seg_index: int, sync: bool):
+        if self._opt_apply is not None and sync:
+            # optimizer inside the backward: this segment's gradients are final once the side
+            # stream (its weight gradients, deferred dγ / bias reductions) has caught up with the
+            # main stream (its other gradients); nothing later in this backward reads its weights
+            s, e = self.segments[seg_index]
+            if getattr(self, "_side", None) is None:
+                self._opt_apply(s, e)
+                return
+            main = torch.cuda.current_stream(self.device)
+            with torch.cuda.stream(self._side):
+                self._side.wait_stream(main)
+                self._opt_apply(s, e)
+            return
         if self.reducer is None or not sync:
             return
         bkt = self._seg_bucket[seg_index]
@@ -552,10 +566,26 @@ class GPTExecutor:
 
     @torch.no_grad()
     def train_micro_step(self, idx: Tensor, targets: Tensor, scale: float, sync: bool = True,
-                         capture: bool = False) -> Tensor:
+                         capture: bool = False, fuse_optimizer: bool = False) -> Tensor:
         """Forward + backward of one micro-batch; gradients accumulate into the flat buffer.
-        Returns the (scaled) mean loss as a device scalar."""
-        return self._train_micro_step(idx, targets, scale, sync, capture)
+        Returns the (scaled) mean loss as a device scalar.
+
+        ``fuse_optimizer`` (the last micro-step of a step whose ``optimizer_step`` follows, single
+        process): the fused AdamW updates each parameter segment inside the backward, on the side
+        stream, as soon as that segment's gradients are final — the optimizer pass overlaps the
+        rest of the backward instead of running after it (``optimizer_step`` then has nothing left
+        to do). ``PENROZ_OPT_IN_BWD=0`` keeps the separate step."""
+        import os
+        self._opt_apply = None
+        if (fuse_optimizer and sync and not capture and self.reducer is None and self._opt_flat
+                and os.environ.get("PENROZ_OPT_IN_BWD", "1") != "0"):
+            self._opt_apply = self.model.optimizer.begin_flat_ranges()
+        try:
+            loss = self._train_micro_step(idx, targets, scale, sync, capture)
+        finally:
+            self._opt_done = self._opt_apply is not None
+            self._opt_apply = None
+        return loss
 
     def _train_micro_step(self, idx: Tensor, targets: Tensor, scale: float, sync: bool, capture: bool) -> Tensor:
         s = self.spec
@@ -675,6 +705,9 @@ class GPTExecutor:
 
     def optimizer_step(self):
         opt = self.model.optimizer
+        if getattr(self, "_opt_done", False):  # applied segment by segment inside the backward
+            self._opt_done = False
+            return
         with trace_range("optimizer"):
             if self._reduce_pending:
                 self._reduce_pending = False

@@ -172,6 +172,7 @@ class GemmaExecutor(GPTExecutor):
         self._reduce_pending = False
         import os
         self._overlap_opt = os.environ.get("PENROZ_OVERLAP_OPT", "1") != "0"
+        self._opt_apply, self._opt_done = None, False
         self._side_init()
         self._rope_tables = {}
 

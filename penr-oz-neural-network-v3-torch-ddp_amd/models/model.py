@@ -773,7 +773,9 @@ class _FusedRunner:
         self.exec.zero_grad()
 
     def micro_step(self, x, y, scale, first, last, capture):
-        return self.exec.train_micro_step(x, y, scale, sync=last, capture=capture)
+        # the last micro-step's backward may apply the optimizer per parameter segment (step()
+        # always follows it in the training loop and the bench)
+        return self.exec.train_micro_step(x, y, scale, sync=last, capture=capture, fuse_optimizer=last)
 
     def step(self):
         self.exec.optimizer_step()

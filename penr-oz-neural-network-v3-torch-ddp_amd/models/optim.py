@@ -132,6 +132,29 @@ class _FusedMixin:
             fn(f["param"][s:e], f["grad"][s:e], f["m"][s:e], f["v"][s:e], sh[s:e] if sh is not None else None,
                lr, b1, b2, eps, wd, step, grad_scale, maximize)
 
+    def begin_flat_ranges(self, grad_scale: float = 1.0):
+        """Start a flat step whose ranges are applied later, one call per range, e.g. each
+        parameter segment as soon as its gradients are final inside the backward. Returns
+        ``apply(s, e)`` or None when the flat path does not apply. The step counter advances now,
+        once; the caller must cover the flat buffer exactly once before the next step."""
+        if not (len(self.param_groups) == 1 and self._flat is not None
+                and {id(p) for p in self.param_groups[0]["params"]} == self._flat["ids"]):
+            return None
+        f, group = self._flat, self.param_groups[0]
+        lr, b1, b2, eps, wd, maximize = self._hyper(group)
+        step = None
+        for p in f["params"]:
+            st = self.state[p]
+            st["step"] += 1
+            step = int(st["step"].item()) if step is None else step
+        fn = fused_ops.adamw_step if self._decoupled else fused_ops.adam_step
+        sh = f["shadow"]
+
+        def apply(s: int, e: int):
+            fn(f["param"][s:e], f["grad"][s:e], f["m"][s:e], f["v"][s:e], sh[s:e] if sh is not None else None,
+               lr, b1, b2, eps, wd, step, grad_scale, maximize)
+        return apply
+
     def flat_step_ranges(self, ranges, grad_scale: float = 1.0) -> bool:
         """Flat step applied range by range (``ranges`` must cover the flat buffer exactly once);
         False (nothing done) when the flat path does not apply."""

@@ -185,3 +185,19 @@ def choose(rows: list[dict], bucket_mb: float, margin: float = 1.03) -> dict:
         return {"transport": "native", "reason": f"native {n['busbw_GBps']} vs c10d {c['busbw_GBps']} GB/s",
                 "at_mb": size}
     return {"transport": "c10d", "reason": f"native {n['busbw_GBps']} vs c10d {c['busbw_GBps']} GB/s", "at_mb": size}
+
+
+def choose_bucket(rows: list[dict], transport: str, frac: float = 0.9) -> dict | None:
+    """Gradient bucket size for ``transport``: the SMALLEST swept fp32 size whose bus bandwidth
+    is within ``frac`` of the best one. On point-to-point xGMI a ring all-reduce is per-link bound,
+    so past the size where the links saturate a bigger bucket only starts its collective later in
+    the backward (and leaves more bytes exposed after it); below it, per-call latency dominates.
+    The sweep's timings are MAX-reduced over ranks, so every rank picks the same size (the bucket
+    plans must match). None when nothing correct was swept for ``transport``."""
+    fp = [r for r in rows if r["wire"] == "fp32" and r["transport"] == transport and r["ok"]]
+    if not fp:
+        return None
+    best = max(r["busbw_GBps"] for r in fp)
+    pick = min((r for r in fp if r["busbw_GBps"] >= frac * best), key=lambda r: r["bucket_mb"])
+    return {"bucket_mb": pick["bucket_mb"], "busbw_GBps": pick["busbw_GBps"], "best_busbw_GBps": best,
+            "rule": f"smallest size within {frac:.0%} of the best bus bandwidth"}

@@ -43,6 +43,11 @@ GLOO_BUCKET_MB = float(os.environ.get("PENROZ_BUCKET_MB", "25"))
 
 
 def default_bucket_mb(backend: str | None) -> float:
+    """PENROZ_BUCKET_MB read at call time (the multi-GPU bench sets it from its first-contact
+    all-reduce sweep, parallel/commtune.py: choose_bucket), else the per-backend default."""
+    env = os.environ.get("PENROZ_BUCKET_MB")
+    if env is not None:
+        return float(env)
     return GLOO_BUCKET_MB if backend == "gloo" else DEFAULT_BUCKET_MB
 WIRE_DTYPES = {"fp32": None, "bf16": torch.bfloat16}
 

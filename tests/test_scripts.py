@@ -59,12 +59,13 @@ def test_bench_cli_help():
         assert flag in r.stdout
 
 
-def test_bench_gemma_config_uses_generic_engine_and_gemma_layers():
+def test_bench_gemma_config_uses_fused_engine_and_gemma_layers():
+    """The Gemma-3 1B bench config runs the fused engine (lowered to the Gemma executor)."""
     import sys
     sys.path.insert(0, ROOT)
     import bench
     args = bench.parse_args(["--model", "gemma3-1b"])
-    assert args.engine == "generic" and args.batch == 64 and args.seq == 1024
+    assert args.engine == "fused" and args.batch == 64 and args.seq == 1024
     assert bench.parse_args([]).engine == "fused"
     layers = bench.gemma3_1b_layers(2)
     names = [next(iter(l)) for l in layers]
@@ -130,6 +131,24 @@ def test_comm_choice_rules():
     # nearest swept size to the reducer's bucket decides
     rows = [row("c10d", 100, mb=32), row("native", 90, mb=32), row("c10d", 100, mb=128), row("native", 150, mb=128)]
     assert choose(rows, 100)["transport"] == "native" and choose(rows, 40)["transport"] == "c10d"
+
+
+def test_comm_bucket_choice_rule(monkeypatch):
+    """Smallest swept bucket within 90 % of the best bus bandwidth of the chosen transport; wrong
+    sums and other transports / wires are ignored; the reducer reads the chosen size at call time."""
+    from penroz.parallel.commtune import choose_bucket
+    from penroz.parallel import reducer as R
+    row = lambda tr, mb, bw, ok=True, wire="fp32": {"transport": tr, "wire": wire, "bucket_mb": mb,
+                                                     "busbw_GBps": bw, "ok": ok}
+    rows = [row("c10d", 16, 60), row("c10d", 32, 88), row("c10d", 64, 95), row("c10d", 128, 100),
+            row("c10d", 256, 99), row("native", 16, 150, ok=False), row("c10d", 16, 200, wire="bf16")]
+    c = choose_bucket(rows, "c10d")
+    assert c["bucket_mb"] == 64 and c["best_busbw_GBps"] == 100
+    assert choose_bucket(rows, "native") is None
+    monkeypatch.setenv("PENROZ_BUCKET_MB", "32")
+    assert R.default_bucket_mb("nccl") == 32.0 and R.default_bucket_mb("gloo") == 32.0
+    monkeypatch.delenv("PENROZ_BUCKET_MB")
+    assert R.default_bucket_mb("gloo") == R.GLOO_BUCKET_MB and R.default_bucket_mb("nccl") == R.DEFAULT_BUCKET_MB
 
 
 def test_init_group_passes_timeout(monkeypatch):
