@@ -198,3 +198,51 @@ def test_bf16_params_train_and_keep_state_dict():
         _, c_mod = m(x, y, skip_softmax=True)
         c_ex = ex.eval_loss(x, y)
     assert abs(c_mod.item() - c_ex.item()) < 0.1, (c_mod.item(), c_ex.item())
+
+
+def _train(m, steps, fuse, micro=1):
+    from penroz.models.model import _FusedRunner
+    runner = _FusedRunner(m, torch.device(DEV), False)
+    g = torch.Generator(device=DEV).manual_seed(7)
+    data = torch.randint(0, 512, (steps * micro, 2, 65), device=DEV, generator=g)
+    losses = []
+    for i in range(steps):
+        runner.zero_grad()
+        tot = 0.0
+        for j in range(micro):
+            b = data[i * micro + j]
+            tot += float(runner.exec.train_micro_step(b[:, :-1].contiguous(), b[:, 1:].contiguous(), 1.0 / micro,
+                                                      sync=j == micro - 1, fuse_optimizer=fuse and j == micro - 1))
+        runner.step()
+        losses.append(tot)
+    return losses
+
+
+@pytest.mark.parametrize("micro", [1, 2])
+def test_optimizer_in_backward_matches_the_separate_step(micro):
+    """The fused AdamW applied per segment inside the backward == the step after it (same
+    kernel, same values; only the launch order differs), with and without grad accumulation.
+    Bitwise except the embedding table, whose gradient is a scatter-add (atomic order)."""
+    a, b = _gemma("gemma3_text", seed=3).to(DEV), _gemma("gemma3_text", seed=3).to(DEV)
+    la, lb = _train(a, 3, False, micro), _train(b, 3, True, micro)
+    assert la == pytest.approx(lb, abs=1e-5)
+    for (n, p), (_, q) in zip(a.named_parameters(), b.named_parameters()):
+        if n == "layers.0.weight":
+            assert torch.allclose(p, q, rtol=0, atol=1e-5), n
+        else:
+            assert torch.equal(p, q), n
+
+
+def test_capture_returns_activation_and_gradient_pairs():
+    m = _gemma("gemma2").to(DEV)
+    ex = GemmaExecutor(m, torch.device(DEV))
+    ex.setup_training(False)
+    x = torch.randint(0, 512, (2, 32), device=DEV)
+    ex.zero_grad()
+    ex.train_micro_step(x, torch.roll(x, -1, 1), 1.0, capture=True)
+    algos, pairs = ex.captured()
+    assert algos[0] == "scaledembedding" and algos.count("transformerblock") == 2
+    assert len(pairs) == len(algos) - 1  # no pair for the softmax head
+    for act, grad in pairs:
+        assert act.shape[:2] == (2, 32) and act.shape == grad.shape
+        assert torch.isfinite(act).all() and torch.isfinite(grad).all()
