@@ -39,7 +39,6 @@ def main():
     ap.add_argument("--which", default="fwd,bwd")
     ap.add_argument("--sdpa", action="store_true")
     ap.add_argument("--p", type=float, default=0.0, help="attention dropout probability")
-    ap.add_argument("--bwd-variants", default="3,4", help="flash backward variants to time (head_dim 64)")
     a = ap.parse_args()
     B, T, H, D = a.B, a.T, a.H, a.D
     Hkv = a.Hkv or H
@@ -65,15 +64,8 @@ def main():
         k = kernels()
         dout = torch.randn_like(out)
         dq = torch.empty_like(qkv)
-        variants = [int(v) for v in a.bwd_variants.split(",")] if (hasattr(k, "flash_bwd_variant") and D == 64) else [0]
-        for v in variants:
-            if v:
-                prev = k.flash_bwd_variant(v)
-            t = timeit(lambda: A.flash_bwd(dout, qkv, out, lse, H, Hkv, D, a.p, 7, dqkv=dq), a.iters)
-            sfx = f"_v{v}" if v else ""
-            res.update({f"bwd{sfx}_us": round(t * 1e6, 1), f"bwd{sfx}_TF": round(2.5 * fl / t / 1e12, 1)})
-            if v:
-                k.flash_bwd_variant(prev)
+        t = timeit(lambda: A.flash_bwd(dout, qkv, out, lse, H, Hkv, D, a.p, 7, dqkv=dq), a.iters)
+        res.update({"bwd_us": round(t * 1e6, 1), "bwd_TF": round(2.5 * fl / t / 1e12, 1)})
     if a.sdpa:
         q, k, v = qkv.split([H * D, Hkv * D, Hkv * D], dim=2)
         q = q.reshape(B, T, H, D).transpose(1, 2).detach().requires_grad_()

@@ -89,7 +89,6 @@ void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad, int64_t t
 void flash_attn_fwd(torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int64_t H, int64_t Hkv, int64_t D,
                     double scale, double p_drop, int64_t seed);
 int64_t flash_fwd_variant(int64_t v);
-int64_t flash_bwd_variant(int64_t v);
 void flash_attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, torch::Tensor dqkv,
                     int64_t H, int64_t Hkv, int64_t D, double scale, double p_drop, int64_t seed,
                     c10::optional<torch::Tensor> dbias);
@@ -179,8 +178,7 @@ PYBIND11_MODULE(penroz_kernels, m) {
   m.def("wgrad_gemm", &wgrad_gemm, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("grad"),
         pybind11::arg("tile") = 256, pybind11::arg("variant") = 8);
   m.def("flash_attn_fwd", &flash_attn_fwd);
-  m.def("flash_bwd_variant", &flash_bwd_variant, pybind11::arg("variant") = 0,
-        "select the dK/dV kernel (1 register-staged, 2 LDS-DMA pipelined); returns the previous one");
+returns the previous one");
   m.def("flash_fwd_variant", &flash_fwd_variant, pybind11::arg("variant") = 0,
         "select the forward kernel (1 single-stage, 2 tile-pipelined); returns the previous one");
   m.def("flash_attn_bwd", &flash_attn_bwd, pybind11::arg("dout"), pybind11::arg("qkv"), pybind11::arg("out"),

@@ -92,6 +92,20 @@ __device__ __forceinline__ bool dropout_keep(uint64_t seed, int b, int h, int H,
 
 __device__ __forceinline__ uint4 zero4() { return uint4{0u, 0u, 0u, 0u}; }
 
+// 8 bf16 values × c, rounded back to bf16: the backward kernels prescale the operand of
+// S = Q·Kᵀ that they keep in registers by c = scale·log2(e) once, and start the S accumulator
+// at the row's −LSE·log2(e), so P = exp2(S) costs one instruction per score instead of an FMA
+// and an exponential (the same one extra bf16 rounding of that operand a Triton flash kernel
+// applies to q; the forward's statistics stay exact)
+__device__ __forceinline__ uint4 scale_bf16x8(uint4 u, float c) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+  uint32_t o[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    o[i] = pack_bf16x2(__uint_as_float(w[i] << 16) * c, __uint_as_float(w[i] & 0xffff0000u) * c);
+  return uint4{o[0], o[1], o[2], o[3]};
+}
+
 // raw v_exp_f32 (no denormal range fix-up: softmax weights that small are 0 anyway)
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 

@@ -18,7 +18,9 @@
 //   K/V tiles of 64 keys are double-buffered in LDS and staged through registers (the global
 //   loads of tile j+1 are issued before tile j's MFMAs, written to LDS after them);
 //   heaviest (latest) query blocks launch first; fully-masked tiles are skipped per wave.
-// backward (deterministic, no atomics):
+// backward (deterministic, no atomics; the S = Q·Kᵀ operand each kernel keeps in registers is
+// prescaled by scale·log2(e) and S starts from the row's −LSE·log2(e), so P = exp2(S) — one VALU
+// instruction per score fewer than exp2(fma(S, c, −LSE·log2 e)); attn_common.h scale_bf16x8):
 //   dK/dV kernel — a wave keeps 32 keys' K, V fragments and dKᵀ, dVᵀ accumulators in
 //   registers while sweeping 32-row query slices staged in LDS (all query heads of its KV
 //   group): S = Q·Kᵀ and dP = dO·Vᵀ put the key on the lane, so P and dS feed dVᵀ = dOᵀ·P and
@@ -541,6 +543,7 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv3_kernel(const bf16* __rest
   }
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
+    kf[s] = scale_bf16x8(kf[s], c);  // S = Q·(cK)ᵀ (see scale_bf16x8); dK uses Q, not K
     launder(kf[s]);
     launder(vf[s]);
   }
@@ -647,9 +650,10 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv3_kernel(const bf16* __rest
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const float4_t dl = *reinterpret_cast<const float4_t*>(&del_s[32 * half + 8 * g + 4 * hh]);
+          const float4_t l2 = *reinterpret_cast<const float4_t*>(&lse_s[32 * half + 8 * g + 4 * hh]) * kLog2e;
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
-            sp[half][4 * g + k] = 0.f;
+            sp[half][4 * g + k] = -l2[k];  // S accumulates onto −LSE·log2(e): P = exp2(S)
             dp[half][4 * g + k] = DROPOUT ? 0.f : -dl[k];
           }
         }
@@ -673,14 +677,13 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv3_kernel(const bf16* __rest
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             const int r0 = 8 * g + 4 * hh;
-            const float4_t l2 = *reinterpret_cast<const float4_t*>(&lse_s[32 * half + r0]) * kLog2e;
             float4_t dl = {0.f, 0.f, 0.f, 0.f};
             if constexpr (DROPOUT) dl = *reinterpret_cast<const float4_t*>(&del_s[32 * half + r0]);
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
               const int i = 4 * g + k;
               const int q = qh0 + r0 + k;
-              float p = fexp2(fmaf(sp[half][i], c, -l2[k]));
+              float p = fexp2(sp[half][i]);
               if constexpr (MASK) p = (key > q || q >= T || key >= T) ? 0.f : p;
               if constexpr (DROPOUT) {  // row q = qh0 + 4hh + 8g + k: row product by addition
                 const bool keep = dropout_keep_mixed(drow0 + (uint32_t)(8 * g + k) * kDropRowMul, dkey, key & 1, dthr);
@@ -781,6 +784,7 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dq4_kernel(const bf16* __restri
   float dl = qok ? delta[rr] : 0.f;
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
+    qf[s] = scale_bf16x8(qf[s], c);  // S = (cQ)·Kᵀ (see scale_bf16x8); dQ uses K, not Q
     launder(qf[s]);
     launder(dof[s]);
   }
@@ -860,7 +864,7 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dq4_kernel(const bf16* __restri
       for (int kh = 0; kh < 2; ++kh) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          s[kh][i] = 0.f;
+          s[kh][i] = -l2;  // S accumulates onto −LSE·log2(e) of this lane's query row: P = exp2(S)
           dp[kh][i] = DROPOUT ? 0.f : -dl;
         }
 #pragma unroll
@@ -878,7 +882,7 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dq4_kernel(const bf16* __restri
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
             const int k = kt0 + 32 * kh + acc_row(i, lane);
-            float p = fexp2(fmaf(s[kh][i], c, -l2));
+            float p = fexp2(s[kh][i]);
             if constexpr (MASK) p = (k > qrow || k >= T || !qok) ? 0.f : p;
             if constexpr (DROPOUT) {  // key k = kt0 + 32kh + 4hh + (i&3) + 8(i>>2); pairs share a hash
               const uint32_t km = kpair0 + (uint32_t)(16 * kh + 4 * (i >> 2) + ((i & 3) >> 1)) * kDropKeyMul;
@@ -934,7 +938,6 @@ static void check_qkv(const torch::Tensor& qkv, int64_t H, int64_t Hkv, int64_t 
 }
 
 static int g_fa_fwd_variant = 3;
-static int g_fa_bwd_variant = 3;
 
 void flash_attn_fwd(torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int64_t H, int64_t Hkv, int64_t D,
                     double scale, double p_drop, int64_t seed) {
@@ -962,15 +965,8 @@ void flash_attn_fwd(torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int
 
 // forward: 1 = single-stage (fa_fwd_kernel; also the dropout path), 3 = two query blocks per
 // wave (fa_fwd3_kernel, default). backward:
-// 3 = LDS-DMA pipelined dK/dV and dQ kernels with precomputed per-lane LDS offsets and
-// stage-unrolled 3-stage rings (default; dropout included), 4 = the same with 4-stage rings
-int64_t flash_bwd_variant(int64_t v) {
-  const int64_t prev = g_fa_bwd_variant;
-  TORCH_CHECK(v <= 0 || v == 3 || v == 4, "flash backward variant must be 3 or 4");
-  if (v > 0) g_fa_bwd_variant = (int)v;
-  return prev;
-}
-
+// 3-stage LDS-DMA rings throughout the backward (4 stages measured neutral in the training step:
+// 65.47 / 65.51 vs 65.52 / 65.35 ms, so the knob is gone)
 int64_t flash_fwd_variant(int64_t v) {
   const int64_t prev = g_fa_fwd_variant;
   if (v > 0) g_fa_fwd_variant = (int)v;
@@ -1003,13 +999,8 @@ void flash_attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, to
                             uint64_t);
   const bool drop = p_drop > 0.0;
   BwdKernel kv, dq;
-  if (g_fa_bwd_variant == 4) {  // 4-stage rings: three slices / tiles in flight
-    kv = drop ? fa_bwd_dkdv3_kernel<true, 4> : fa_bwd_dkdv3_kernel<false, 4>;
-    dq = drop ? fa_bwd_dq4_kernel<true, 4> : fa_bwd_dq4_kernel<false, 4>;
-  } else {
-    kv = drop ? fa_bwd_dkdv3_kernel<true, 3> : fa_bwd_dkdv3_kernel<false, 3>;
-    dq = drop ? fa_bwd_dq4_kernel<true, 3> : fa_bwd_dq4_kernel<false, 3>;
-  }
+  kv = drop ? fa_bwd_dkdv3_kernel<true, 3> : fa_bwd_dkdv3_kernel<false, 3>;
+  dq = drop ? fa_bwd_dq4_kernel<true, 3> : fa_bwd_dq4_kernel<false, 3>;
   const float pd = drop ? (float)p_drop : 0.f;
   const bool want_bias = dbias.has_value() && dbias->defined();
   const int W = (int)((H + 2 * Hkv) * D), nblk = (T + 127) / 128;

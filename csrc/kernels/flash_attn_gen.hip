@@ -292,10 +292,12 @@ __global__ void __launch_bounds__(128, 1)
     }
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
+      kf[s] = scale_bf16x8(kf[s], c);  // S = Q·(cK)ᵀ (attn_common.h); dK uses Q, not K
       launder(kf[s]);
       launder(vf[s]);
     }
   }
+  static_assert(!KVLDS, "the prescaled-K form keeps K in registers");
   // B fragment s of Kᵀ (Vᵀ): element j = K[key][16s + 8hh + j]
   auto kfrag = [&](int s) -> uint4 {
     if constexpr (KVLDS) return row_frag(panel(KVs, BK, s >> 2), 32 * w, s & 3, lane);
@@ -346,9 +348,10 @@ __global__ void __launch_bounds__(128, 1)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const float4_t dl = *reinterpret_cast<const float4_t*>(&del_s[8 * g + 4 * hh]);
+        const float4_t l2 = *reinterpret_cast<const float4_t*>(&lse_s[8 * g + 4 * hh]) * kLog2e;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          sp[4 * g + k] = 0.f;
+          sp[4 * g + k] = -l2[k];  // S accumulates onto −LSE·log2(e): P = exp2(S)
           dp[4 * g + k] = DROPOUT ? 0.f : -dl[k];
         }
       }
@@ -363,14 +366,13 @@ __global__ void __launch_bounds__(128, 1)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int r0 = 8 * g + 4 * hh;
-          const float4_t l2 = *reinterpret_cast<const float4_t*>(&lse_s[r0]) * kLog2e;
           float4_t dl = {0.f, 0.f, 0.f, 0.f};
           if constexpr (DROPOUT) dl = *reinterpret_cast<const float4_t*>(&del_s[r0]);
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
             const int i = 4 * g + k;
             const int q = qs0 + r0 + k;
-            float p = fexp2(fmaf(sp[i], c, -l2[k]));
+            float p = fexp2(sp[i]);
             if constexpr (MASK) p = (key > q || q >= T || key >= T) ? 0.f : p;
             if constexpr (DROPOUT) {
               const bool keep = dropout_keep(seed, b, hq, H, T, q, key, p_drop);
@@ -491,6 +493,7 @@ __global__ void __launch_bounds__(128, (D >= 256 ? 1 : 2))
   float dl = qok ? delta[rr] : 0.f;
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
+    qf[s] = scale_bf16x8(qf[s], c);  // S = (cQ)·Kᵀ (attn_common.h); dQ uses K, not Q
     launder(qf[s]);
     launder(dof[s]);
   }
@@ -520,7 +523,7 @@ __global__ void __launch_bounds__(128, (D >= 256 ? 1 : 2))
       f32x16 st, dp;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        st[i] = 0.f;
+        st[i] = -l2;  // S accumulates onto −LSE·log2(e): P = exp2(S)
         dp[i] = DROPOUT ? 0.f : -dl;
       }
 #pragma unroll
@@ -534,7 +537,7 @@ __global__ void __launch_bounds__(128, (D >= 256 ? 1 : 2))
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int k = kt0 + acc_row(i, lane);
-          float p = fexp2(fmaf(st[i], c, -l2));
+          float p = fexp2(st[i]);
           if constexpr (MASK) p = (k > qrow || k >= T || !qok) ? 0.f : p;
           if constexpr (DROPOUT) {
             const bool keep = dropout_keep(seed, b, h, H, T, qrow, k, p_drop);

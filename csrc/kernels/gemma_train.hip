@@ -158,7 +158,7 @@ __global__ void __launch_bounds__(256) gm_combine_fwd_kernel(int mode, const flo
   }
 }
 
-// part: fp32 [2][gridDim.x * 4][C] — this wave's dw1 (row block 0) and dw2 (row block 1) sums
+// part: fp32 [2][gridDim.x][C] — this workgroup's dw1 (row block 0) and dw2 (row block 1) sums
 template <int NCH>
 __global__ void __launch_bounds__(256) gm_combine_bwd_kernel(int mode, const bf16* __restrict__ dy,
                                                              const float* __restrict__ dh_in,
@@ -242,8 +242,18 @@ __global__ void __launch_bounds__(256) gm_combine_bwd_kernel(int mode, const bf1
       if (mode == 2) st_bf16<NCH>(da + base, dh, lane, C);
     }
   }
-  st_f32<NCH>(part + (size_t)gw * C, p1, lane, C);
-  st_f32<NCH>(part + ((size_t)nw + gw) * C, p2, lane, C);
+  // the workgroup's 4 wave partials summed through LDS in wave order (deterministic): one partial
+  // row per workgroup and weight
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [4][C]
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    st_f32<NCH>(red + (size_t)w * C, pass == 0 ? p1 : p2, lane, C);
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += 256)
+      part[((size_t)pass * gridDim.x + blockIdx.x) * C + c] = (red[c] + red[C + c]) + (red[2 * C + c] + red[3 * C + c]);
+    __syncthreads();
+  }
 }
 
 }  // namespace penroz
@@ -274,7 +284,9 @@ static void gm_check_vec(const c10::optional<torch::Tensor>& t, int64_t n, const
               "gemma combine: ", what, " must be a contiguous fp32 vector of ", n, " elements");
 }
 
-static int gm_grid(int64_t N) { return (int)std::min<int64_t>((N + 3) / 4, 256); }
+// 4 rows in flight per workgroup, up to 4 workgroups per CU: enough waves to overlap each row's
+// memory latency (a one-workgroup-per-CU grid ran the backward 2.4x off its HBM roofline)
+static int gm_grid(int64_t N) { return (int)std::min<int64_t>((N + 3) / 4, 1024); }
 
 // see the file header; x fp32 [N, C]; a bf16 [N, C] (modes 0-2); h_out fp32 (modes 0-2);
 // y_out bf16; s_save fp32 (mode 0); r1 fp32 [N] (modes 0, 1); r2 fp32 [N]
@@ -351,10 +363,11 @@ void gemma_combine_bwd(int64_t mode, torch::Tensor dy, c10::optional<torch::Tens
     dhs = dh_save->data_ptr<float>();
   }
   if (N == 0) return;
-  const int grid = gm_grid(N), G = grid * 4;
+  const int grid = gm_grid(N), G = grid;
   auto part = torch::empty({2, G, C}, h.options());
   auto stream = at::hip::getCurrentHIPStream();
-  PENROZ_GM_NCH(C, hipLaunchKernelGGL((gm_combine_bwd_kernel<NCH>), dim3(grid), dim3(256), 0, stream, (int)mode,
+  PENROZ_GM_NCH(C, hipLaunchKernelGGL((gm_combine_bwd_kernel<NCH>), dim3(grid), dim3(256), 4 * C * sizeof(float),
+                                      stream, (int)mode,
                                       reinterpret_cast<const bf16*>(dy.data_ptr()), dhp, h.data_ptr<float>(),
                                       mode == 0 ? s_save->data_ptr<float>() : nullptr,
                                       mode == 1 ? reinterpret_cast<const bf16*>(a_save->data_ptr()) : nullptr,

@@ -89,19 +89,6 @@ def flash_fwd(qkv: Tensor, H: int, Hkv: int, D: int, dropout_p: float = 0.0, see
     return out, lse
 
 
-_BWD_VARIANT_ENV = "PENROZ_FLASH_BWD_VARIANT"  # 3 / 4 (A/B knob; unset = the kernel default, 3)
-_bwd_variant_applied = False
-
-
-def _apply_bwd_variant():
-    global _bwd_variant_applied
-    if not _bwd_variant_applied:
-        _bwd_variant_applied = True
-        v = int(os.environ.get(_BWD_VARIANT_ENV, "0"))
-        if v:
-            kernels().flash_bwd_variant(v)
-
-
 def flash_bwd(dout: Tensor, qkv: Tensor, out: Tensor, lse: Tensor, H: int, Hkv: int, D: int,
               dropout_p: float = 0.0, seed: int = 0, dqkv: Tensor | None = None,
               dbias: Tensor | None = None) -> Tensor:
@@ -112,7 +99,6 @@ def flash_bwd(dout: Tensor, qkv: Tensor, out: Tensor, lse: Tensor, H: int, Hkv: 
     pass over the 2304-wide gradient); other head dims run the column-sum kernel afterwards."""
     dqkv = torch.empty_like(qkv) if dqkv is None else dqkv
     scale = 1.0 / math.sqrt(D)
-    _apply_bwd_variant()
     if D == 64:
         kernels().flash_attn_bwd(dout, qkv, out, lse, dqkv, H, Hkv, D, scale, float(dropout_p), int(seed), dbias)
     else:

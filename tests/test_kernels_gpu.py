@@ -307,20 +307,14 @@ def test_flash_fwd(B, T, H, Hkv, variant):
     _close(lse, rl, 2e-3, 1e-4, "lse")
 
 
-@pytest.mark.parametrize("variant", [3, 4])
 @pytest.mark.parametrize("B,T,H,Hkv", [(2, 512, 4, 4), (1, 200, 3, 3), (2, 130, 4, 2), (1, 7, 2, 1), (1, 1024, 2, 2),
                                        (1, 320, 4, 1)])
-def test_flash_bwd(B, T, H, Hkv, variant):
+def test_flash_bwd(B, T, H, Hkv):
     torch.manual_seed(0)
     qkv = _qkv(B, T, H, Hkv)
     out, lse = A.flash_fwd(qkv, H, Hkv, 64)
     dout = torch.randn(B, T, H * 64, device=DEV).to(torch.bfloat16)
-    k = _ext.kernels()
-    prev = k.flash_bwd_variant(variant)
-    try:
-        dq = A.flash_bwd(dout, qkv, out, lse, H, Hkv, 64)
-    finally:
-        k.flash_bwd_variant(prev)
+    dq = A.flash_bwd(dout, qkv, out, lse, H, Hkv, 64)
     x = qkv.float().requires_grad_()
     ro, _ = A.reference_attention_lse(x, H, Hkv, 64)
     (ro * dout.float()).sum().backward()
@@ -331,58 +325,28 @@ def test_flash_bwd(B, T, H, Hkv, variant):
         assert rel < 0.02, f"{name} relative error {rel}"
 
 
-@pytest.mark.parametrize("variant", [3, 4])
 @pytest.mark.parametrize("B,T,H,Hkv,p", [(2, 512, 4, 4, 0.0), (1, 200, 3, 3, 0.0), (2, 130, 4, 2, 0.0),
                                          (1, 7, 2, 1, 0.0), (1, 300, 2, 2, 0.1)])
-def test_flash_bwd_fused_bias_grad(B, T, H, Hkv, p, variant):
+def test_flash_bwd_fused_bias_grad(B, T, H, Hkv, p):
     """dbias (the qkv bias gradient) from the attention-backward epilogues == the column sums of the
     dqkv the same call stored, accumulated onto the existing value (fp32 torch reference)."""
     torch.manual_seed(0)
     qkv = _qkv(B, T, H, Hkv)
     out, lse = A.flash_fwd(qkv, H, Hkv, 64, p, 7)
     dout = torch.randn(B, T, H * 64, device=DEV).to(torch.bfloat16)
-    k = _ext.kernels()
-    prev = k.flash_bwd_variant(variant)
-    try:
-        base = torch.randn((H + 2 * Hkv) * 64, device=DEV)
-        dbias = base.clone()
-        dq = A.flash_bwd(dout, qkv, out, lse, H, Hkv, 64, p, 7, dbias=dbias)
-        dq_plain = A.flash_bwd(dout, qkv, out, lse, H, Hkv, 64, p, 7)
-    finally:
-        k.flash_bwd_variant(prev)
+    base = torch.randn((H + 2 * Hkv) * 64, device=DEV)
+    dbias = base.clone()
+    dq = A.flash_bwd(dout, qkv, out, lse, H, Hkv, 64, p, 7, dbias=dbias)
+    dq_plain = A.flash_bwd(dout, qkv, out, lse, H, Hkv, 64, p, 7)
     torch.testing.assert_close(dq, dq_plain, rtol=0, atol=0)  # the epilogue does not change dqkv
     ref = base + dq.float().reshape(-1, dq.shape[-1]).sum(0)
     torch.testing.assert_close(dbias, ref, rtol=1e-4, atol=1e-3)
 
 
-@pytest.mark.parametrize("variant", [3, 4])
-def test_flash_dropout_matches_masked_reference(variant):
+def test_flash_dropout_matches_masked_reference():
     """With one-hot V rows the forward output reveals the dropout mask exactly; the backward
     must reproduce the gradients of softmax -> mask/(1-p) -> @V with that same mask."""
-    prev = _ext.kernels().flash_bwd_variant(variant)
-    try:
-        _dropout_masked_reference()
-    finally:
-        _ext.kernels().flash_bwd_variant(prev)
-
-
-@pytest.mark.parametrize("B,T,H,Hkv", [(2, 300, 4, 4), (1, 1024, 2, 1)])
-def test_flash_dropout_bwd_variants_agree(B, T, H, Hkv):
-    """The dropout backward through the 4-stage rings (variant 4) == the default 3-stage path."""
-    torch.manual_seed(0)
-    qkv = _qkv(B, T, H, Hkv)
-    out, lse = A.flash_fwd(qkv, H, Hkv, 64, 0.1, 5)
-    dout = torch.randn(B, T, H * 64, device=DEV).to(torch.bfloat16)
-    k = _ext.kernels()
-    res = {}
-    for v in (3, 4):
-        prev = k.flash_bwd_variant(v)
-        try:
-            res[v] = A.flash_bwd(dout, qkv, out, lse, H, Hkv, 64, 0.1, 5).float()
-        finally:
-            k.flash_bwd_variant(prev)
-    rel = (res[4] - res[3]).norm() / res[3].norm()
-    assert rel < 1e-3, rel
+    _dropout_masked_reference()
 
 
 def _dropout_masked_reference():
