@@ -178,7 +178,6 @@ PYBIND11_MODULE(penroz_kernels, m) {
   m.def("wgrad_gemm", &wgrad_gemm, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("grad"),
         pybind11::arg("tile") = 256, pybind11::arg("variant") = 8);
   m.def("flash_attn_fwd", &flash_attn_fwd);
-returns the previous one");
   m.def("flash_fwd_variant", &flash_fwd_variant, pybind11::arg("variant") = 0,
         "select the forward kernel (1 single-stage, 2 tile-pipelined); returns the previous one");
   m.def("flash_attn_bwd", &flash_attn_bwd, pybind11::arg("dout"), pybind11::arg("qkv"), pybind11::arg("out"),
