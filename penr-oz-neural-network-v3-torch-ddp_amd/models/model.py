@@ -703,9 +703,10 @@ class _GenericRunner:
             if reference:
                 self.ddp_model = nn.parallel.DistributedDataParallel(model)
             else:
-                from penroz.parallel.reducer import HookedReducer
+                from penroz.parallel.reducer import HookedReducer, row_sparse_tables, sparse_rows_enabled
                 self._broadcast_params()
-                self.reducer = HookedReducer(list(model.parameters()))
+                sparse = row_sparse_tables(model) if sparse_rows_enabled(dist.get_backend()) else None
+                self.reducer = HookedReducer(list(model.parameters()), sparse_rows=sparse)
         self._acts: list[Tensor] = []
         self._algos = [l.__class__.__name__.lower() for l in model.layers]
 

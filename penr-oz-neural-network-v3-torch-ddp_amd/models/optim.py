@@ -76,6 +76,14 @@ class _FusedMixin:
         return bool(ps) and all(p.is_cuda and p.dtype in (torch.float32, torch.bfloat16) and p.grad.dtype == p.dtype
                                 for p in ps) and _ext.available()
 
+    @staticmethod
+    def _group_cpu_fused_ok(group) -> bool:
+        if group.get("differentiable") or group.get("capturable"):
+            return False
+        ps = [p for p in group["params"] if p.grad is not None]
+        return bool(ps) and all(p.device.type == "cpu" and not p.grad.is_sparse and p.grad.dtype == p.dtype
+                                and p.dtype in (torch.float32, torch.float64, torch.bfloat16) for p in ps)
+
     @torch.no_grad()
     def step(self, closure=None, grad_scale: float = 1.0):
         """One optimizer step; ``grad_scale`` multiplies every gradient (e.g. 1/num_steps)."""
@@ -99,12 +107,19 @@ class _FusedMixin:
                     for p in g["params"]:
                         if p.grad is not None:
                             p.grad.mul_(grad_scale)
+            # host parameters: torch's single-pass vectorised CPU kernel (6x the per-tensor loop at
+            # the GPT-2 124M plumbing config: 76 vs 461 ms per step with 4 threads)
+            cpu_fused = [g for g in fallback if self._group_cpu_fused_ok(g)]
+            for g in cpu_fused:
+                g["fused"] = True
             saved = self.param_groups
             self.param_groups = fallback
             try:
                 super().step()
             finally:
                 self.param_groups = saved
+                for g in cpu_fused:
+                    g["fused"] = None
         return loss
 
     def _hyper(self, group):

@@ -182,6 +182,28 @@ class GradReducer:
                 dist.broadcast(flat_param, src=src, group=self.group)
 
 
+def row_sparse_tables(model: torch.nn.Module) -> list[torch.nn.Parameter]:
+    """Embedding weights whose gradient is row-sparse: owned by one ``nn.Embedding`` (dense
+    gradient) and used by no other module — a tied lm_head makes the table's gradient dense."""
+    uses: dict[int, int] = {}
+    for mod in model.modules():
+        for p in mod.parameters(recurse=False):
+            uses[id(p)] = uses.get(id(p), 0) + 1
+    return [m.weight for m in model.modules()
+            if isinstance(m, torch.nn.Embedding) and not m.sparse and m.max_norm is None
+            and m.weight.requires_grad and uses.get(id(m.weight)) == 1]
+
+
+def sparse_rows_enabled(backend: str | None) -> bool:
+    """PENROZ_SPARSE_EMBED_GRAD=1/0 forces it; default on for gloo (host memory bandwidth and TCP
+    make the dense 147 MB token table the largest single cost of the CPU plumbing step) and off
+    for RCCL (at 64k tokens per rank nearly every row of a 50k vocabulary is touched)."""
+    env = os.environ.get("PENROZ_SPARSE_EMBED_GRAD")
+    if env is not None:
+        return env != "0"
+    return backend == "gloo"
+
+
 class HookedReducer:
     """Generic-model reducer: autograd post-accumulate hooks mark parameters ready.
 
@@ -189,28 +211,36 @@ class HookedReducer:
     (≈ backward order); a bucket launches when all its parameters have accumulated.
     """
 
-    def __init__(self, params: list[torch.nn.Parameter], bucket_mb: float | None = None, group=None):
+    def __init__(self, params: list[torch.nn.Parameter], bucket_mb: float | None = None, group=None,
+                 sparse_rows: list[torch.nn.Parameter] | None = None):
+        backend = dist.get_backend(group) if dist.is_initialized() else None
         if bucket_mb is None:
-            bucket_mb = default_bucket_mb(dist.get_backend(group) if dist.is_initialized() else None)
+            bucket_mb = default_bucket_mb(backend)
         self.params = [p for p in params if p.requires_grad]
         order = list(reversed(self.params))
         total = sum(p.numel() for p in order)
         dev, dtype = order[0].device, order[0].dtype
         self.flat_grad = torch.zeros(total, device=dev, dtype=dtype)
         self.offsets = {}
+        # row-sparse tables (embedding weights used by nothing else): reduced over the union of the
+        # rows any rank touched instead of densely (see _reduce_rows); excluded from the buckets
+        ids = {id(p) for p in (sparse_rows or [])}
+        self.sparse = [p for p in order if id(p) in ids and p.dim() == 2]
         segments = []
         off = 0
         for p in order:
             n = p.numel()
             self.offsets[p] = off
-            segments.append((off, off + n))
+            if not any(p is q for q in self.sparse):
+                segments.append((off, off + n))
             off += n
         self.reducer = GradReducer(self.flat_grad, plan_buckets(segments, bucket_mb * 2**20,
                                                                 self.flat_grad.element_size()), group)
-        self._pending = [0] * len(self.reducer.buckets)
+        self.group = group
         self._param_bucket = {}
         for p in order:
-            self._param_bucket[p] = self.reducer.bucket_of(self.offsets[p])
+            self._param_bucket[p] = -1 if any(p is q for q in self.sparse) else self.reducer.bucket_of(self.offsets[p])
+        self._rows_pending: list = []
         self.sync = True
         self._handles = [p.register_post_accumulate_grad_hook(self._hook) for p in order]
         self.attach_grads()
@@ -224,19 +254,44 @@ class HookedReducer:
     def _reset_counts(self):
         self._pending = [0] * len(self.reducer.buckets)
         for p in self.params:
-            self._pending[self._param_bucket[p]] += 1
+            if self._param_bucket[p] >= 0:
+                self._pending[self._param_bucket[p]] += 1
 
     def _hook(self, p):
         if not self.sync:
             return
         b = self._param_bucket[p]
+        if b < 0:  # row-sparse tables reduce in finish(): same collective order on every rank
+            return
         self._pending[b] -= 1
         if self._pending[b] == 0:
             self.reducer.bucket_ready(b)
 
+    def _reduce_rows(self, p):
+        """All-reduce only the rows of ``p.grad`` that some rank touched: one small all-reduce of
+        the row mask, then the union rows packed into one buffer. Exact: a row no rank touched is
+        zero everywhere. The token table of the CPU plumbing config (T = 64, B = 4) is 256 of 50304
+        rows per rank, so its 147 MB of fp32 gradient go over gloo as ≈ 1.5 MB."""
+        if self.reducer.world == 1:
+            return
+        g = self.flat_grad[self.offsets[p]:self.offsets[p] + p.numel()].view_as(p)
+        mask = g.ne(0).any(dim=1).to(torch.int32)
+        dist.all_reduce(mask, group=self.group)
+        rows = mask.nonzero().squeeze(1)
+        packed = g.index_select(0, rows)
+        work = dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        self._rows_pending.append((work, g, rows, packed))
+
     def finish(self):
         if self.sync:
+            self.reducer.launch_remaining()
+            for p in self.sparse:
+                self._reduce_rows(p)
             self.reducer.finish()
+            for work, g, rows, packed in self._rows_pending:
+                work.wait()
+                g.index_copy_(0, rows, packed.div_(self.reducer.world))
+            self._rows_pending.clear()
         self._reset_counts()
 
     def zero_grad(self):

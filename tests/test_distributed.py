@@ -73,24 +73,31 @@ def test_grad_reducer_rejects_unknown_wire():
         GradReducer(torch.zeros(4), [(0, 4)], wire="fp8")
 
 
-def _hooked_worker(rank, world, port, out):
+def _hooked_worker(rank, world, port, out, sparse=False):
     _init(rank, world, port)
     from penroz.models.mapper import Mapper
     from penroz.models.model import NeuralNetworkModel
+    from penroz.parallel.reducer import row_sparse_tables
     torch.manual_seed(0)
     m = NeuralNetworkModel("h", Mapper(bench.gpt2_layers(V=32, C=16, L=1, H=2, P=16), {"sgd": {"lr": 0.1}}))
-    red = HookedReducer(list(m.parameters()), bucket_mb=0.001)
+    tables = row_sparse_tables(m) if sparse else None
+    if sparse:
+        assert len(tables) == 2  # token + position tables (the lm_head is untied)
+    red = HookedReducer(list(m.parameters()), bucket_mb=0.001, sparse_rows=tables)
     torch.manual_seed(100 + rank)
-    x = torch.randint(0, 32, (2, 8))
-    _, loss = m(x, torch.roll(x, -1, 1), skip_softmax=True)
-    loss.backward()
+    for micro in range(2):  # grad accumulation: the row union covers both micro-steps
+        red.sync = micro == 1
+        x = torch.randint(0, 32, (2, 4 + 4 * micro))
+        _, loss = m(x, torch.roll(x, -1, 1), skip_softmax=True)
+        loss.backward()
     red.finish()
     torch.save({n: p.grad.clone() for n, p in m.named_parameters()}, f"{out}/grads{rank}.pt")
     dist.destroy_process_group()
 
 
-def test_hooked_reducer_matches_mean_of_local_grads(tmp_path):
-    mp.spawn(_hooked_worker, args=(2, _port(), str(tmp_path)), nprocs=2)
+@pytest.mark.parametrize("sparse", [False, True])
+def test_hooked_reducer_matches_mean_of_local_grads(tmp_path, sparse):
+    mp.spawn(_hooked_worker, args=(2, _port(), str(tmp_path), sparse), nprocs=2)
     from penroz.models.mapper import Mapper
     from penroz.models.model import NeuralNetworkModel
     local = []
@@ -98,9 +105,10 @@ def test_hooked_reducer_matches_mean_of_local_grads(tmp_path):
         torch.manual_seed(0)
         m = NeuralNetworkModel("h", Mapper(bench.gpt2_layers(V=32, C=16, L=1, H=2, P=16), {"sgd": {"lr": 0.1}}))
         torch.manual_seed(100 + rank)
-        x = torch.randint(0, 32, (2, 8))
-        _, loss = m(x, torch.roll(x, -1, 1), skip_softmax=True)
-        loss.backward()
+        for micro in range(2):
+            x = torch.randint(0, 32, (2, 4 + 4 * micro))
+            _, loss = m(x, torch.roll(x, -1, 1), skip_softmax=True)
+            loss.backward()
         local.append({n: p.grad for n, p in m.named_parameters()})
     g0, g1 = torch.load(tmp_path / "grads0.pt"), torch.load(tmp_path / "grads1.pt")
     for n in g0:

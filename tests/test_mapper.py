@@ -95,6 +95,31 @@ def test_fused_optimizer_cpu_matches_torch():
     assert torch.allclose(p1, p2)
     o3 = torch.optim.AdamW([nn.Parameter(torch.zeros(5, 4))], lr=1e-2)
     o3.load_state_dict(o1.state_dict())  # torch can read our state dict
+    assert o1.param_groups[0]["fused"] is None  # the CPU fused kernel is chosen per step, not saved
+    # and we resume from torch's (non-fused) state: the CPU fused kernel takes over its step tensors
+    p4 = nn.Parameter(p2.detach().clone())
+    o4 = FusedAdamW([p4], lr=1e-2, weight_decay=0.1)
+    o4.load_state_dict(copy.deepcopy(o2.state_dict()))  # (torch's state_dict shares its state tensors)
+    g = torch.randn(5, 4)
+    p4.grad, p2.grad = g.clone(), g.clone()
+    o4.step(grad_scale=0.5)
+    p2.grad.mul_(0.5)
+    o2.step()
+    assert torch.allclose(p4, p2)
+
+
+def test_fused_adam_cpu_matches_torch():
+    torch.manual_seed(1)
+    p1 = nn.Parameter(torch.randn(7, 3))
+    p2 = nn.Parameter(p1.detach().clone())
+    o1 = FusedAdam([p1], lr=1e-2, weight_decay=0.05, betas=(0.8, 0.9))
+    o2 = torch.optim.Adam([p2], lr=1e-2, weight_decay=0.05, betas=(0.8, 0.9))
+    for _ in range(4):
+        g = torch.randn(7, 3)
+        p1.grad, p2.grad = g.clone(), g.clone()
+        o1.step()
+        o2.step()
+    assert torch.allclose(p1, p2, atol=1e-6)
 
 
 def test_unsupported():
