@@ -24,6 +24,7 @@
 // (variant 4, the round-1 default) stay selectable for A/B measurement.
 #include "common.h"
 #include "host_plan.h"
+#include <cstdlib>
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 
@@ -315,9 +316,9 @@ __device__ __forceinline__ void unroll_steps(F&& f) {
 template <int BKT, int NBUF, bool PF = false>
 __global__ void __launch_bounds__(512, 1) wgrad256_ring16o_kernel(const bf16* __restrict__ A,
                                                                   const bf16* __restrict__ B,
-                                                                  float* __restrict__ out, int M, int N, int K,
-                                                                  int lda, int ldb, int klen, int tiles_m,
-                                                                  int tiles_n, int direct) {
+                                                                  float* __restrict__ grad, float* __restrict__ slab,
+                                                                  int M, int N, int K, int lda, int ldb, int tiles_m,
+                                                                  int tiles_n, WgradPlan plan) {
   extern __shared__ __attribute__((aligned(16))) char smem2[];  // [NBUF][A|B][BKT * 512]
   constexpr int TILE = BKT * 512;
   constexpr int PIECES = BKT / 16;
@@ -325,10 +326,23 @@ __global__ void __launch_bounds__(512, 1) wgrad256_ring16o_kernel(const bf16* __
   static_assert(BKT % 32 == 0 && NBUF == 4 && (NBUF - 2) * G <= 63, "ring geometry");
   static_assert(!PF || (BKT == 32 && NBUF == 4), "fragment prefetch: 32-deep stages, 4-stage ring");
   const int nwg = gridDim.x, wg = blockIdx.x;
-  const int xcd = wg & 7, qd = nwg >> 3, rd = nwg & 7;
-  const int id = (xcd < rd ? xcd * (qd + 1) : rd * (qd + 1) + (xcd - rd) * qd) + (wg >> 3);
   const int ntiles = tiles_m * tiles_n;
-  const int split = id / ntiles, tile = id - split * ntiles;
+  // (plan_wgrad, host_plan.h) ids [0, main_tiles·main_splits): the main tiles, split-major; then
+  // the tail tiles [main_tiles, ntiles) split-major, each split into its own per-tile slab. The
+  // XCD remap is applied within each range, so the main range is dispatched first and the tail's
+  // short workgroups fill the last round (a remap over the whole grid sent tail ids to the first
+  // round of some XCDs and long main tiles to their last).
+  const int n_main = plan.main_tiles * plan.main_splits;
+  const bool in_tail = wg >= n_main;
+  const int rbase = in_tail ? n_main : 0, rcnt = in_tail ? nwg - n_main : n_main, rwg = wg - rbase;
+  const int xcd = rwg & 7, qd = rcnt >> 3, rd = rcnt & 7;
+  const int id = rbase + (xcd < rd ? xcd * (qd + 1) : rd * (qd + 1) + (xcd - rd) * qd) + (rwg >> 3);
+  const int nt = ntiles - plan.main_tiles;
+  const int jt = id - n_main;
+  const int split = in_tail ? jt / nt : id / plan.main_tiles;
+  const int tail_i = in_tail ? jt - split * nt : 0;
+  const int tile = in_tail ? plan.main_tiles + tail_i : id - split * plan.main_tiles;
+  const int klen = in_tail ? plan.tail_klen : plan.main_klen;
   const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
   const int m0 = tm * BM2, n0 = tn * BN2;
   const int k0 = split * klen, k1 = min(K, k0 + klen);
@@ -471,7 +485,44 @@ __global__ void __launch_bounds__(512, 1) wgrad256_ring16o_kernel(const bf16* __
     if (st + decltype(ic)::value < nsteps) step(st + decltype(ic)::value, ic);
   });
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the zero-page prefetches
-  float* o = direct ? out : out + (size_t)split * M * N;
+  // main tiles: direct read-add-write (one split) or a full-size slab per split; tail tiles: a
+  // packed [256][256] slab per (split, tail tile), added by tile_slab_reduce_kernel
+  const bool direct = !in_tail && plan.main_splits == 1;
+  float* const obase = direct ? grad : slab;
+  const int64_t ld = in_tail ? BN2 : N;  // element (m, n) sits at obase[ob + m·ld + n]
+  const int64_t ob = direct ? 0
+                     : in_tail ? ((int64_t)split * nt + tail_i) * (BM2 * BN2) - (int64_t)m0 * BN2 - n0
+                               : (int64_t)split * M * N;
+  if (direct) {
+    // read-add-write in groups of 16 values: every read of a group is issued before its writes
+    // (written element by element, the compiler must assume each write may alias the next read
+    // and serialises 128 memory round trips per lane: 1.0 ms of a 4.0 ms lm_head wgrad)
+#pragma unroll
+    for (int i0 = 0; i0 < 8; ++i0) {
+      float cur[1][4][4];
+#pragma unroll
+      for (int ii = 0; ii < 1; ++ii)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int n = n0 + 64 * wn + 16 * j + (lane & 15);
+            const int m = m0 + 128 * wm + 16 * (i0 + ii) + 4 * g + r;
+            cur[ii][j][r] = (m < M && n < N) ? grad[(int64_t)m * N + n] : 0.f;
+          }
+#pragma unroll
+      for (int ii = 0; ii < 1; ++ii)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int n = n0 + 64 * wn + 16 * j + (lane & 15);
+            const int m = m0 + 128 * wm + 16 * (i0 + ii) + 4 * g + r;
+            if (m < M && n < N) grad[(int64_t)m * N + n] = cur[ii][j][r] + acc[i0 + ii][j][r];
+          }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -481,11 +532,7 @@ __global__ void __launch_bounds__(512, 1) wgrad256_ring16o_kernel(const bf16* __
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + 128 * wm + 16 * i + 4 * g + r;
-        if (m < M) {
-          float* pp = o + (size_t)m * N + n;
-          if (direct) *pp += acc[i][j][r];
-          else *pp = acc[i][j][r];
-        }
+        if (m < M) obase[ob + (int64_t)m * ld + n] = acc[i][j][r];
       }
     }
 }
@@ -497,6 +544,27 @@ __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restric
     float4_t acc = reinterpret_cast<float4_t*>(g)[i];
     for (int s = 0; s < splits; ++s) acc += reinterpret_cast<const float4_t*>(slab)[s * stride4 + i];
     reinterpret_cast<float4_t*>(g)[i] = acc;
+  }
+}
+
+// G[tile t of the tail] += Σ_s slab[s][t] for the tail tiles of a split-tail plan (packed
+// [256][256] fp32 per (split, tile); fixed order, so the result is bitwise reproducible)
+__global__ void __launch_bounds__(256) tile_slab_reduce_kernel(const float* __restrict__ slab, float* __restrict__ g,
+                                                               int M, int N, int tiles_n, int first_tile, int nt,
+                                                               int splits) {
+  constexpr int T4 = BM2 * BN2 / 4;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < (int64_t)nt * T4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int ti = (int)(i / T4), e = (int)(i - (int64_t)ti * T4);
+    const int r = e / (BN2 / 4), c = 4 * (e - r * (BN2 / 4));
+    const int tile = first_tile + ti, tm = tile / tiles_n, tn = tile - tm * tiles_n;
+    const int m = tm * BM2 + r, n = tn * BN2 + c;
+    if (m >= M || n >= N) continue;  // N % 8 == 0: n < N covers n + 3
+    float4_t* gp = reinterpret_cast<float4_t*>(g + (size_t)m * N + n);
+    float4_t acc = *gp;
+    for (int s = 0; s < splits; ++s)
+      acc += reinterpret_cast<const float4_t*>(slab + ((size_t)s * nt + ti) * (BM2 * BN2))[e];
+    *gp = acc;
   }
 }
 
@@ -535,11 +603,19 @@ void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad, int64_t t
     hipDeviceProp_t prop;
     n_cu = hipGetDeviceProperties(&prop, grad.get_device()) == hipSuccess ? prop.multiProcessorCount : 256;
   }
-  // split-K from the wave-quantisation cost model (host_plan.h, sanitizer-tested on the host)
-  const SplitK plan = plan_wgrad_splits(M, N, K, T, n_cu, T == 256 ? BK2 : BK);
-  const int splits = plan.splits, klen = plan.klen;
+  // split-K from the wave-quantisation cost model (host_plan.h, sanitizer-tested on the host);
+  // the ring16o variants (6, 8) may also take a split-tail plan (plan_wgrad)
+  const SplitK uplan = plan_wgrad_splits(M, N, K, T, n_cu, T == 256 ? BK2 : BK);
+  static const bool tail_ok = [] {  // PENROZ_WGRAD_TAIL=0: uniform plans only (A/B)
+    const char* e = std::getenv("PENROZ_WGRAD_TAIL");
+    return !(e && e[0] == '0');
+  }();
+  const bool ring16o = T == 256 && (variant == 6 || variant == 8) && tail_ok;
+  const WgradPlan wp = ring16o ? plan_wgrad(M, N, K, T, n_cu, BK2) : WgradPlan{ntiles, uplan.splits, uplan.klen, 0, 0};
+  const int splits = wp.main_splits, klen = wp.main_klen;
+  const int tail_tiles = ntiles - wp.main_tiles;
   auto stream = at::hip::getCurrentHIPStream();
-  const int nwg = ntiles * splits;
+  const int nwg = wp.main_tiles * splits + tail_tiles * wp.tail_splits;
   const bf16* a = reinterpret_cast<const bf16*>(dy.data_ptr());
   const bf16* b = reinterpret_cast<const bf16*>(x.data_ptr());
   torch::Tensor slab;
@@ -547,6 +623,8 @@ void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad, int64_t t
   if (splits > 1) {
     slab = torch::empty({(int64_t)splits * M * N}, grad.options());
     dst = slab.data_ptr<float>();
+  } else if (wp.tail_splits > 0) {
+    slab = torch::empty({(int64_t)wp.tail_splits * tail_tiles * T * T}, grad.options());
   }
   const int direct = splits == 1 ? 1 : 0;
   if (T == 256) {
@@ -574,14 +652,23 @@ void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad, int64_t t
       hipLaunchKernelGGL((wgrad256_ring16_kernel<BK2, 4>), dim3(nwg), dim3(512), lds, stream, a, b, dst, M, N, K,
                          lda, ldb, klen, tiles_m, tiles_n, direct);
     else if (variant == 8)
-      hipLaunchKernelGGL((wgrad256_ring16o_kernel<BK2, 4, true>), dim3(nwg), dim3(512), lds, stream, a, b, dst, M,
-                         N, K, lda, ldb, klen, tiles_m, tiles_n, direct);
+      hipLaunchKernelGGL((wgrad256_ring16o_kernel<BK2, 4, true>), dim3(nwg), dim3(512), lds, stream, a, b,
+                         grad.data_ptr<float>(), slab.defined() ? slab.data_ptr<float>() : nullptr, M, N, K, lda, ldb,
+                         tiles_m, tiles_n, wp);
     else
-      hipLaunchKernelGGL((wgrad256_ring16o_kernel<BK2, 4>), dim3(nwg), dim3(512), lds, stream, a, b, dst, M, N, K,
-                         lda, ldb, klen, tiles_m, tiles_n, direct);
+      hipLaunchKernelGGL((wgrad256_ring16o_kernel<BK2, 4>), dim3(nwg), dim3(512), lds, stream, a, b,
+                         grad.data_ptr<float>(), slab.defined() ? slab.data_ptr<float>() : nullptr, M, N, K, lda, ldb,
+                         tiles_m, tiles_n, wp);
   } else {
     hipLaunchKernelGGL(wgrad_kernel, dim3(nwg), dim3(256), 0, stream, a, b, dst, M, N, K, (int)dy.stride(0),
                        (int)x.stride(0), klen, tiles_m, tiles_n, direct);
+  }
+  if (wp.tail_splits > 0) {
+    const int64_t n4 = (int64_t)tail_tiles * T * T / 4;
+    hipLaunchKernelGGL(tile_slab_reduce_kernel, dim3((int)std::min<int64_t>((n4 + 255) / 256, 2048)), dim3(256), 0,
+                       stream, slab.data_ptr<float>(), grad.data_ptr<float>(), M, N, tiles_n, wp.main_tiles, tail_tiles,
+                       wp.tail_splits);
+    return;
   }
   if (splits == 1) return;
   const int64_t n4 = (int64_t)M * N / 4;
