@@ -347,7 +347,13 @@ __global__ void __launch_bounds__(512, 1) wgrad256_ring16o_kernel(const bf16* __
   const int m0 = tm * BM2, n0 = tn * BN2;
   const int k0 = split * klen, k1 = min(K, k0 + klen);
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = w >> 2, wn = w & 3;
+  // Half tiles (the last tile column of N = 1152 = 4.5 × 256, or the last tile row of M = 1152):
+  // the 8 waves are re-laid out over the 256 × 128 (4 × 2 waves) or 128 × 256 (2 × 4) part that
+  // exists, 64 × 64 outputs each, so every wave does useful MFMAs and the tile takes about half
+  // the time (with the full-tile layout half of the waves multiply clamped columns).
+  const int half = N - n0 <= 128 ? 1 : (M - m0 <= 128 ? 2 : 0);
+  const int wm = half == 1 ? w >> 1 : w >> 2, wn = half == 1 ? w & 1 : w & 3;
+  const int rspan = half ? 64 : 128;  // output rows per wave
 
   // DMA: piece i of wave w = tile rows 2(PIECES·w + i) + (lane>>5), 16-B chunk (lane&31) ^ swz
   const int rl = lane >> 5, pc = lane & 31;
@@ -388,7 +394,7 @@ __global__ void __launch_bounds__(512, 1) wgrad256_ring16o_kernel(const bf16* __
   unsigned fa[8], fb[4];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const int col = 128 * wm + 16 * i + p4;
+    const int col = rspan * wm + 16 * i + p4;
     fa[i] = (unsigned)(off512b(8 * g + q, col >> 3) + ((col & 4) << 1));
   }
 #pragma unroll
@@ -403,138 +409,143 @@ __global__ void __launch_bounds__(512, 1) wgrad256_ring16o_kernel(const bf16* __
     return uint4{ua.x, ua.y, ub.x, ub.y};
   };
 
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto run = [&](auto ni_c) {  // NI = 16-row fragment blocks per wave: 8 (full tile) or 4 (half)
+    constexpr int NI = decltype(ni_c)::value;
+    f32x4 acc[8][4];
+  #pragma unroll
+    for (int i = 0; i < NI; ++i)
+  #pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nsteps = (k1 - k0 + BKT - 1) / BKT;
-  // PF (fragment prefetch): each step's MFMAs run on fragments read during the PREVIOUS step, so
-  // no wave starts a step waiting on LDS reads after the barrier; the barrier at the end of step
-  // st must then publish stage st+2 (read during step st+1), leaving one stage in flight
-  constexpr int WAITN = PF ? (NBUF - 3) * G : (NBUF - 2) * G;
-#pragma unroll
-  for (int t = 0; t < NBUF - 1; ++t) dma(t);
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WAITN) : "memory");
-  __syncthreads();
-  constexpr int PFA = 2;  // A fragments read one step ahead
-  uint4 ca[PFA], cb[4];  // PF: the current step's prefetched fragments
-  if constexpr (PF) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) cb[j] = frag(smem2 + TILE, fb[j]);
-#pragma unroll
-    for (int i = 0; i < PFA; ++i) ca[i] = frag(smem2, fa[i]);
-  }
-  auto step = [&](int st, auto stage_tag) {
-    constexpr int ST = decltype(stage_tag)::value;
-    dma(st + NBUF - 1);  // into the stage consumed at step st-1 (freed by its barrier)
-    const char* At = smem2 + ST * 2 * TILE;
-    const char* Bt = At + TILE;
+    const int nsteps = (k1 - k0 + BKT - 1) / BKT;
+    // PF (fragment prefetch): each step's MFMAs run on fragments read during the PREVIOUS step, so
+    // no wave starts a step waiting on LDS reads after the barrier; the barrier at the end of step
+    // st must then publish stage st+2 (read during step st+1), leaving one stage in flight
+    constexpr int WAITN = PF ? (NBUF - 3) * G : (NBUF - 2) * G;
+  #pragma unroll
+    for (int t = 0; t < NBUF - 1; ++t) dma(t);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WAITN) : "memory");
+    __syncthreads();
+    constexpr int PFA = 2;  // A fragments read one step ahead
+    uint4 ca[PFA], cb[4];  // PF: the current step's prefetched fragments
     if constexpr (PF) {
-      // the B fragments and the first PFA A fragments come from the previous step; the other A
-      // fragments of this stage are read under those MFMAs, then next stage's prefetch is read
-      // under the rest (all 8 A fragments ahead would need 48 more VGPRs: 31 spilled)
-      const char* An = smem2 + ((ST + 1) % NBUF) * 2 * TILE;  // published by the previous barrier
-      uint4 la[8 - PFA];
-#pragma unroll
-      for (int i = PFA; i < 8; ++i) la[i - PFA] = frag(At, fa[i]);
-#pragma unroll
-      for (int i = 0; i < PFA; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(ca[i], cb[j], acc[i][j]);
-      uint4 nb[4], na[PFA];
-#pragma unroll
-      for (int i = PFA; i < 8; ++i) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(la[i - PFA], cb[j], acc[i][j]);
-        if (i == PFA) {
-#pragma unroll
-          for (int q = 0; q < PFA; ++q) na[q] = frag(An, fa[q]);
+  #pragma unroll
+      for (int j = 0; j < 4; ++j) cb[j] = frag(smem2 + TILE, fb[j]);
+  #pragma unroll
+      for (int i = 0; i < PFA; ++i) ca[i] = frag(smem2, fa[i]);
+    }
+    auto step = [&](int st, auto stage_tag) {
+      constexpr int ST = decltype(stage_tag)::value;
+      dma(st + NBUF - 1);  // into the stage consumed at step st-1 (freed by its barrier)
+      const char* At = smem2 + ST * 2 * TILE;
+      const char* Bt = At + TILE;
+      if constexpr (PF) {
+        // the B fragments and the first PFA A fragments come from the previous step; the other A
+        // fragments of this stage are read under those MFMAs, then next stage's prefetch is read
+        // under the rest (all 8 A fragments ahead would need 48 more VGPRs: 31 spilled)
+        const char* An = smem2 + ((ST + 1) % NBUF) * 2 * TILE;  // published by the previous barrier
+        uint4 la[NI - PFA];
+  #pragma unroll
+        for (int i = PFA; i < NI; ++i) la[i - PFA] = frag(At, fa[i]);
+  #pragma unroll
+        for (int i = 0; i < PFA; ++i)
+  #pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(ca[i], cb[j], acc[i][j]);
+        uint4 nb[4], na[PFA];
+  #pragma unroll
+        for (int i = PFA; i < NI; ++i) {
+  #pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(la[i - PFA], cb[j], acc[i][j]);
+          if (i == PFA) {
+  #pragma unroll
+            for (int q = 0; q < PFA; ++q) na[q] = frag(An, fa[q]);
+          }
+        }
+  #pragma unroll
+        for (int j = 0; j < 4; ++j) nb[j] = frag(An + TILE, fb[j]);
+  #pragma unroll
+        for (int i = 0; i < PFA; ++i) ca[i] = na[i];
+  #pragma unroll
+        for (int j = 0; j < 4; ++j) cb[j] = nb[j];
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WAITN) : "memory");  // stage st+2 landed
+        __syncthreads();
+        return;
+      }
+  #pragma unroll
+      for (int s = 0; s < BKT / 32; ++s) {
+        uint4 bf[4];
+  #pragma unroll
+        for (int j = 0; j < 4; ++j) bf[j] = frag(Bt + s * 32 * 512, fb[j]);
+  #pragma unroll
+        for (int i = 0; i < NI; ++i) {
+          const uint4 af = frag(At + s * 32 * 512, fa[i]);
+  #pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af, bf[j], acc[i][j]);
         }
       }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) nb[j] = frag(An + TILE, fb[j]);
-#pragma unroll
-      for (int i = 0; i < PFA; ++i) ca[i] = na[i];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) cb[j] = nb[j];
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WAITN) : "memory");  // stage st+2 landed
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NBUF - 2) * G) : "memory");  // stage st+1 landed
       __syncthreads();
+    };
+    int st = 0;
+    for (; st + NBUF <= nsteps; st += NBUF)  // unrolled by the ring depth: stage bases are immediates
+      unroll_steps<0, NBUF>([&](auto ic) { step(st + decltype(ic)::value, ic); });
+    unroll_steps<0, NBUF - 1>([&](auto ic) {
+      if (st + decltype(ic)::value < nsteps) step(st + decltype(ic)::value, ic);
+    });
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the zero-page prefetches
+    // main tiles: direct read-add-write (one split) or a full-size slab per split; tail tiles: a
+    // packed [256][256] slab per (split, tail tile), added by tile_slab_reduce_kernel
+    const bool direct = !in_tail && plan.main_splits == 1;
+    float* const obase = direct ? grad : slab;
+    const int64_t ld = in_tail ? BN2 : N;  // element (m, n) sits at obase[ob + m·ld + n]
+    const int64_t ob = direct ? 0
+                       : in_tail ? ((int64_t)split * nt + tail_i) * (BM2 * BN2) - (int64_t)m0 * BN2 - n0
+                                 : (int64_t)split * M * N;
+    if (direct) {
+      // read-add-write in groups of 16 values: every read of a group is issued before its writes
+      // (written element by element, the compiler must assume each write may alias the next read
+      // and serialises 128 memory round trips per lane: 1.0 ms of a 4.0 ms lm_head wgrad)
+  #pragma unroll
+      for (int i0 = 0; i0 < NI; ++i0) {
+        float cur[1][4][4];
+  #pragma unroll
+        for (int ii = 0; ii < 1; ++ii)
+  #pragma unroll
+          for (int j = 0; j < 4; ++j)
+  #pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int n = n0 + 64 * wn + 16 * j + (lane & 15);
+              const int m = m0 + rspan * wm + 16 * (i0 + ii) + 4 * g + r;
+              cur[ii][j][r] = (m < M && n < N) ? grad[(int64_t)m * N + n] : 0.f;
+            }
+  #pragma unroll
+        for (int ii = 0; ii < 1; ++ii)
+  #pragma unroll
+          for (int j = 0; j < 4; ++j)
+  #pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int n = n0 + 64 * wn + 16 * j + (lane & 15);
+              const int m = m0 + rspan * wm + 16 * (i0 + ii) + 4 * g + r;
+              if (m < M && n < N) grad[(int64_t)m * N + n] = cur[ii][j][r] + acc[i0 + ii][j][r];
+            }
+      }
       return;
     }
-#pragma unroll
-    for (int s = 0; s < BKT / 32; ++s) {
-      uint4 bf[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bf[j] = frag(Bt + s * 32 * 512, fb[j]);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const uint4 af = frag(At + s * 32 * 512, fa[i]);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af, bf[j], acc[i][j]);
+  #pragma unroll
+    for (int i = 0; i < NI; ++i)
+  #pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + 64 * wn + 16 * j + (lane & 15);
+        if (n >= N) continue;
+  #pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + rspan * wm + 16 * i + 4 * g + r;
+          if (m < M) obase[ob + (int64_t)m * ld + n] = acc[i][j][r];
+        }
       }
-    }
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NBUF - 2) * G) : "memory");  // stage st+1 landed
-    __syncthreads();
   };
-  int st = 0;
-  for (; st + NBUF <= nsteps; st += NBUF)  // unrolled by the ring depth: stage bases are immediates
-    unroll_steps<0, NBUF>([&](auto ic) { step(st + decltype(ic)::value, ic); });
-  unroll_steps<0, NBUF - 1>([&](auto ic) {
-    if (st + decltype(ic)::value < nsteps) step(st + decltype(ic)::value, ic);
-  });
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the zero-page prefetches
-  // main tiles: direct read-add-write (one split) or a full-size slab per split; tail tiles: a
-  // packed [256][256] slab per (split, tail tile), added by tile_slab_reduce_kernel
-  const bool direct = !in_tail && plan.main_splits == 1;
-  float* const obase = direct ? grad : slab;
-  const int64_t ld = in_tail ? BN2 : N;  // element (m, n) sits at obase[ob + m·ld + n]
-  const int64_t ob = direct ? 0
-                     : in_tail ? ((int64_t)split * nt + tail_i) * (BM2 * BN2) - (int64_t)m0 * BN2 - n0
-                               : (int64_t)split * M * N;
-  if (direct) {
-    // read-add-write in groups of 16 values: every read of a group is issued before its writes
-    // (written element by element, the compiler must assume each write may alias the next read
-    // and serialises 128 memory round trips per lane: 1.0 ms of a 4.0 ms lm_head wgrad)
-#pragma unroll
-    for (int i0 = 0; i0 < 8; ++i0) {
-      float cur[1][4][4];
-#pragma unroll
-      for (int ii = 0; ii < 1; ++ii)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int n = n0 + 64 * wn + 16 * j + (lane & 15);
-            const int m = m0 + 128 * wm + 16 * (i0 + ii) + 4 * g + r;
-            cur[ii][j][r] = (m < M && n < N) ? grad[(int64_t)m * N + n] : 0.f;
-          }
-#pragma unroll
-      for (int ii = 0; ii < 1; ++ii)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int n = n0 + 64 * wn + 16 * j + (lane & 15);
-            const int m = m0 + 128 * wm + 16 * (i0 + ii) + 4 * g + r;
-            if (m < M && n < N) grad[(int64_t)m * N + n] = cur[ii][j][r] + acc[i0 + ii][j][r];
-          }
-    }
-    return;
-  }
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + 64 * wn + 16 * j + (lane & 15);
-      if (n >= N) continue;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + 128 * wm + 16 * i + 4 * g + r;
-        if (m < M) obase[ob + (int64_t)m * ld + n] = acc[i][j][r];
-      }
-    }
+  if (half) run(std::integral_constant<int, 4>{});
+  else run(std::integral_constant<int, 8>{});
 }
 
 // G[e] += Σ_s slab[s][e]  (vectorised, fixed order)

@@ -625,11 +625,13 @@ def test_tensor_stats():
 
 @pytest.mark.parametrize("tile,variant", [(128, 0), (256, 4), (256, 6), (256, 8)])
 @pytest.mark.parametrize("K,M,N", [(65536, 2304, 768), (4096, 768, 768), (1000, 200, 136), (8192, 50304, 768), (3000, 1600, 6400),
-                                   (4096, 13816, 1144), (1000, 13824, 1152)])
+                                   (4096, 13816, 1144), (1000, 13824, 1152), (512, 1104, 1096)])
 def test_wgrad_gemm(K, M, N, tile, variant):
     """(8192, 50304, 768), (4096, 13816, 1144), (1000, 13824, 1152): split-tail plans for the ring16o
     variants (full rounds direct, the last round's tiles split along K into per-tile slabs), with
-    ragged tail tiles and a ragged K."""
+    ragged tail tiles and a ragged K. Half tiles (<= 128 live columns or rows: the re-laid-out
+    4 x 2 / 2 x 4 waves): N = 1144 / 1152 / 1096, M = 1600 / 50304 / 1104 (1104 x 1096: a corner tile
+    that is half in both)."""
     from penroz.ops import gemm as G
     torch.manual_seed(0)
     dy = torch.randn(K, M, device=DEV).to(torch.bfloat16)
