@@ -84,7 +84,7 @@ void decode_ln_gemm(torch::Tensor resid, torch::Tensor gamma, torch::Tensor beta
 void decode_gemm_acc(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> bias, torch::Tensor resid,
                      int64_t flags);
 // gemm_wgrad.hip
-void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad, int64_t tile, int64_t variant);
+void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad, int64_t tile, int64_t variant, bool accumulate);
 // flash_attn.hip
 void flash_attn_fwd(torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int64_t H, int64_t Hkv, int64_t D,
                     double scale, double p_drop, int64_t seed);
@@ -176,7 +176,8 @@ PYBIND11_MODULE(penroz_kernels, m) {
         pybind11::arg("resid"), pybind11::arg("flags") = 0,
         "batched decode: resid += x·wᵀ + bias (fp32 residual, in place)");
   m.def("wgrad_gemm", &wgrad_gemm, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("grad"),
-        pybind11::arg("tile") = 256, pybind11::arg("variant") = 8);
+        pybind11::arg("tile") = 256, pybind11::arg("variant") = 8, pybind11::arg("accumulate") = true,
+        "grad (+)= dyᵀ·x (fp32 gradient, bf16 operands); accumulate=False overwrites grad");
   m.def("flash_attn_fwd", &flash_attn_fwd);
   m.def("flash_fwd_variant", &flash_fwd_variant, pybind11::arg("variant") = 0,
         "select the forward kernel (1 single-stage, 2 tile-pipelined); returns the previous one");

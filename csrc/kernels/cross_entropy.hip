@@ -104,22 +104,26 @@ __global__ void __launch_bounds__(kCEThreads) ce_loop_kernel(T* __restrict__ log
   T* gp = gout ? gout + (size_t)row * ld : rp;
   const int64_t tgt = targets[row];
   PZ_DEVICE_CHECK(tgt == ignore_index || (tgt >= 0 && tgt < V));
-  float m = -INFINITY;
+  // one pass for max and sum (online: the running sum is rescaled when the running max grows),
+  // so the row is read twice in all (here and for the gradient) instead of three times —
+  // Gemma's 262k-token rows are 512 KB each, beyond what the L2 keeps between passes
+  float m = -INFINITY, s = 0.f;
   for (int c = 8 * threadIdx.x; c < V; c += 8 * kCEThreads) {
     float v[8];
     Vec8<T>::load(rp + c, v);
+    float cm = -INFINITY;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) m = fmaxf(m, c + j < V ? v[j] : -INFINITY);
-  }
-  m = block_reduce(m, sh, true);
-  float s = 0.f;
-  for (int c = 8 * threadIdx.x; c < V; c += 8 * kCEThreads) {
-    float v[8];
-    Vec8<T>::load(rp + c, v);
+    for (int j = 0; j < 8; ++j) cm = fmaxf(cm, c + j < V ? v[j] : -INFINITY);
+    if (cm > m) {
+      s *= __expf(m - cm);  // m = -inf: s is 0 and stays 0
+      m = cm;
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) s += c + j < V ? __expf(v[j] - m) : 0.f;
   }
-  s = block_reduce(s, sh, false);
+  const float mb = block_reduce(m, sh, true);
+  s = block_reduce(m == -INFINITY ? 0.f : s * __expf(m - mb), sh, false);
+  m = mb;
   const float lse = m + __logf(s);
   const bool valid = tgt != ignore_index && tgt >= 0 && tgt < V;
   if (threadIdx.x == 0) loss[row] = valid ? lse - to_f(rp[tgt]) : 0.f;

@@ -318,7 +318,7 @@ __global__ void __launch_bounds__(512, 1) wgrad256_ring16o_kernel(const bf16* __
                                                                   const bf16* __restrict__ B,
                                                                   float* __restrict__ grad, float* __restrict__ slab,
                                                                   int M, int N, int K, int lda, int ldb, int tiles_m,
-                                                                  int tiles_n, WgradPlan plan) {
+                                                                  int tiles_n, WgradPlan plan, int acc_in) {
   extern __shared__ __attribute__((aligned(16))) char smem2[];  // [NBUF][A|B][BKT * 512]
   constexpr int TILE = BKT * 512;
   constexpr int PIECES = BKT / 16;
@@ -516,7 +516,7 @@ __global__ void __launch_bounds__(512, 1) wgrad256_ring16o_kernel(const bf16* __
             for (int r = 0; r < 4; ++r) {
               const int n = n0 + 64 * wn + 16 * j + (lane & 15);
               const int m = m0 + rspan * wm + 16 * (i0 + ii) + 4 * g + r;
-              cur[ii][j][r] = (m < M && n < N) ? grad[(int64_t)m * N + n] : 0.f;
+              cur[ii][j][r] = (acc_in && m < M && n < N) ? grad[(int64_t)m * N + n] : 0.f;
             }
   #pragma unroll
         for (int ii = 0; ii < 1; ++ii)
@@ -550,9 +550,9 @@ __global__ void __launch_bounds__(512, 1) wgrad256_ring16o_kernel(const bf16* __
 
 // G[e] += Σ_s slab[s][e]  (vectorised, fixed order)
 __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restrict__ slab, float* __restrict__ g,
-                                                          int64_t n4, int splits, int64_t stride4) {
+                                                          int64_t n4, int splits, int64_t stride4, int acc_in) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-    float4_t acc = reinterpret_cast<float4_t*>(g)[i];
+    float4_t acc = acc_in ? reinterpret_cast<float4_t*>(g)[i] : float4_t{0.f, 0.f, 0.f, 0.f};
     for (int s = 0; s < splits; ++s) acc += reinterpret_cast<const float4_t*>(slab)[s * stride4 + i];
     reinterpret_cast<float4_t*>(g)[i] = acc;
   }
@@ -562,7 +562,7 @@ __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restric
 // [256][256] fp32 per (split, tile); fixed order, so the result is bitwise reproducible)
 __global__ void __launch_bounds__(256) tile_slab_reduce_kernel(const float* __restrict__ slab, float* __restrict__ g,
                                                                int M, int N, int tiles_n, int first_tile, int nt,
-                                                               int splits) {
+                                                               int splits, int acc_in) {
   constexpr int T4 = BM2 * BN2 / 4;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < (int64_t)nt * T4;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -572,7 +572,7 @@ __global__ void __launch_bounds__(256) tile_slab_reduce_kernel(const float* __re
     const int m = tm * BM2 + r, n = tn * BN2 + c;
     if (m >= M || n >= N) continue;  // N % 8 == 0: n < N covers n + 3
     float4_t* gp = reinterpret_cast<float4_t*>(g + (size_t)m * N + n);
-    float4_t acc = *gp;
+    float4_t acc = acc_in ? *gp : float4_t{0.f, 0.f, 0.f, 0.f};
     for (int s = 0; s < splits; ++s)
       acc += reinterpret_cast<const float4_t*>(slab + ((size_t)s * nt + ti) * (BM2 * BN2))[e];
     *gp = acc;
@@ -586,7 +586,7 @@ using namespace penroz;
 
 // grad[M][N] += dyᵀ·x with dy [K, M], x [K, N] (bf16, row-major, contiguous rows).
 // tile = 256 (default, 8 waves) or 128 (4 waves); variant selects the 256-tile pipeline (see below).
-void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad, int64_t tile, int64_t variant) {
+void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad, int64_t tile, int64_t variant, bool accumulate) {
   TORCH_CHECK(dy.is_cuda() && x.is_cuda() && grad.is_cuda());
   TORCH_CHECK(dy.scalar_type() == torch::kBFloat16 && x.scalar_type() == torch::kBFloat16 &&
               grad.scalar_type() == torch::kFloat32, "wgrad: bf16 operands, fp32 gradient");
@@ -605,7 +605,10 @@ void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad, int64_t t
                                                              Mp) * 2,
               "wgrad: dy's last row padding must be allocated");
   TORCH_CHECK(tile == 128 || tile == 256, "wgrad: tile must be 128 or 256");
-  if (K == 0) return;
+  if (K == 0) {
+    if (!accumulate) grad.zero_();
+    return;
+  }
   const int T = (int)tile;
   const int tiles_m = (M + T - 1) / T, tiles_n = (N + T - 1) / T;
   const int ntiles = tiles_m * tiles_n;
@@ -638,6 +641,10 @@ void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad, int64_t t
     slab = torch::empty({(int64_t)wp.tail_splits * tail_tiles * T * T}, grad.options());
   }
   const int direct = splits == 1 ? 1 : 0;
+  // overwrite (accumulate = false: the first micro-step after a zero-free zero_grad): the ring16o
+  // variants and the slab reductions write instead of read-add-write; the others zero first
+  if (!accumulate && !ring16o) grad.zero_();
+  const int acc_in = accumulate || !ring16o ? 1 : 0;
   if (T == 256) {
     // variant 6: ring16o; 4: ring16 (per-lane 64-bit DMA addresses and fragment
     // address math in the loop; kept for A/B). v4 / v6 (TF): qkv 879/959, proj 822/914,
@@ -665,11 +672,11 @@ void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad, int64_t t
     else if (variant == 8)
       hipLaunchKernelGGL((wgrad256_ring16o_kernel<BK2, 4, true>), dim3(nwg), dim3(512), lds, stream, a, b,
                          grad.data_ptr<float>(), slab.defined() ? slab.data_ptr<float>() : nullptr, M, N, K, lda, ldb,
-                         tiles_m, tiles_n, wp);
+                         tiles_m, tiles_n, wp, acc_in);
     else
       hipLaunchKernelGGL((wgrad256_ring16o_kernel<BK2, 4>), dim3(nwg), dim3(512), lds, stream, a, b,
                          grad.data_ptr<float>(), slab.defined() ? slab.data_ptr<float>() : nullptr, M, N, K, lda, ldb,
-                         tiles_m, tiles_n, wp);
+                         tiles_m, tiles_n, wp, acc_in);
   } else {
     hipLaunchKernelGGL(wgrad_kernel, dim3(nwg), dim3(256), 0, stream, a, b, dst, M, N, K, (int)dy.stride(0),
                        (int)x.stride(0), klen, tiles_m, tiles_n, direct);
@@ -678,11 +685,11 @@ void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad, int64_t t
     const int64_t n4 = (int64_t)tail_tiles * T * T / 4;
     hipLaunchKernelGGL(tile_slab_reduce_kernel, dim3((int)std::min<int64_t>((n4 + 255) / 256, 2048)), dim3(256), 0,
                        stream, slab.data_ptr<float>(), grad.data_ptr<float>(), M, N, tiles_n, wp.main_tiles, tail_tiles,
-                       wp.tail_splits);
+                       wp.tail_splits, acc_in);
     return;
   }
   if (splits == 1) return;
   const int64_t n4 = (int64_t)M * N / 4;
   hipLaunchKernelGGL(slab_reduce_kernel, dim3((int)std::min<int64_t>((n4 + 255) / 256, 2048)), dim3(256), 0, stream,
-                     slab.data_ptr<float>(), grad.data_ptr<float>(), n4, splits, n4);
+                     slab.data_ptr<float>(), grad.data_ptr<float>(), n4, splits, n4, acc_in);
 }

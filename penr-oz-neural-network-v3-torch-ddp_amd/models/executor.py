@@ -478,9 +478,42 @@ class GPTExecutor:
         self.reducer = None
 
     def zero_grad(self):
+        """Zero the gradients. Once a backward has shown which flat ranges only the weight-gradient
+        GEMMs write (the linear weights: most of the buffer), those are left alone and the first
+        GEMM into each writes instead of accumulating (``gemm_ops.wgrad(accumulate=False)``), so
+        the step neither clears them nor reads them back (PENROZ_GRAD_OVERWRITE=0: clear all)."""
         self.wait_gradients()
-        self.flat_grad.zero_()
+        gaps = getattr(self, "_zero_gaps", None)
+        if gaps is not None:
+            if getattr(self, "_zero_views_of", None) is not self.flat_grad:  # views of THIS buffer
+                self._zero_views = [self.flat_grad[a:b] for a, b in gaps]
+                self._zero_views_of = self.flat_grad
+            torch._foreach_zero_(self._zero_views)
+            self._fresh = set(self._wgrad_ranges)
+        else:
+            self.flat_grad.zero_()
+            self._fresh = set()
         self._captured = None
+
+    def _learn_wgrad_ranges(self):
+        """After the first backward: the flat ranges outside the weight-gradient GEMMs' outputs,
+        as views for one multi-tensor zero (neighbouring ranges merged)."""
+        import os
+        self._zero_gaps = None
+        if (os.environ.get("PENROZ_GRAD_OVERWRITE", "1") == "0" or self.device.type != "cuda"
+                or not getattr(self, "_wgrad_ranges", None)):
+            return
+        covered = sorted(self._wgrad_ranges.values())
+        gaps, pos = [], 0
+        for s, e in covered:
+            if s < pos:  # overlapping outputs: not a partition, keep clearing everything
+                return
+            if s > pos:
+                gaps.append((pos, s))
+            pos = e
+        if pos < self.flat_grad.numel():
+            gaps.append((pos, self.flat_grad.numel()))
+        self._zero_gaps = gaps
 
     def _segment_done(self, seg_index: int, sync: bool):
         if self._opt_apply is not None and sync:
@@ -545,7 +578,36 @@ class GPTExecutor:
         self._buf_free[operand.data_ptr()] = done
 
     def _wgrad(self, dy: Tensor, x: Tensor, p: Tensor):
-        self._side_call(dy, lambda: gemm_ops.wgrad(dy, x, self.grad(p)))
+        self._wgrad_into(id(p), dy, x, self.grad(p))
+
+    def _wgrad_into(self, key: int, dy: Tensor, x: Tensor, g: Tensor):
+        """g (+)= dyᵀ·x on the side stream: the first write of a range that zero_grad left alone
+        overwrites it; the ranges are recorded during the first backward (see zero_grad)."""
+        fresh = getattr(self, "_fresh", None)
+        acc = not (fresh and key in fresh)
+        if not acc:
+            fresh.discard(key)
+        rec = getattr(self, "_wgrad_ranges", None)
+        if rec is None:
+            rec = self._wgrad_ranges = {}
+        if not getattr(self, "_ranges_learned", False):
+            off = g.data_ptr() - self.flat_grad.data_ptr()
+            rec[key] = (off // 4, off // 4 + g.numel())
+        self._side_call(dy, lambda: gemm_ops.wgrad(dy, x, g, acc))
+
+    def _finish_wgrad_bookkeeping(self):
+        """End of a backward: learn the ranges once; clear any range zero_grad skipped that no GEMM
+        wrote (not expected: every backward writes every linear weight's gradient)."""
+        if not getattr(self, "_ranges_learned", False):
+            self._ranges_learned = True
+            self._learn_wgrad_ranges()
+        fresh = getattr(self, "_fresh", None)
+        if fresh:
+            log.warning(f"weight-gradient ranges not written by this backward: {len(fresh)}; clearing them")
+            for key in list(fresh):
+                s_, e_ = self._wgrad_ranges[key]
+                self.flat_grad[s_:e_].zero_()
+            fresh.clear()
 
     def _defer_reductions(self, on: bool):
         """LayerNorm / bias column-reduction finishing kernels go to the side stream (on) or not."""
@@ -675,6 +737,7 @@ class GPTExecutor:
                                 s.wpe.position_offset, dropout_p=s.p_embd, dropout_seed=_site_seed(seed, -1))
         self._segment_done(self.L + 1, sync)
         self._defer_reductions(False)
+        self._finish_wgrad_bookkeeping()
         self._join_side()
         if sync and self.reducer is not None:
             # Overlap the tail: the last bucket (token embedding, produced by the final kernel of

@@ -429,7 +429,7 @@ class GemmaExecutor(GPTExecutor):
             dgu = self._reuse(self.d_gu2[l & 1])
             k.gated_act_bwd_packed(self.d_g, self.gu[l], dgu, s.act)
             torch.mm(dgu, self._dgrad(b.mlp.gate_proj.weight, self.gu_bf16(b)), out=self.d_c)
-            self._side_call(dgu, lambda dgu=dgu, l=l, b=b: gemm_ops.wgrad(dgu, self.y_mlp[l], self.gu_grad(b)))
+            self._wgrad_into(id(b.mlp.gate_proj.weight), dgu, self.y_mlp[l], self.gu_grad(b))
             # ---- attention combine: dy = d(pre-MLP norm output), dh_in = dresid (grad of mid[l])
             pa = b.post_attn
             rb ^= 1
@@ -471,6 +471,7 @@ class GemmaExecutor(GPTExecutor):
         gw.index_add_(0, idx.reshape(-1), self.dresid, alpha=float(s.emb.scale))
         self._segment_done(self.L + 1, sync)
         self._defer_reductions(False)
+        self._finish_wgrad_bookkeeping()
         self._join_side()
         if sync and self.reducer is not None:
             self.reducer.launch_remaining()

@@ -29,18 +29,24 @@ def _native_ok(m: int, n: int, lda: int | None = None) -> bool:
     return NATIVE_WGRAD != "0" and n % 8 == 0 and (m % 8 == 0 or (lda is not None and lda >= (m + 7) // 8 * 8))
 
 
-def reference_wgrad(dy: Tensor, x: Tensor, grad: Tensor) -> None:
-    grad.add_(dy.float().t() @ x.float())
+def reference_wgrad(dy: Tensor, x: Tensor, grad: Tensor, accumulate: bool = True) -> None:
+    if accumulate:
+        grad.add_(dy.float().t() @ x.float())
+    else:
+        grad.copy_(dy.float().t() @ x.float())
 
 
-def wgrad(dy: Tensor, x: Tensor, grad: Tensor) -> None:
+def wgrad(dy: Tensor, x: Tensor, grad: Tensor, accumulate: bool = True) -> None:
+    """grad += dyᵀ·x, or grad = dyᵀ·x with accumulate=False (the first weight-gradient write of a
+    step whose zero_grad skipped this range)."""
     if (use_kernels(dy) and _native_ok(dy.shape[1], x.shape[1], dy.stride(0)) and dy.dtype == torch.bfloat16
             and x.dtype == torch.bfloat16 and dy.stride(0) % 8 == 0 and x.stride(0) % 8 == 0):
-        kernels().wgrad_gemm(dy, x, grad, 256, WGRAD_VARIANT)
+        kernels().wgrad_gemm(dy, x, grad, 256, WGRAD_VARIANT, accumulate)
     elif dy.is_cuda:
-        grad.add_(torch.mm(dy.t(), x, out_dtype=torch.float32))
+        prod = torch.mm(dy.t(), x, out_dtype=torch.float32)
+        grad.add_(prod) if accumulate else grad.copy_(prod)
     else:
-        reference_wgrad(dy, x, grad)
+        reference_wgrad(dy, x, grad, accumulate)
 
 
 # ---- library GEMM solution choice (hipBLASLt / rocBLAS through torch) -----------------------
