@@ -38,6 +38,7 @@
 // the identical mask; the softmax normaliser uses the undropped probabilities (SDPA
 // semantics).
 #include "attn_common.h"
+#include <cstdlib>
 #include "deferred.h"
 #include <type_traits>
 #include <torch/extension.h>
@@ -745,9 +746,9 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv3_kernel(const bf16* __rest
 template <bool DROPOUT, int NST>
 __global__ void __launch_bounds__(256, 2) fa_bwd_dq4_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                                         const float* __restrict__ lse,
-                                                        const float* __restrict__ delta, bf16* __restrict__ dqkv, float* __restrict__ cpart,
+                                                        float* __restrict__ delta, bf16* __restrict__ dqkv, float* __restrict__ cpart,
                                                         int T, int H, int Hkv, float scale, float p_drop,
-                                                        uint64_t seed) {
+                                                        uint64_t seed, const bf16* __restrict__ out) {
   constexpr int BM = 128, BN = 64;
   __shared__ __attribute__((aligned(16))) char smem[NST][2][BN * 128];
   const int nqb = (T + BM - 1) / BM;
@@ -781,7 +782,30 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dq4_kernel(const bf16* __restri
   }
   const size_t rr = ((size_t)b * H + h) * T + qrow;
   float l2 = qok ? lse[rr] * kLog2e : 0.f;
-  float dl = qok ? delta[rr] : 0.f;
+  float dl;
+  if (out != nullptr) {
+    // δ = Σ_d dO·O of this row, from the dO fragments already in registers and the matching O
+    // fragments (lanes l and l + 32 hold the two halves of a row); written for the dK/dV kernel,
+    // which runs after this one — no separate pre-pass over dO and O
+    float sum = 0.f;
+    if (qok) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const uint4 o4 = *reinterpret_cast<const uint4*>(out + (size_t)b * T * ORS + (size_t)h * kD +
+                                                         (size_t)qrow * ORS + 16 * s + 8 * hh);
+        const uint32_t ow[4] = {o4.x, o4.y, o4.z, o4.w}, dw[4] = {dof[s].x, dof[s].y, dof[s].z, dof[s].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          sum += __uint_as_float(ow[k] << 16) * __uint_as_float(dw[k] << 16) +
+                 __uint_as_float(ow[k] & 0xffff0000u) * __uint_as_float(dw[k] & 0xffff0000u);
+      }
+    }
+    sum += __shfl_xor(sum, 32, 64);
+    dl = sum;
+    if (qok && hh == 0) delta[rr] = sum;
+  } else {
+    dl = qok ? delta[rr] : 0.f;
+  }
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     qf[s] = scale_bf16x8(qf[s], c);  // S = (cQ)·Kᵀ (see scale_bf16x8); dQ uses K, not Q
@@ -987,18 +1011,29 @@ void flash_attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, to
   if (B == 0 || T == 0) return;
   auto delta = torch::empty({B, H, T}, qkv.options().dtype(torch::kFloat32));
   auto stream = at::hip::getCurrentHIPStream();
-  const int rows = B * T * H;
-  hipLaunchKernelGGL(fa_bwd_pre_kernel, dim3((rows * 8 + 255) / 256), dim3(256), 0, stream,
-                     reinterpret_cast<const bf16*>(dout.data_ptr()), reinterpret_cast<const bf16*>(out.data_ptr()),
-                     delta.data_ptr<float>(), B, T, (int)H);
+  // δ = rowsum(dO·O) is computed by the dQ kernel from the dO fragments it loads anyway and written
+  // for the dK/dV kernel, so dQ runs first (PENROZ_FA_DELTA_PREPASS=1: the separate pre-pass)
+  static const bool prepass = [] {
+    const char* e = std::getenv("PENROZ_FA_DELTA_PREPASS");
+    return e && e[0] == '1';
+  }();
+  if (prepass) {
+    const int rows = B * T * H;
+    hipLaunchKernelGGL(fa_bwd_pre_kernel, dim3((rows * 8 + 255) / 256), dim3(256), 0, stream,
+                       reinterpret_cast<const bf16*>(dout.data_ptr()), reinterpret_cast<const bf16*>(out.data_ptr()),
+                       delta.data_ptr<float>(), B, T, (int)H);
+  }
   const bf16* q = reinterpret_cast<const bf16*>(qkv.data_ptr());
   const bf16* d = reinterpret_cast<const bf16*>(dout.data_ptr());
   bf16* g = reinterpret_cast<bf16*>(dqkv.data_ptr());
   dim3 gkv((T + 127) / 128, B * Hkv), gq((T + 127) / 128, B * H);
   using BwdKernel = void (*)(const bf16*, const bf16*, const float*, const float*, bf16*, float*, int, int, int, float, float,
                             uint64_t);
+  using DqKernel = void (*)(const bf16*, const bf16*, const float*, float*, bf16*, float*, int, int, int, float, float,
+                            uint64_t, const bf16*);
   const bool drop = p_drop > 0.0;
-  BwdKernel kv, dq;
+  BwdKernel kv;
+  DqKernel dq;
   kv = drop ? fa_bwd_dkdv3_kernel<true, 3> : fa_bwd_dkdv3_kernel<false, 3>;
   dq = drop ? fa_bwd_dq4_kernel<true, 3> : fa_bwd_dq4_kernel<false, 3>;
   const float pd = drop ? (float)p_drop : 0.f;
@@ -1010,9 +1045,10 @@ void flash_attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, to
   torch::Tensor part;
   if (want_bias) part = torch::empty({(int64_t)B * nblk * 4, W}, qkv.options().dtype(torch::kFloat32));
   float* pp = want_bias ? part.data_ptr<float>() : nullptr;
-  hipLaunchKernelGGL(kv, gkv, dim3(256), 0, stream, q, d, lse.data_ptr<float>(), delta.data_ptr<float>(), g, pp, T,
-                     (int)H, (int)Hkv, (float)scale, pd, (uint64_t)seed);
   hipLaunchKernelGGL(dq, gq, dim3(256), 0, stream, q, d, lse.data_ptr<float>(), delta.data_ptr<float>(), g, pp, T,
+                     (int)H, (int)Hkv, (float)scale, pd, (uint64_t)seed,
+                     prepass ? nullptr : reinterpret_cast<const bf16*>(out.data_ptr()));
+  hipLaunchKernelGGL(kv, gkv, dim3(256), 0, stream, q, d, lse.data_ptr<float>(), delta.data_ptr<float>(), g, pp, T,
                      (int)H, (int)Hkv, (float)scale, pd, (uint64_t)seed);
   if (want_bias) {
     float* outs[1] = {dbias->data_ptr<float>()};

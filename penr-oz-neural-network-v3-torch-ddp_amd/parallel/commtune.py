@@ -20,12 +20,15 @@ job's own group, outside any timed region:
 from __future__ import annotations
 
 import glob
+import logging
 import os
 import re
 import time
 
 import torch
 import torch.distributed as dist
+
+log = logging.getLogger(__name__)
 
 SWEEP_SIZES_MB = (16, 32, 64, 128, 256)
 _LOG_DIR = "/tmp"
@@ -86,7 +89,10 @@ def _native_or_none(device):
     """The C++ communicator on every rank, or None on every rank (agreed over the c10d group)."""
     ok = torch.zeros(1, device=device)
     native = None
-    if device.type == "cuda" and os.environ.get("PENROZ_COMM_SWEEP_NATIVE", "1") != "0":
+    # only where it can work: RCCL ranks (a gloo rehearsal of several ranks on one GPU makes RCCL
+    # refuse the duplicate device — "invalid usage" — which must not end the run) on distinct GPUs
+    if (device.type == "cuda" and os.environ.get("PENROZ_COMM_SWEEP_NATIVE", "1") != "0"
+            and dist.get_backend() == "nccl"):
         try:
             from penroz.parallel import rccl
             rccl.load_module()
@@ -94,6 +100,10 @@ def _native_or_none(device):
         except Exception:  # module missing on this rank: nobody builds a communicator
             pass
     dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if ok.item() > 0:
+        ids = [(d.get("host"), d.get("pci"), d.get("uuid")) for d in gather_identities(device)]
+        if len(set(ids)) != len(ids):
+            ok.zero_()
     if ok.item() > 0:
         import threading
         from penroz.parallel import rccl
@@ -103,10 +113,17 @@ def _native_or_none(device):
         guard = threading.Timer(dist_timeout_s(), lambda: os._exit(124))
         guard.daemon = True
         guard.start()
+        built = torch.zeros(1, device=device)
         try:
             native = rccl.NativeComm.get()
+            built += 1
+        except RuntimeError as e:  # refused right away on this rank: everybody falls back to c10d
+            log.warning(f"native RCCL communicator unavailable: {e}")
         finally:
             guard.cancel()
+        dist.all_reduce(built, op=dist.ReduceOp.MIN)
+        if built.item() == 0:
+            native = None
     return native
 
 
