@@ -2,7 +2,11 @@
 
 Prints one JSON line per measurement: GPT-2 124M shapes at B=64, T=1024.
 """
-import json, math, sys, time, os
+import json
+import math
+import os
+import sys
+import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 import torch.nn.functional as F
@@ -62,6 +66,8 @@ if "adam" in which:
     sh = torch.empty(n, device="cuda", dtype=torch.bfloat16)
     t = timeit(lambda: k.adamw_step(p, g, m, v, sh, 6e-4, 0.9, 0.95, 1e-8, 0.01, 10, 1.0, False))
     emit(kernel="adamw_flat", n=n, us=round(t * 1e6, 1), TBps=round(30 * n / t / 1e12, 2))
+    t = timeit(lambda: p.copy_(g))  # the same kind of traffic: 1 read + 1 write stream of fp32
+    emit(kernel="torch_copy_fp32", n=n, us=round(t * 1e6, 1), TBps=round(8 * n / t / 1e12, 2))
 if "stream" in which:
     # memory-bound streams at the fc activation shape [65536, 3072] bf16: GELU forward (read +
     # write), GELU backward fused with the fc bias-gradient column sum (2 reads + 1 write), the
