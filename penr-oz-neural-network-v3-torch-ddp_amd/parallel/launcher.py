@@ -11,6 +11,12 @@ design:
   * a monitor polls worker exit codes; the first failure tears the group down and is
     *returned* (and reported through ``on_failure``) so the caller can mark the model
     ``Error`` instead of leaving it ``Training`` forever (reference bug 9);
+  * rendezvous on the loopback interface: 127.0.0.1 on Linux; off Linux (macOS / Windows
+    development boxes) the address family that actually works — ``::1`` when an IPv6 loopback
+    socket connects, else 127.0.0.1 — with ``GLOO_USE_IPV6`` (and ``GLOO_SOCKET_IFNAME=lo0`` for
+    IPv6 on macOS) set to match, as the reference does (``ddp.py:22-36, 59-68``); ``mps`` runs
+    get ``PYTORCH_ENABLE_MPS_FALLBACK=1`` so collectives MPS lacks fall back to the CPU
+    (``ddp.py:39-42``);
   * fault injection for tests: ``PENROZ_FAULT_RANK`` / ``PENROZ_FAULT_STEP`` make that rank
     exit with code 13 at that training step (checked in the runtime's loop).
 """
@@ -21,6 +27,7 @@ import multiprocessing as mp
 from multiprocessing import connection as mp_connection
 import os
 import socket
+import sys
 import time
 import traceback
 from typing import Callable
@@ -33,9 +40,40 @@ FAULT_EXIT_CODE = 13
 
 
 def free_port(host: str = "127.0.0.1") -> int:
-    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+    family = socket.AF_INET6 if ":" in host else socket.AF_INET
+    with socket.socket(family, socket.SOCK_STREAM) as s:
         s.bind((host, 0))
         return s.getsockname()[1]
+
+
+def detect_active_ip_family() -> str:
+    """"ipv6" when a datagram socket can be connected to the IPv6 loopback, else "ipv4"."""
+    if not socket.has_ipv6:
+        return "ipv4"
+    try:
+        with socket.socket(socket.AF_INET6, socket.SOCK_DGRAM) as s:
+            s.settimeout(0.5)
+            s.connect(("::1", 1))
+        return "ipv6"
+    except OSError:
+        return "ipv4"
+
+
+def rendezvous_env(device: str, platform: str | None = None) -> tuple[str, dict]:
+    """(loopback address, extra worker environment) for a single-node run on this platform."""
+    platform = platform or sys.platform
+    env: dict = {}
+    if device == "mps":
+        env["PYTORCH_ENABLE_MPS_FALLBACK"] = "1"
+        log.warning("MPS device: PYTORCH_ENABLE_MPS_FALLBACK=1, so ops MPS lacks (e.g. c10d::allgather_) "
+                    "fall back to the CPU")
+    if platform.startswith("linux"):
+        return "127.0.0.1", env
+    ipv6 = detect_active_ip_family() == "ipv6"
+    env["GLOO_USE_IPV6"] = "1" if ipv6 else "0"
+    if ipv6 and platform == "darwin":
+        env["GLOO_SOCKET_IFNAME"] = "lo0"
+    return ("::1" if ipv6 else "127.0.0.1"), env
 
 
 def default_nproc(device: str) -> int:
@@ -62,17 +100,19 @@ def launch_single_node_ddp(run_id: str, device: str, worker_op: Callable[..., No
                            monitor_interval: float = 0.5, extra_env: dict | None = None) -> int:
     """Run ``worker_op(*args)`` in ``nproc`` ranks; return 0 or the first failing exit code."""
     nproc = nproc or default_nproc(device)
-    port = free_port()
+    addr, rdzv_env = rendezvous_env(str(device))
+    port = free_port(addr)
     threads = max(1, (os.cpu_count() or 1) // nproc)
-    log.info(f"Launching run {run_id}: {nproc} worker(s) on {device}, rendezvous 127.0.0.1:{port}")
+    log.info(f"Launching run {run_id}: {nproc} worker(s) on {device}, rendezvous [{addr}]:{port}")
     ctx = mp.get_context("spawn")
     procs = []
     for rank in range(nproc):
         env = {
             "RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(nproc),
             "LOCAL_WORLD_SIZE": str(nproc), "GROUP_RANK": "0",
-            "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+            "MASTER_ADDR": addr, "MASTER_PORT": str(port),
             "PENROZ_RUN_ID": str(run_id), "HSA_ENABLE_IPC_MODE_LEGACY": "0",
+            **rdzv_env,
         }
         if not str(device).startswith("cuda"):
             env["OMP_NUM_THREADS"] = str(threads)

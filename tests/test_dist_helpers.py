@@ -253,3 +253,79 @@ def test_allreduce_bench_cpu_rehearsal():
     lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 3 and lines[-1]["summary"] and lines[-1]["n_ranks"] == 2
     assert {l["wire"] for l in lines[:2]} == {"fp32", "bf16"} and lines[1]["wire_mb"] == 0.5
+
+
+# ---- loopback rendezvous per platform / address family (reference ddp.py:22-36, 39-42, 59-68)
+
+def test_rendezvous_linux_is_ipv4_loopback_without_gloo_overrides():
+    addr, env = LA.rendezvous_env("cpu", platform="linux")
+    assert addr == "127.0.0.1" and env == {}
+
+
+@pytest.mark.parametrize("platform,family,addr,ifname", [
+    ("darwin", "ipv6", "::1", "lo0"), ("darwin", "ipv4", "127.0.0.1", None),
+    ("win32", "ipv6", "::1", None), ("win32", "ipv4", "127.0.0.1", None)])
+def test_rendezvous_off_linux_follows_the_active_family(platform, family, addr, ifname):
+    with mock.patch.object(LA, "detect_active_ip_family", return_value=family):
+        got, env = LA.rendezvous_env("cpu", platform=platform)
+    assert got == addr
+    assert env["GLOO_USE_IPV6"] == ("1" if family == "ipv6" else "0")
+    assert env.get("GLOO_SOCKET_IFNAME") == ifname
+
+
+def test_rendezvous_mps_enables_cpu_fallback(caplog):
+    with caplog.at_level(logging.WARNING):
+        _, env = LA.rendezvous_env("mps", platform="linux")
+    assert env["PYTORCH_ENABLE_MPS_FALLBACK"] == "1"
+    assert "PYTORCH_ENABLE_MPS_FALLBACK" in caplog.text
+
+
+def test_detect_active_ip_family_falls_back_to_ipv4_when_ipv6_connect_fails():
+    class Refusing:
+        def __init__(self, *a, **k):
+            pass
+
+        def __enter__(self):
+            return self
+
+        def __exit__(self, *exc):
+            return False
+
+        def settimeout(self, t):
+            pass
+
+        def connect(self, addr):
+            raise OSError("no ipv6")
+
+    with mock.patch.object(LA.socket, "socket", Refusing), mock.patch.object(LA.socket, "has_ipv6", True):
+        assert LA.detect_active_ip_family() == "ipv4"
+    with mock.patch.object(LA.socket, "has_ipv6", False):
+        assert LA.detect_active_ip_family() == "ipv4"
+
+
+def test_launch_passes_the_rendezvous_env_to_every_rank():
+    seen = []
+
+    class FakeProc:
+        exitcode = 0
+        sentinel = None
+
+        def __init__(self, target, args, name):
+            seen.append(args[0])
+            self.sentinel = object()
+
+        def start(self):
+            pass
+
+        def join(self, timeout=None):
+            pass
+
+    class Ctx:
+        Process = FakeProc
+
+    with mock.patch.object(LA, "rendezvous_env", return_value=("127.0.0.1", {"GLOO_USE_IPV6": "0"})), \
+            mock.patch.object(LA.mp, "get_context", return_value=Ctx()), \
+            mock.patch.object(LA.mp_connection, "wait", side_effect=lambda objs, timeout: objs):
+        assert LA.launch_single_node_ddp("r", "cpu", print, nproc=2) == 0
+    assert len(seen) == 2
+    assert all(e["GLOO_USE_IPV6"] == "0" and e["MASTER_ADDR"] == "127.0.0.1" for e in seen)
