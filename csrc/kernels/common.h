@@ -146,6 +146,12 @@ __device__ __forceinline__ float gelu_f(float x, int approx) {
   return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));
 }
 
+// gated-MLP activations: 0 gelu (erf), 1 gelu (tanh), 2 silu
+__device__ __forceinline__ float act_f(float x, int kind) {  // 0 gelu, 1 gelu_tanh, 2 silu
+  if (kind == 2) return x / (1.f + __expf(-x));
+  return gelu_f(x, kind);
+}
+
 __device__ __forceinline__ float gelu_grad_f(float x, int approx) {
   if (approx) {
     const float k = 0.7978845608028654f;

@@ -13,10 +13,6 @@
 
 namespace penroz {
 
-__device__ __forceinline__ float act_f(float x, int kind) {  // 0 gelu, 1 gelu_tanh, 2 silu
-  if (kind == 2) return x / (1.f + __expf(-x));
-  return gelu_f(x, kind);
-}
 __device__ __forceinline__ float act_grad_f(float x, int kind) {
   if (kind == 2) {
     const float s = 1.f / (1.f + __expf(-x));

@@ -128,6 +128,87 @@ __global__ void __launch_bounds__(256) skinny_gemm_kernel(const bf16* __restrict
   }
 }
 
+// Gated-MLP decode projection with the activation in the epilogue:
+//   out[M, I] = act(x · Wgᵀ) ⊙ (x · Wuᵀ),  gu = [Wg; Wu] ([2I, K], the packed gate|up weight).
+// A workgroup owns 16 output columns n0.. and runs the skinny main loop on BOTH weight slices
+// (gate rows n0 + r16 and up rows I + n0 + r16) with the same 4-way K split, group size and
+// LDS reduction order as skinny_gemm_kernel at splitk 1; the epilogue rounds gate and up to bf16
+// (the unfused GEMM's output) before act(g) · u, so the result is bit-identical to skinny_gemm
+// followed by the packed gated-activation kernel — one launch and one [M, 2I] round trip fewer
+// per block of the Gemma decode step.
+template <int MB>
+__global__ void __launch_bounds__(256) skinny_gated_kernel(const bf16* __restrict__ x, int64_t x_rs,
+                                                           const bf16* __restrict__ gu, bf16* __restrict__ out,
+                                                           int64_t o_rs, int M, int I, int K, int kind) {
+  __shared__ __attribute__((aligned(16))) float red[2 * 4 * MB * 64 * 4];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int n0 = blockIdx.x * 16;
+  const int steps = K / 32;
+  const int s0 = steps * wid / 4, s1 = steps * (wid + 1) / 4;
+  const int r16 = lane & 15, kq = 8 * (lane >> 4);
+  const int nr = min(n0 + r16, I - 1);  // rows past I: clamped, never stored
+  const bf16* wg = gu + (size_t)nr * K + kq;
+  const bf16* wu = gu + (size_t)(I + nr) * K + kq;
+  const bf16* xp[MB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    const int m = mb * 16 + r16;
+    xp[mb] = x + (size_t)(m < M ? m : 0) * x_rs + kq;
+  }
+  sk_f32x4 ag[MB], au[MB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) ag[mb] = au[mb] = (sk_f32x4){0.f, 0.f, 0.f, 0.f};
+
+  for (int s = s0; s < s1; s += kSkU) {
+    sk_u32x4 ga[kSkU], ua[kSkU], xb[kSkU][MB];
+#pragma unroll
+    for (int u = 0; u < kSkU; ++u) {
+      const size_t ko = (size_t)min(s + u, s1 - 1) * 32;
+      ga[u] = *reinterpret_cast<const sk_u32x4*>(wg + ko);
+      ua[u] = *reinterpret_cast<const sk_u32x4*>(wu + ko);
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) xb[u][mb] = *reinterpret_cast<const sk_u32x4*>(xp[mb] + ko);
+    }
+#pragma unroll
+    for (int u = 0; u < kSkU; ++u) {
+      if (s + u < s1) {
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) {
+          ag[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(sk_bf16x8, ga[u]),
+                                                           __builtin_bit_cast(sk_bf16x8, xb[u][mb]), ag[mb], 0, 0, 0);
+          au[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(sk_bf16x8, ua[u]),
+                                                           __builtin_bit_cast(sk_bf16x8, xb[u][mb]), au[mb], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  sk_f32x4* r4 = reinterpret_cast<sk_f32x4*>(red);
+  sk_f32x4* u4 = r4 + 4 * MB * 64;
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    r4[(wid * MB + mb) * 64 + lane] = ag[mb];
+    u4[(wid * MB + mb) * 64 + lane] = au[mb];
+  }
+  __syncthreads();
+  for (int it = t; it < MB * 64; it += 256) {
+    const int mb = it >> 6, ln = it & 63;
+    const sk_f32x4 g = r4[mb * 64 + ln] + r4[(MB + mb) * 64 + ln] + r4[(2 * MB + mb) * 64 + ln] +
+                       r4[(3 * MB + mb) * 64 + ln];
+    const sk_f32x4 v = u4[mb * 64 + ln] + u4[(MB + mb) * 64 + ln] + u4[(2 * MB + mb) * 64 + ln] +
+                       u4[(3 * MB + mb) * 64 + ln];
+    const int m = mb * 16 + (ln & 15), nb = n0 + 4 * (ln >> 4);
+    if (m >= M) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = nb + r;
+      if (n < I)
+        out[(size_t)m * o_rs + n] =
+            from_f<bf16>(act_f(bf2f(from_f<bf16>(g[r])), kind) * bf2f(from_f<bf16>(v[r])));
+    }
+  }
+}
+
 // Decode-step linear with the residual add + LayerNorm fused in front and an optional GELU
 // behind: out = act(LN(resid_in + delta + dbias) · Wᵀ + bias), M ≤ 64 rows, K ≤ 1024. Every
 // workgroup normalises all M rows itself (one wave per row, the add+LayerNorm kernel's math:
@@ -375,4 +456,34 @@ int64_t skinny_gemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tenso
   else PENROZ_SKINNY(4);
 #undef PENROZ_SKINNY
   return splitk;
+}
+
+// out[M, I] = act(x · gu[:I]ᵀ) ⊙ (x · gu[I:]ᵀ) for M <= 64 decode rows (kind: 0 gelu, 1 gelu_tanh,
+// 2 silu); bit-identical to skinny_gemm(x, gu) followed by gated_act_packed.
+void skinny_gated(torch::Tensor x, torch::Tensor gu, torch::Tensor out, int64_t kind) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kBFloat16 && gu.scalar_type() == torch::kBFloat16 &&
+                  out.scalar_type() == torch::kBFloat16, "skinny_gated: bf16 x / gu / out");
+  TORCH_CHECK(x.dim() == 2 && gu.dim() == 2 && out.dim() == 2, "skinny_gated: 2-D operands");
+  const int M = x.size(0), K = x.size(1);
+  TORCH_CHECK(gu.size(0) % 2 == 0, "skinny_gated: packed [gate; up] weight [2I, K]");
+  const int I = gu.size(0) / 2;
+  TORCH_CHECK(M >= 1 && M <= 64 && I >= 1 && gu.size(1) == K && K % 32 == 0, "skinny_gated: M <= 64, K % 32 == 0");
+  TORCH_CHECK(x.stride(1) == 1 && x.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "skinny_gated: x rows 16-B aligned");
+  TORCH_CHECK(gu.is_contiguous() && reinterpret_cast<uintptr_t>(gu.data_ptr()) % 16 == 0, "skinny_gated: gu contiguous");
+  TORCH_CHECK(out.size(0) == M && out.size(1) == I && out.stride(1) == 1, "skinny_gated: out [M, I]");
+  TORCH_CHECK(kind >= 0 && kind <= 2, "skinny_gated: kind 0 (gelu), 1 (gelu_tanh), 2 (silu)");
+  const int MB = M <= 16 ? 1 : M <= 32 ? 2 : 4;
+  auto stream = at::hip::getCurrentHIPStream();
+  const dim3 grid((I + 15) / 16);
+  auto xp = reinterpret_cast<const bf16*>(x.data_ptr());
+  auto wp = reinterpret_cast<const bf16*>(gu.data_ptr());
+  auto op = reinterpret_cast<bf16*>(out.data_ptr());
+#define PENROZ_SKG(MBV)                                                                                              \
+  hipLaunchKernelGGL(skinny_gated_kernel<MBV>, grid, dim3(256), 0, stream, xp, (int64_t)x.stride(0), wp, op,        \
+                     (int64_t)out.stride(0), M, I, K, (int)kind)
+  if (MB == 1) PENROZ_SKG(1);
+  else if (MB == 2) PENROZ_SKG(2);
+  else PENROZ_SKG(4);
+#undef PENROZ_SKG
 }

@@ -298,11 +298,11 @@ class GemmaDecodeProgram:
     kernel sequence.
 
     The module forward runs ~16 kernels per block at decode shapes (four RMSNorms, two residual
-    adds, separate gate and up GEMMs). Per block this runs 8 (+1 split-K combine): QKV GEMM →
+    adds, separate gate and up GEMMs). Per block this runs 7 (+1 split-K combine): QKV GEMM →
     RoPE (device-offset table) → decode attention with fused K/V append → O GEMM →
     [residual add + post-attention norm + pre-MLP norm] → gate|up GEMM (one concatenated weight)
-    → gated activation on the packed halves → down GEMM → [residual add + post-MLP norm + the next
-    block's input norm]. Rounding follows the module path (bf16 residual stream, torch's rounding
+    with the gated activation in its epilogue (``skinny_gated``) → down GEMM → [residual add +
+    post-MLP norm + the next block's input norm]. Rounding follows the module path (bf16 residual stream, torch's rounding
     points), so only the GEMM accumulation order of the fused gate|up projection can differ.
     Reference block semantics: ``neural_net_layers.py:188-225``.
     """
@@ -379,12 +379,20 @@ class GemmaDecodeProgram:
             pa, pm, pre = b["post_attn"], b["post_mlp"], b["pre_mlp"]
             h, y = K.rms_residual(x, o, pa.weight if pa is not None else None, pre.weight, b["mode"],
                                   pa.eps if pa is not None else 0.0, pre.eps)
-            g = K.gated_act_packed(_linear(y, b["gu"]), b["kind"])
+            g = _gated(y, b["gu"], b["kind"])
             d = _linear(g, b["down"])
             nxt = self.blocks[l + 1]["in_norm"] if l + 1 < len(self.blocks) else self.norm_f
             x, y = K.rms_residual(h, d, pm.weight if pm is not None else None, nxt.weight, b["mode"],
                                   pm.eps if pm is not None else 0.0, nxt.eps)
         return _linear(y, self.head.weight)
+
+
+def _gated(x: Tensor, gu: Tensor, kind: int) -> Tensor:
+    """act(x·Wgᵀ) ⊙ (x·Wuᵀ) from the packed gate|up weight: one fused skinny launch up to
+    SKINNY_MAX_ROWS rows (activation in the GEMM epilogue), else GEMM + packed activation."""
+    if x.shape[0] <= SKINNY_MAX_ROWS and gemm_ops.skinny_ok(x, gu):
+        return gemm_ops.skinny_gated(x, gu, kind)
+    return _ext.kernels().gated_act_packed(_linear(x, gu), kind)
 
 
 def _linear(x: Tensor, w: Tensor) -> Tensor:

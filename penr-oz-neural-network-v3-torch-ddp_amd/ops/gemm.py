@@ -163,6 +163,15 @@ def skinny_linear(x: Tensor, w: Tensor, bias: Tensor | None) -> Tensor:
     return out.view(*x.shape[:-1], N)
 
 
+def skinny_gated(x: Tensor, gu: Tensor, kind: int) -> Tensor:
+    """Gated-MLP decode projection in one launch: act(x·gu[:I]ᵀ) ⊙ (x·gu[I:]ᵀ) for ≤ 64 rows,
+    ``gu`` the packed [gate; up] weight [2I, K]; kind 0 gelu, 1 gelu_tanh, 2 silu. Bit-identical to
+    ``skinny_linear`` + the packed gated-activation kernel (csrc/kernels/skinny_gemm.hip)."""
+    out = torch.empty(x.shape[0], gu.shape[0] // 2, device=x.device, dtype=x.dtype)
+    kernels().skinny_gated(x, gu, out, kind)
+    return out
+
+
 class decode_gemms:
     """Context: the ``nn.Linear`` modules of ``model`` run decode-shaped inputs through the skinny
     kernel (others keep ``F.linear``). Entered by the graph decoder around the captured step of a

@@ -666,6 +666,30 @@ def test_skinny_gemm(M, K, N, with_bias):
     _close(Gm.skinny_linear(x.reshape(1, M, K), w, b).view(M, N), ref, 0.03, 0.01, "module path")
 
 
+@pytest.mark.parametrize("M,K,I", [(1, 1152, 6912), (64, 1152, 6912), (17, 768, 264), (33, 256, 1000), (5, 96, 8)])
+@pytest.mark.parametrize("kind", ["gelu", "gelu_tanh", "silu"])
+def test_skinny_gated(M, K, I, kind):
+    """Fused gate|up projection + gated activation == the unfused pair (skinny GEMM at split 1,
+    then the packed activation kernel) bit for bit, and close to fp32 torch; partial last column
+    tile (I % 16 != 0), masked rows, strided x rows."""
+    from penroz.ops import activations as Ac
+    from penroz.ops import gemm as Gm
+    torch.manual_seed(M + K + I)
+    big = torch.randn(M, K + 64, device=DEV).to(torch.bfloat16)
+    x = big[:, 32:32 + K]
+    gu = (torch.randn(2 * I, K, device=DEV) / math.sqrt(K)).to(torch.bfloat16)
+    ws, cnt = Gm.skinny_workspace(x.device)
+    lin = torch.empty(M, 2 * I, device=DEV, dtype=torch.bfloat16)
+    _ext.kernels().skinny_gemm(x, gu, None, lin, ws, cnt, 1)
+    unfused = _ext.kernels().gated_act_packed(lin, Ac._GATED[kind])
+    fused = Gm.skinny_gated(x, gu, Ac._GATED[kind])
+    assert fused.shape == (M, I)
+    assert torch.equal(fused, unfused)
+    h = x.float() @ gu.float().t()
+    ref = Ac.reference_gated_act(h[:, :I], h[:, I:], kind)
+    _close(fused.float(), ref, 0.03, 0.02)
+
+
 @pytest.mark.parametrize("R,C", [(768, 2304), (3072, 768), (64, 64), (50304, 768)])
 def test_transpose_bf16(R, C):
     x = torch.randn(R, C, device=DEV).to(torch.bfloat16)
