@@ -76,6 +76,8 @@ torch::Tensor gemm8_dma_probe(torch::Tensor src, int64_t bytes, int64_t lds_off,
 int64_t skinny_gemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> bias, torch::Tensor out,
                     torch::Tensor ws, torch::Tensor cnt, int64_t splitk);
 void skinny_gated(torch::Tensor x, torch::Tensor gu, torch::Tensor out, int64_t kind);
+int64_t skinny_qkv_rope(torch::Tensor x, torch::Tensor w, torch::Tensor cosv, torch::Tensor sinv, int64_t D,
+                        int64_t nrot, torch::Tensor out, torch::Tensor ws, torch::Tensor cnt, int64_t splitk);
 void decode_ln_linear(torch::Tensor rin, c10::optional<torch::Tensor> delta, c10::optional<torch::Tensor> dbias,
                       c10::optional<torch::Tensor> rout, torch::Tensor gamma, torch::Tensor beta, double eps,
                       torch::Tensor w, c10::optional<torch::Tensor> bias, torch::Tensor out, int64_t act);
@@ -168,6 +170,10 @@ PYBIND11_MODULE(penroz_kernels, m) {
   m.def("skinny_gated", &skinny_gated, pybind11::arg("x"), pybind11::arg("gu"), pybind11::arg("out"),
         pybind11::arg("kind"),
         "decode gated MLP projection: out[M<=64, I] = act(x·gu[:I]ᵀ)·(x·gu[I:]ᵀ), bf16, one launch");
+  m.def("skinny_qkv_rope", &skinny_qkv_rope, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("cos"),
+        pybind11::arg("sin"), pybind11::arg("D"), pybind11::arg("nrot"), pybind11::arg("out"), pybind11::arg("ws"),
+        pybind11::arg("cnt"), pybind11::arg("splitk") = 0,
+        "decode QKV projection with RoPE on the first nrot heads in the epilogue, M <= 64; returns the split");
   m.def("decode_ln_linear", &decode_ln_linear, pybind11::arg("resid_in"), pybind11::arg("delta"),
         pybind11::arg("dbias"), pybind11::arg("resid_out"), pybind11::arg("gamma"), pybind11::arg("beta"),
         pybind11::arg("eps"), pybind11::arg("w"), pybind11::arg("bias"), pybind11::arg("out"), pybind11::arg("act") = 0,

@@ -209,6 +209,138 @@ __global__ void __launch_bounds__(256) skinny_gated_kernel(const bf16* __restric
   }
 }
 
+// Decode QKV projection with RoPE in the epilogue: out[M, (H + 2Hkv)·D] = rope(x · Wᵀ) for the
+// first `nrot` heads (Q and K, rotate-half pairs (j, j + D/2) with one position's cos / sin [D/2]:
+// every decode row sits at the same cache position), V columns passed through. A workgroup owns
+// a PAIR of 16-column slices — columns j0.. and j0 + D/2.. of one head — so both halves of every
+// rotated pair end in the same lanes; the main loop is the skinny one on two weight slices, with
+// the split-K slab hand-off of skinny_gemm_kernel for the narrow grid (Gemma-3 1B: 48 pair tiles).
+// Rounding: both halves are rounded to bf16 (the unfused GEMM's output) before the rotation, whose
+// arithmetic is the RoPE kernel's (x1·c − x2·s, x2·c + x1·s). One launch and one [M, W] round trip
+// per block fewer than GEMM → RoPE kernel.
+template <int MB>
+__global__ void __launch_bounds__(256) skinny_qkv_rope_kernel(const bf16* __restrict__ x, int64_t x_rs,
+                                                              const bf16* __restrict__ w, bf16* __restrict__ out,
+                                                              int64_t o_rs, int M, int K, int D, int nrot,
+                                                              const float* __restrict__ cosv,
+                                                              const float* __restrict__ sinv, int splitk,
+                                                              float* __restrict__ ws, int* __restrict__ cnt) {
+  __shared__ __attribute__((aligned(16))) float red[2 * 4 * MB * 64 * 4 + 4];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int ntiles = gridDim.x / splitk;
+  const int tile = blockIdx.x / splitk, split = blockIdx.x % splitk;
+  const int half = D / 2, ppt = half / 16;  // pair tiles per head
+  const int head = tile / ppt, j0 = (tile - head * ppt) * 16;
+  const int c1 = head * D + j0, c2 = c1 + half;
+  const int steps = K / 32;
+  const int sb0 = (int)((int64_t)steps * split / splitk), sb1 = (int)((int64_t)steps * (split + 1) / splitk);
+  const int nsb = sb1 - sb0;
+  const int s0 = sb0 + nsb * wid / 4, s1 = sb0 + nsb * (wid + 1) / 4;
+  const int r16 = lane & 15, kq = 8 * (lane >> 4);
+  const bf16* w1 = w + (size_t)(c1 + r16) * K + kq;
+  const bf16* w2 = w + (size_t)(c2 + r16) * K + kq;
+  const bf16* xp[MB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    const int m = mb * 16 + r16;
+    xp[mb] = x + (size_t)(m < M ? m : 0) * x_rs + kq;
+  }
+  sk_f32x4 a1[MB], a2[MB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) a1[mb] = a2[mb] = (sk_f32x4){0.f, 0.f, 0.f, 0.f};
+
+  for (int s = s0; s < s1; s += kSkU) {
+    sk_u32x4 wa1[kSkU], wa2[kSkU], xb[kSkU][MB];
+#pragma unroll
+    for (int u = 0; u < kSkU; ++u) {
+      const size_t ko = (size_t)min(s + u, s1 - 1) * 32;
+      wa1[u] = *reinterpret_cast<const sk_u32x4*>(w1 + ko);
+      wa2[u] = *reinterpret_cast<const sk_u32x4*>(w2 + ko);
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) xb[u][mb] = *reinterpret_cast<const sk_u32x4*>(xp[mb] + ko);
+    }
+#pragma unroll
+    for (int u = 0; u < kSkU; ++u) {
+      if (s + u < s1) {
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) {
+          a1[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(sk_bf16x8, wa1[u]),
+                                                           __builtin_bit_cast(sk_bf16x8, xb[u][mb]), a1[mb], 0, 0, 0);
+          a2[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(sk_bf16x8, wa2[u]),
+                                                           __builtin_bit_cast(sk_bf16x8, xb[u][mb]), a2[mb], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  sk_f32x4* r4 = reinterpret_cast<sk_f32x4*>(red);  // [half 0 | half 1][wave][mb][lane]
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    r4[(wid * MB + mb) * 64 + lane] = a1[mb];
+    r4[((4 + wid) * MB + mb) * 64 + lane] = a2[mb];
+  }
+  __syncthreads();
+  auto block_sum = [&](int hf, int it) {
+    const sk_f32x4* b = r4 + hf * 4 * MB * 64;
+    const int mb = it >> 6, ln = it & 63;
+    return b[mb * 64 + ln] + b[(MB + mb) * 64 + ln] + b[(2 * MB + mb) * 64 + ln] + b[(3 * MB + mb) * 64 + ln];
+  };
+  const bool rot = head < nrot;
+  auto epilogue = [&](int it, sk_f32x4 v1, sk_f32x4 v2) {
+    const int ln = it & 63, m = (it >> 6) * 16 + (ln & 15), nb = 4 * (ln >> 4);
+    if (m >= M) return;
+    bf16* o = out + (size_t)m * o_rs;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float x1 = bf2f(from_f<bf16>(v1[r])), x2 = bf2f(from_f<bf16>(v2[r]));
+      float y1 = x1, y2 = x2;
+      if (rot) {
+        const float cs = cosv[j0 + nb + r], sn = sinv[j0 + nb + r];
+        y1 = x1 * cs - x2 * sn;
+        y2 = x2 * cs + x1 * sn;
+      }
+      o[c1 + nb + r] = from_f<bf16>(y1);
+      o[c2 + nb + r] = from_f<bf16>(y2);
+    }
+  };
+  if (splitk == 1) {
+    for (int it = t; it < MB * 64; it += 256) epilogue(it, block_sum(0, it), block_sum(1, it));
+    return;
+  }
+  // split-K: the pair's two partial slabs, then the counter hand-off of skinny_gemm_kernel
+  sk_f32x4* slab = reinterpret_cast<sk_f32x4*>(ws);
+  const size_t per = (size_t)2 * MB * 64;
+  for (int it = t; it < MB * 64; it += 256) {
+    slab[((size_t)split * ntiles + tile) * per + it] = block_sum(0, it);
+    slab[((size_t)split * ntiles + tile) * per + MB * 64 + it] = block_sum(1, it);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(red + 2 * 4 * MB * 64 * 4);
+  if (t == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int prev = __hip_atomic_fetch_add(&cnt[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = prev == splitk - 1;
+  }
+  __syncthreads();
+  if (!*flag) return;
+  if (t == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(&cnt[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  for (int it = t; it < MB * 64; it += 256) {
+    sk_f32x4 v1 = slab[(size_t)tile * per + it], v2 = slab[(size_t)tile * per + MB * 64 + it];
+    for (int sp = 1; sp < splitk; ++sp) {
+      v1 += slab[((size_t)sp * ntiles + tile) * per + it];
+      v2 += slab[((size_t)sp * ntiles + tile) * per + MB * 64 + it];
+    }
+    epilogue(it, v1, v2);
+  }
+}
+
 // Decode-step linear with the residual add + LayerNorm fused in front and an optional GELU
 // behind: out = act(LN(resid_in + delta + dbias) · Wᵀ + bias), M ≤ 64 rows, K ≤ 1024. Every
 // workgroup normalises all M rows itself (one wave per row, the add+LayerNorm kernel's math:
@@ -486,4 +618,53 @@ void skinny_gated(torch::Tensor x, torch::Tensor gu, torch::Tensor out, int64_t 
   else if (MB == 2) PENROZ_SKG(2);
   else PENROZ_SKG(4);
 #undef PENROZ_SKG
+}
+
+// out[M, (H + 2Hkv)·D] = x · wᵀ with RoPE (cos / sin [D/2] of the one decode position) applied to
+// the first nrot = H + Hkv heads; M <= 64, D % 32 == 0. Returns the split-K factor used.
+int64_t skinny_qkv_rope(torch::Tensor x, torch::Tensor w, torch::Tensor cosv, torch::Tensor sinv, int64_t D,
+                        int64_t nrot, torch::Tensor out, torch::Tensor ws, torch::Tensor cnt, int64_t splitk) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kBFloat16 && w.scalar_type() == torch::kBFloat16 &&
+                  out.scalar_type() == torch::kBFloat16, "skinny_qkv_rope: bf16 x / w / out");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "skinny_qkv_rope: 2-D operands");
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(M >= 1 && M <= 64 && w.size(1) == K && K % 32 == 0, "skinny_qkv_rope: M <= 64, K % 32 == 0");
+  TORCH_CHECK(D >= 32 && D % 32 == 0 && N % D == 0 && nrot >= 0 && nrot <= N / D,
+              "skinny_qkv_rope: D % 32 == 0, whole heads, nrot <= heads");
+  TORCH_CHECK(x.stride(1) == 1 && x.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "skinny_qkv_rope: x rows 16-B aligned");
+  TORCH_CHECK(w.is_contiguous() && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0, "skinny_qkv_rope: w contiguous");
+  TORCH_CHECK(out.size(0) == M && out.size(1) == N && out.stride(1) == 1, "skinny_qkv_rope: out [M, N]");
+  TORCH_CHECK(cosv.scalar_type() == torch::kFloat32 && sinv.scalar_type() == torch::kFloat32 && cosv.is_contiguous() &&
+                  sinv.is_contiguous() && cosv.numel() == D / 2 && sinv.numel() == D / 2,
+              "skinny_qkv_rope: fp32 cos / sin [D/2]");
+  const int ntiles = N / 32, steps = K / 32;
+  const int MB = M <= 16 ? 1 : M <= 32 ? 2 : 4;
+  if (splitk <= 0) {
+    splitk = 1;
+    if (ntiles < 128) splitk = std::max(1, std::min({(192 + ntiles - 1) / ntiles, steps / 4, 16}));
+  }
+  TORCH_CHECK(splitk >= 1 && splitk <= steps, "skinny_qkv_rope: bad split");
+  if (splitk > 1) {
+    TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == torch::kFloat32 &&
+                    ws.numel() >= (int64_t)splitk * ntiles * MB * 512, "skinny_qkv_rope: workspace too small");
+    TORCH_CHECK(cnt.is_cuda() && cnt.scalar_type() == torch::kInt32 && cnt.numel() >= ntiles,
+                "skinny_qkv_rope: counters too small");
+  }
+  auto stream = at::hip::getCurrentHIPStream();
+  const dim3 grid(ntiles * splitk);
+  auto xp = reinterpret_cast<const bf16*>(x.data_ptr());
+  auto wp = reinterpret_cast<const bf16*>(w.data_ptr());
+  auto op = reinterpret_cast<bf16*>(out.data_ptr());
+  float* wsp = splitk > 1 ? ws.data_ptr<float>() : nullptr;
+  int* cp = splitk > 1 ? cnt.data_ptr<int>() : nullptr;
+#define PENROZ_SQR(MBV)                                                                                              \
+  hipLaunchKernelGGL(skinny_qkv_rope_kernel<MBV>, grid, dim3(256), 0, stream, xp, (int64_t)x.stride(0), wp, op,     \
+                     (int64_t)out.stride(0), M, K, (int)D, (int)nrot, cosv.data_ptr<float>(), sinv.data_ptr<float>(), \
+                     (int)splitk, wsp, cp)
+  if (MB == 1) PENROZ_SQR(1);
+  else if (MB == 2) PENROZ_SQR(2);
+  else PENROZ_SQR(4);
+#undef PENROZ_SQR
+  return splitk;
 }

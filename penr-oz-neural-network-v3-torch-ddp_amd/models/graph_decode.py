@@ -298,8 +298,8 @@ class GemmaDecodeProgram:
     kernel sequence.
 
     The module forward runs ~16 kernels per block at decode shapes (four RMSNorms, two residual
-    adds, separate gate and up GEMMs). Per block this runs 7 (+1 split-K combine): QKV GEMM →
-    RoPE (device-offset table) → decode attention with fused K/V append → O GEMM →
+    adds, separate gate and up GEMMs). Per block this runs 6 (+1 split-K combine): QKV GEMM with
+    RoPE (device-offset table) in its epilogue (``skinny_qkv_rope``) → decode attention with fused K/V append → O GEMM →
     [residual add + post-attention norm + pre-MLP norm] → gate|up GEMM (one concatenated weight)
     with the gated activation in its epilogue (``skinny_gated``) → down GEMM → [residual add +
     post-MLP norm + the next block's input norm]. Rounding follows the module path (bf16 residual stream, torch's rounding
@@ -368,11 +368,16 @@ class GemmaDecodeProgram:
         for l, b in enumerate(self.blocks):
             a = b["attn"]
             H, Hkv, D = a.num_heads, a.num_kv_heads, a.head_dim
-            qkv = _linear(y, b["qkv"]).view(rows, 1, -1)
             if a.rope_theta is not None:
-                inv = a._inv_freq(D, qkv.device)
-                qkv = rope_ops.apply_rope_qkv(qkv, H, Hkv, D, inv, 0,
-                                              table=cache.rope_table((a.rope_theta, D), inv, 1))
+                inv = a._inv_freq(D, y.device)
+                cos, sin = cache.rope_table((a.rope_theta, D), inv, 1)
+                if rows <= SKINNY_MAX_ROWS and gemm_ops.skinny_qkv_rope_ok(y, b["qkv"], D):
+                    qkv = gemm_ops.skinny_qkv_rope(y, b["qkv"], cos, sin, D, H + Hkv).view(rows, 1, -1)
+                else:
+                    qkv = rope_ops.apply_rope_qkv(_linear(y, b["qkv"]).view(rows, 1, -1), H, Hkv, D, inv, 0,
+                                                  table=(cos, sin))
+            else:
+                qkv = _linear(y, b["qkv"]).view(rows, 1, -1)
             q, k, v = qkv.split([H * D, Hkv * D, Hkv * D], dim=2)
             att = cache.attend(l, q.reshape(rows, 1, H, D), k.view(rows, 1, Hkv, D), v.view(rows, 1, Hkv, D))
             o = _linear(att.view(rows, H * D), b["o"])

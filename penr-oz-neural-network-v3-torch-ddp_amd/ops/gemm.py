@@ -172,6 +172,26 @@ def skinny_gated(x: Tensor, gu: Tensor, kind: int) -> Tensor:
     return out
 
 
+def skinny_qkv_rope_ok(x: Tensor, w: Tensor, D: int) -> bool:
+    """The fused QKV + RoPE decode kernel applies: skinny shapes, whole heads of D % 32 == 0, and
+    its split-K slabs fit the shared workspace."""
+    if not (skinny_ok(x, w) and D % 32 == 0 and w.shape[0] % D == 0):
+        return False
+    rows, ntiles, steps = x.numel() // x.shape[-1], w.shape[0] // 32, x.shape[-1] // 32
+    mb = 1 if rows <= 16 else 2 if rows <= 32 else 4
+    split = 1 if ntiles >= 128 else max(1, min(-(-192 // ntiles), steps // 4, 16))
+    return split * ntiles * mb * 512 <= (1 << 19) and ntiles <= (1 << 12)
+
+
+def skinny_qkv_rope(x: Tensor, w: Tensor, cos: Tensor, sin: Tensor, D: int, nrot: int) -> Tensor:
+    """Decode QKV projection with RoPE (one position's cos / sin [D/2]) applied to the first
+    ``nrot`` heads in the GEMM epilogue (csrc/kernels/skinny_gemm.hip); ≤ 64 rows."""
+    out = torch.empty(x.shape[0], w.shape[0], device=x.device, dtype=x.dtype)
+    ws, cnt = skinny_workspace(x.device)
+    kernels().skinny_qkv_rope(x, w, cos, sin, D, nrot, out, ws, cnt)
+    return out
+
+
 class decode_gemms:
     """Context: the ``nn.Linear`` modules of ``model`` run decode-shaped inputs through the skinny
     kernel (others keep ``F.linear``). Entered by the graph decoder around the captured step of a

@@ -690,6 +690,37 @@ def test_skinny_gated(M, K, I, kind):
     _close(fused.float(), ref, 0.03, 0.02)
 
 
+@pytest.mark.parametrize("M,K,H,Hkv,D", [(1, 1152, 4, 1, 256), (64, 1152, 4, 1, 256), (17, 768, 12, 12, 64),
+                                         (33, 256, 8, 2, 32), (5, 96, 2, 1, 128)])
+@pytest.mark.parametrize("split", [0, 1, 2])
+def test_skinny_qkv_rope(M, K, H, Hkv, D, split):
+    """Fused decode QKV projection + RoPE (Q and K heads rotated, V passed through) vs the unfused
+    pair (skinny GEMM at the same split-K, then the RoPE kernel) and vs fp32 torch; repeated calls
+    leave the split-K counters at zero."""
+    from penroz.ops import gemm as Gm
+    from penroz.ops import rope as Ro
+    torch.manual_seed(M + K + D + split)
+    N = (H + 2 * Hkv) * D
+    big = torch.randn(M, K + 64, device=DEV).to(torch.bfloat16)
+    x = big[:, 32:32 + K]
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).to(torch.bfloat16)
+    inv = 1.0 / (10000.0 ** (torch.arange(0, D, 2, device=DEV, dtype=torch.float32) / D))
+    cos, sin = Ro.rope_table(inv, 37, 1, DEV)
+    ws, cnt = Gm.skinny_workspace(x.device)
+    assert Gm.skinny_qkv_rope_ok(x, w, D)
+    for _ in range(2):
+        out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        used = _ext.kernels().skinny_qkv_rope(x, w, cos, sin, D, H + Hkv, out, ws, cnt, split)
+        lin = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        _ext.kernels().skinny_gemm(x, w, None, lin, ws, cnt, used)
+        unfused = _ext.kernels().rope_qkv(lin.view(M, 1, N), cos, sin, H, Hkv, D, False, None).view(M, N)
+        assert torch.allclose(out.float(), unfused.float(), rtol=8e-3, atol=1e-5), (out.float() - unfused.float()).abs().max()
+    assert int(cnt.abs().sum()) == 0
+    ref = Ro.reference_apply_rope_qkv((x.float() @ w.float().t()).view(M, 1, N), H, Hkv, D, inv, 37).view(M, N)
+    _close(out.float(), ref.float(), 0.03, 0.02)
+    _close(Gm.skinny_qkv_rope(x, w, cos, sin, D, H + Hkv).float(), ref.float(), 0.03, 0.02, "python entry")
+
+
 @pytest.mark.parametrize("R,C", [(768, 2304), (3072, 768), (64, 64), (50304, 768)])
 def test_transpose_bf16(R, C):
     x = torch.randn(R, C, device=DEV).to(torch.bfloat16)
