@@ -63,6 +63,9 @@ FUSED_APPEND = os.environ.get("PENROZ_FUSED_APPEND", "1") != "0"
 # decode rows up to which the linears use the decode-shaped MFMA kernel instead of hipBLASLt
 # (measured: a win at batch 1, none at batch 64 — profiles/bench_r1_decode_graph.log)
 SKINNY_MAX_ROWS = int(os.environ.get("PENROZ_SKINNY_MAX_ROWS", "16"))
+# Gemma program: RoPE and the gated activation in the skinny GEMM epilogues ("1", default) or the
+# separate RoPE / packed-activation kernels after plain skinny GEMMs ("0": same-box A/B switch)
+DECODE_EPILOGUES = os.environ.get("PENROZ_DECODE_EPILOGUES", "1") != "0"
 # GPT decode program: residual add + LayerNorm fused in front of the QKV and fc GEMMs (and GELU
 # behind fc) in one decode-shaped kernel (csrc/kernels/skinny_gemm.hip decode_ln_linear); "0":
 # separate add+LN, GEMM and GELU kernels
@@ -371,7 +374,7 @@ class GemmaDecodeProgram:
             if a.rope_theta is not None:
                 inv = a._inv_freq(D, y.device)
                 cos, sin = cache.rope_table((a.rope_theta, D), inv, 1)
-                if rows <= SKINNY_MAX_ROWS and gemm_ops.skinny_qkv_rope_ok(y, b["qkv"], D):
+                if DECODE_EPILOGUES and rows <= SKINNY_MAX_ROWS and gemm_ops.skinny_qkv_rope_ok(y, b["qkv"], D):
                     qkv = gemm_ops.skinny_qkv_rope(y, b["qkv"], cos, sin, D, H + Hkv).view(rows, 1, -1)
                 else:
                     qkv = rope_ops.apply_rope_qkv(_linear(y, b["qkv"]).view(rows, 1, -1), H, Hkv, D, inv, 0,
@@ -395,7 +398,7 @@ class GemmaDecodeProgram:
 def _gated(x: Tensor, gu: Tensor, kind: int) -> Tensor:
     """act(x·Wgᵀ) ⊙ (x·Wuᵀ) from the packed gate|up weight: one fused skinny launch up to
     SKINNY_MAX_ROWS rows (activation in the GEMM epilogue), else GEMM + packed activation."""
-    if x.shape[0] <= SKINNY_MAX_ROWS and gemm_ops.skinny_ok(x, gu):
+    if DECODE_EPILOGUES and x.shape[0] <= SKINNY_MAX_ROWS and gemm_ops.skinny_ok(x, gu):
         return gemm_ops.skinny_gated(x, gu, kind)
     return _ext.kernels().gated_act_packed(_linear(x, gu), kind)
 
