@@ -29,9 +29,12 @@ Extra fields (outside the timed region):
   * ``comm`` at N > 1 also holds the first-contact record made before the model is built
     (``penroz.parallel.commtune``): ``devices`` (every rank's PCI id; duplicate devices abort
     the run), ``sweep`` (bare all-reduce ms / busbw over bucket sizes 16-256 MB x fp32/bf16 wire x
-    c10d/native transport, each result checked for the exact average), ``choice`` (the transport
-    the gradient reducer then uses, unless ``PENROZ_COMM`` is set) and ``rccl.coll_channels``
-    (parsed from RCCL's INIT log). The process group has an explicit timeout
+    c10d/native transport x native channel count 0 (RCCL's)/8/16/32, each result checked for the
+    exact average), ``plan`` (``commtune.plan``: transport + channel count, bucket size and wire
+    the gradient reducer then uses — each transport judged at its own bucket size, the bf16 wire
+    only when the predicted fp32 all-reduce exceeds the estimated backward; user-set
+    ``PENROZ_COMM`` / ``PENROZ_RCCL_CHANNELS`` / ``PENROZ_BUCKET_MB`` / ``PENROZ_GRAD_WIRE`` win)
+    and ``rccl.coll_channels`` (parsed from RCCL's INIT log). The process group has an explicit timeout
     (``PENROZ_DIST_TIMEOUT``, 300 s), so a stuck rank fails the run instead of hanging it;
   * ``vs_reference_eager_same_gpu``: the same config through the ``reference`` engine (stock
     PyTorch eager + autocast + foreach AdamW, the reference's semantics) measured in this same
@@ -252,13 +255,28 @@ def _allreduce_probe(device, world: int, iters: int) -> dict:
             "probe_busbw_GBps": buf.numel() * 4 * 2 * (world - 1) / world / t / 1e9}
 
 
+def _grad_plan_inputs(args) -> tuple[int, float]:
+    """(fp32 gradient bytes, estimated backward ms per rank) of the benchmarked model, before it
+    is built: parameter count from the config (GPT: 12·L·C² blocks + untied wte/lm_head + wpe;
+    Gemma: the layer list's linears), backward ≈ 2/3 of 6·params·tokens at a planning 1.0 PF/s."""
+    cfg = MODELS[args.model]
+    C, L, V = cfg["C"], cfg["L"], cfg["V"]
+    if cfg.get("gemma"):
+        n = L * (C * (cfg["H"] * 256 * 2 + 256 * 2) + 3 * C * 6912) + V * C
+    else:
+        n = L * (12 * C * C + 13 * C) + 2 * V * C + cfg["P"] * C + 2 * C
+    tokens = args.batch * args.seq
+    return 4 * n, 4.0 * n * tokens / 1.0e15 * 1e3
+
+
 def _first_contact(args, device, world: int, rccl_log) -> dict:
     """World > 1, before the model is built (outside the timed region): every rank's device
     identity (N distinct PCI devices, or fail), the all-reduce sweep over bucket size × wire dtype
-    × transport (``penroz.parallel.commtune``), the transport the reducer will use (unless
-    ``PENROZ_COMM`` was set) and the channel count RCCL picked."""
+    × transport × RCCL channel count (``penroz.parallel.commtune``), and the plan the reducer will
+    use — transport + channels, bucket size, wire — each transport judged at its own bucket size
+    (``commtune.plan``; any of ``PENROZ_COMM`` / ``PENROZ_RCCL_CHANNELS`` / ``PENROZ_BUCKET_MB`` /
+    ``PENROZ_GRAD_WIRE`` set by the user wins), and the channel count RCCL picked."""
     from penroz.parallel import commtune
-    from penroz.parallel.reducer import DEFAULT_BUCKET_MB
     devices = commtune.gather_identities(device)
     if device.type == "cuda" and "PENROZ_BENCH_DEVICE" not in os.environ:
         pcis = [d.get("pci") for d in devices]
@@ -267,23 +285,31 @@ def _first_contact(args, device, world: int, rccl_log) -> dict:
     out = {"devices": [d.get("pci", d.get("host")) for d in devices]}
     if args.comm_sweep:
         sizes = commtune.SWEEP_SIZES_MB if device.type == "cuda" else (1, 4)
-        rows = commtune.sweep(device, sizes_mb=sizes, iters=args.comm_probe_iters or 3)
+        channels = commtune.SWEEP_CHANNELS if device.type == "cuda" else (0,)
+        rows = commtune.sweep(device, sizes_mb=sizes, iters=args.comm_probe_iters or 3, channels=channels)
         out["sweep"] = rows
-        choice = commtune.choose(rows, DEFAULT_BUCKET_MB)
-        if "PENROZ_COMM" in os.environ:
-            choice = {"transport": os.environ["PENROZ_COMM"], "reason": "PENROZ_COMM set"}
-        else:
-            os.environ["PENROZ_COMM"] = choice["transport"]
-        out["choice"] = choice
-        # the gradient bucket size from the same table (RCCL only: the gloo plumbing config keeps
-        # the reference DDP's 25 MB, whose TCP transfers the sweep's sizes do not model)
+        grad_bytes, bwd_ms = _grad_plan_inputs(args)
+        pl = commtune.plan(rows, grad_bytes, bwd_ms)
+        pl["grad_bytes"], pl["backward_ms_estimate"] = grad_bytes, round(bwd_ms, 4)
+        # the gloo plumbing config keeps the reference DDP's 25 MB buckets and fp32 wire: the sweep's
+        # sizes do not model its TCP transfers
+        applied = {"PENROZ_COMM": pl["transport"]}
+        if pl["transport"] == "native" and pl.get("channels"):
+            applied["PENROZ_RCCL_CHANNELS"] = str(pl["channels"])
         if device.type == "cuda":
-            bucket = commtune.choose_bucket(rows, "native" if choice["transport"] == "native" else "c10d")
-            if "PENROZ_BUCKET_MB" in os.environ:
-                bucket = {"bucket_mb": float(os.environ["PENROZ_BUCKET_MB"]), "rule": "PENROZ_BUCKET_MB set"}
-            elif bucket is not None:
-                os.environ["PENROZ_BUCKET_MB"] = str(bucket["bucket_mb"])
-            out["bucket"] = bucket
+            if pl.get("bucket_mb") is not None:
+                applied["PENROZ_BUCKET_MB"] = str(pl["bucket_mb"])
+            applied["PENROZ_GRAD_WIRE"] = pl["wire"]
+        for k, v in applied.items():
+            if k in os.environ:
+                pl.setdefault("user_set", {})[k] = os.environ[k]
+            else:
+                os.environ[k] = v
+        out["plan"] = pl
+        if device.type == "cuda":
+            from penroz.parallel import rccl
+            keep = int(os.environ.get("PENROZ_RCCL_CHANNELS", "0") or 0) if os.environ["PENROZ_COMM"] == "native" else -1
+            rccl.NativeComm.release(keep=keep)
     out["rccl"] = commtune.rccl_channels(rccl_log)
     return out
 

@@ -83,6 +83,18 @@ case $cmd in
         echo "$e B$b $(grep metric gpurun_out/dec.log)"
       done
     done ;;
+  decode-ab)
+    # same-box A/B of an env switch on the graph decode program, two interleaved passes
+    model=$1; var=$2; shift 2
+    for pass in 1 2; do
+      for b in "$@"; do
+        for v in 0 1; do
+          env PENROZ_GRAPH_DECODE=1 $var=$v timeout -k 10 240 python bench/bench_decode.py --model $model --batch $b \
+            > gpurun_out/dec.log 2>&1 || { tail -20 gpurun_out/dec.log; exit 1; }
+          echo "pass$pass $var=$v B$b $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/dec.log)"
+        done
+      done
+    done ;;
   gemma-train)
     for B in 8 16; do
       timeout -k 10 400 python bench.py --model gemma3-1b --batch $B --steps 5 --warmup 2 --ref-steps 0 \

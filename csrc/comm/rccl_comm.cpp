@@ -44,7 +44,12 @@ static ncclDataType_t to_nccl(at::ScalarType t) {
 
 class RcclComm {
  public:
-  RcclComm(const std::string& id_bytes, int rank, int world, int device) : rank_(rank), world_(world), device_(device) {
+  // channels > 0: the communicator is built with exactly that many channels (RCCL CTAs:
+  // ncclConfig_t minCTAs = maxCTAs), the per-communicator form of NCCL_MIN/MAX_NCHANNELS — the
+  // environment variables are read once per process, so the first-contact sweep compares
+  // channel counts with one communicator each
+  RcclComm(const std::string& id_bytes, int rank, int world, int device, int channels = 0)
+      : rank_(rank), world_(world), device_(device), channels_(channels) {
     if (id_bytes.size() != sizeof(ncclUniqueId)) throw std::runtime_error("bad RCCL unique id size");
     ncclUniqueId id;
     std::memcpy(&id, id_bytes.data(), sizeof(id));
@@ -52,7 +57,14 @@ class RcclComm {
     int lo = 0, hi = 0;
     HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
     HIP_OK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi));  // highest priority
-    NCCL_OK(ncclCommInitRank(&comm_, world, id, rank));
+    if (channels > 0) {
+      ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+      cfg.minCTAs = channels;
+      cfg.maxCTAs = channels;
+      NCCL_OK(ncclCommInitRankConfig(&comm_, world, id, rank, &cfg));
+    } else {
+      NCCL_OK(ncclCommInitRank(&comm_, world, id, rank));
+    }
   }
 
   ~RcclComm() {
@@ -116,6 +128,7 @@ class RcclComm {
   void synchronize() { HIP_OK(hipStreamSynchronize(stream_)); }
   int rank() const { return rank_; }
   int world() const { return world_; }
+  int channels() const { return channels_; }
 
  private:
   void fence_from_current() {
@@ -147,7 +160,7 @@ class RcclComm {
     return e;
   }
 
-  int rank_, world_, device_;
+  int rank_, world_, device_, channels_;
   ncclComm_t comm_ = nullptr;
   hipStream_t stream_ = nullptr;
   std::vector<hipEvent_t> events_;
@@ -160,7 +173,8 @@ class RcclComm {
 PYBIND11_MODULE(penroz_comm, m) {
   m.doc() = "penroz native RCCL communicator (xGMI gradient all-reduce on a dedicated HIP stream)";
   pybind11::class_<RcclComm>(m, "RcclComm")
-      .def(pybind11::init<const std::string&, int, int, int>())
+      .def(pybind11::init<const std::string&, int, int, int, int>(), pybind11::arg("id"), pybind11::arg("rank"),
+           pybind11::arg("world"), pybind11::arg("device"), pybind11::arg("channels") = 0)
       .def_static("unique_id", [] { return pybind11::bytes(RcclComm::unique_id()); })
       .def("all_reduce_avg_async", &RcclComm::all_reduce_avg_async)
       .def("all_reduce_sum_async", &RcclComm::all_reduce_sum_async)
@@ -170,7 +184,8 @@ PYBIND11_MODULE(penroz_comm, m) {
       .def("wait_all", &RcclComm::wait_all)
       .def("synchronize", &RcclComm::synchronize)
       .def_property_readonly("rank", &RcclComm::rank)
-      .def_property_readonly("world", &RcclComm::world);
+      .def_property_readonly("world", &RcclComm::world)
+      .def_property_readonly("channels", &RcclComm::channels);
   m.def("version", [] {
     int v = 0;
     ncclGetVersion(&v);

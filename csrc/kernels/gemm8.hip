@@ -122,6 +122,14 @@ __device__ __forceinline__ void tile_coords8(int t, int tiles_m, int tiles_n, in
 __device__ __forceinline__ float bflo(uint32_t u) { return __uint_as_float(u << 16); }
 __device__ __forceinline__ float bfhi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
 
+// 16-B buffer store with a cache policy chosen at run time (ablation: 0 plain, 1 sc0, 2 nt, 3 sc0 nt)
+__device__ __forceinline__ void store_pol(u32x4 v, rsrc_t r, unsigned off, int pol) {
+  if (pol == 0) __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, 0);
+  else if (pol == 1) __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, 1);
+  else if (pol == 2) __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, 2);
+  else __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, 3);
+}
+
 #define PZ_BARRIER()                  \
   do {                                \
     asm volatile("" ::: "memory");    \
@@ -235,6 +243,9 @@ __global__ void __launch_bounds__(512, 1) gemm8_kernel(const bf16* __restrict__ 
   zero_acc();
   uint4 af[4][2], bfr[2][2][2];  // A: [m-frag][k-step]; B: [nb][n-frag][k-step]
 
+  // ablation (ablate >> 8): odd workgroups start that many s_sleep 127 late (de-synchronised epilogues)
+  if ((ablate >> 8) && (u & 1))
+    for (int i = 0; i < (ablate >> 8); ++i) __builtin_amdgcn_s_sleep(127);
   // ---- prologue: units 0-5 (k-tile 0 whole, k-tile 1's A_ma0 / B_nb0); the first two landed
   set_dma_tile(0);
   issue(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
@@ -344,7 +355,7 @@ __global__ void __launch_bounds__(512, 1) gemm8_kernel(const bf16* __restrict__ 
           if (ablate & 1) {
             asm volatile("" ::"v"(o.x), "v"(o.y), "v"(o.z), "v"(o.w));
           } else {
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rc, (int)off, 0, 0);
+            store_pol(__builtin_bit_cast(u32x4, o), rc, off, (ablate >> 4) & 3);
           }
           if constexpr (EPI == E8_BIAS_GELU) {
             const uint4 q = uint4{pack_bf16x2(gelu_f(bflo(o.x), approx), gelu_f(bfhi(o.x), approx)),
@@ -352,7 +363,7 @@ __global__ void __launch_bounds__(512, 1) gemm8_kernel(const bf16* __restrict__ 
                                   pack_bf16x2(gelu_f(bflo(o.z), approx), gelu_f(bfhi(o.z), approx)),
                                   pack_bf16x2(gelu_f(bflo(o.w), approx), gelu_f(bfhi(o.w), approx))};
             if (ablate & 1) asm volatile("" ::"v"(q.x), "v"(q.y), "v"(q.z), "v"(q.w));
-            else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, q), rc2, (int)off, 0, 0);
+            else store_pol(__builtin_bit_cast(u32x4, q), rc2, off, (ablate >> 4) & 3);
           }
         }
       }

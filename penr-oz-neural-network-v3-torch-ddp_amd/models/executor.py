@@ -501,7 +501,7 @@ class GPTExecutor:
         import os
         self._zero_gaps = None
         if (os.environ.get("PENROZ_GRAD_OVERWRITE", "1") == "0" or self.device.type != "cuda"
-                or not getattr(self, "_wgrad_ranges", None)):
+                or not getattr(self, "_wgrad_ranges", None) or getattr(self, "_wgrad_ranges_invalid", False)):
             return
         covered = sorted(self._wgrad_ranges.values())
         gaps, pos = [], 0
@@ -583,16 +583,33 @@ class GPTExecutor:
     def _wgrad_into(self, key: int, dy: Tensor, x: Tensor, g: Tensor):
         """g (+)= dyᵀ·x on the side stream: the first write of a range that zero_grad left alone
         overwrites it; the ranges are recorded during the first backward (see zero_grad)."""
+        rec = getattr(self, "_wgrad_ranges", None)
+        if rec is None:
+            rec = self._wgrad_ranges = {}
+        off = g.data_ptr() - self.flat_grad.data_ptr()
+        rng = (off // 4, off // 4 + g.numel())
+        if not getattr(self, "_ranges_learned", False):
+            if rec.get(key, rng) != rng:  # one key, several sub-ranges: not a plain overwrite
+                self._wgrad_ranges_invalid = True
+            rec[key] = rng
+        elif rec.get(key) != rng:
+            # a range zero_grad did not learn (e.g. a chunked wgrad writing sub-ranges under one
+            # key): zero_grad clears everything from the next step on; in this step the learned
+            # range, which zero_grad skipped, is cleared before the first write, then accumulated
+            self._wgrad_ranges_invalid = True
+            self._zero_gaps = None
+            fresh = getattr(self, "_fresh", None)
+            if fresh and key in fresh:
+                fresh.discard(key)
+                s_, e_ = rec[key]
+                stale = self.flat_grad[s_:e_]
+                self._side_call(dy, lambda: stale.zero_())
+            self._side_call(dy, lambda: gemm_ops.wgrad(dy, x, g, True))
+            return
         fresh = getattr(self, "_fresh", None)
         acc = not (fresh and key in fresh)
         if not acc:
             fresh.discard(key)
-        rec = getattr(self, "_wgrad_ranges", None)
-        if rec is None:
-            rec = self._wgrad_ranges = {}
-        if not getattr(self, "_ranges_learned", False):
-            off = g.data_ptr() - self.flat_grad.data_ptr()
-            rec[key] = (off // 4, off // 4 + g.numel())
         self._side_call(dy, lambda: gemm_ops.wgrad(dy, x, g, acc))
 
     def _finish_wgrad_bookkeeping(self):

@@ -31,6 +31,9 @@ import torch.distributed as dist
 log = logging.getLogger(__name__)
 
 SWEEP_SIZES_MB = (16, 32, 64, 128, 256)
+# native communicator channel counts tried on first contact (0 = RCCL's own choice); an MI355X
+# node has 7 xGMI links per GPU, so the useful counts are multiples of the rings RCCL lays over them
+SWEEP_CHANNELS = (0, 8, 16, 32)
 _LOG_DIR = "/tmp"
 
 
@@ -85,8 +88,15 @@ def _sync(device):
         torch.cuda.synchronize(device)
 
 
-def _native_or_none(device):
-    """The C++ communicator on every rank, or None on every rank (agreed over the c10d group)."""
+def _native_or_none(device, channels: int = 0):
+    """The C++ communicator (``channels`` > 0: built with exactly that many RCCL channels) on every
+    rank, or None on every rank (agreed over the c10d group).
+
+    A rank that refuses right away (module missing, duplicate device, init error) makes every
+    rank fall back. A rank that BLOCKS inside ncclCommInitRank while another refused cannot be
+    released: ncclCommInitRank has no timeout, so the guard timer ends that process with exit
+    code 124 after ``PENROZ_DIST_TIMEOUT`` — the failure conditions that can be checked without
+    RCCL (module import, distinct devices) are agreed on BEFORE any rank enters the init."""
     ok = torch.zeros(1, device=device)
     native = None
     # only where it can work: RCCL ranks (a gloo rehearsal of several ranks on one GPU makes RCCL
@@ -115,10 +125,10 @@ def _native_or_none(device):
         guard.start()
         built = torch.zeros(1, device=device)
         try:
-            native = rccl.NativeComm.get()
+            native = rccl.NativeComm.get(channels=channels)
             built += 1
         except RuntimeError as e:  # refused right away on this rank: everybody falls back to c10d
-            log.warning(f"native RCCL communicator unavailable: {e}")
+            log.warning(f"native RCCL communicator ({channels or 'default'} channels) unavailable: {e}")
         finally:
             guard.cancel()
         dist.all_reduce(built, op=dist.ReduceOp.MIN)
@@ -128,24 +138,38 @@ def _native_or_none(device):
 
 
 def sweep(device: torch.device, sizes_mb=SWEEP_SIZES_MB, wires=("fp32", "bf16"), transports=("c10d", "native"),
-          iters: int = 3, warmup: int = 1) -> list[dict]:
+          iters: int = 3, warmup: int = 1, channels=(0,)) -> list[dict]:
     """Time every (transport, wire, bucket size); max over ranks; correctness-checked.
+
+    ``channels``: the native communicator is swept once per channel count (0 = RCCL's own
+    choice; others build a communicator with exactly that many channels — the per-communicator
+    form of ``NCCL_MIN/MAX_NCHANNELS``); the extra counts are swept at fp32 only. Every row says
+    which (``channels``: None for c10d).
 
     The input on rank r is r + 1 everywhere, so the average is (n + 1) / 2 exactly in fp32 and
     bf16 (n ≤ 255); ``ok`` records whether the result matched on every rank."""
     world, rank = dist.get_world_size(), dist.get_rank()
     gloo = dist.get_backend() != "nccl"
-    native = _native_or_none(device) if "native" in transports else None
+    natives = {}
+    if "native" in transports:
+        for ch in channels:
+            c = _native_or_none(device, ch)
+            if c is None and ch == channels[0]:
+                break  # the communicator cannot be built at all
+            if c is not None:
+                natives[ch] = c
     expect = (world + 1) / 2.0
+    arms = [(tr, None) for tr in transports if tr != "native"] + [("native", ch) for ch in natives]
     rows = []
     for wire in wires:
         dt = {"fp32": torch.float32, "bf16": torch.bfloat16}[wire]
         for mb in sizes_mb:
             n = int(mb * 2**20) // 4  # elements of an fp32 gradient bucket of that size
             buf = torch.empty(n, device=device, dtype=dt)
-            for tr in transports:
-                if tr == "native" and native is None:
+            for tr, ch in arms:
+                if tr == "native" and wire != "fp32" and ch != channels[0]:
                     continue
+                native = natives.get(ch)
 
                 def one():
                     if tr == "native":
@@ -176,11 +200,76 @@ def sweep(device: torch.device, sizes_mb=SWEEP_SIZES_MB, wires=("fp32", "bf16"),
                 sec = float(t.item())
                 nbytes = buf.numel() * buf.element_size()
                 alg = nbytes / sec / 1e9
-                rows.append({"transport": tr, "wire": wire, "bucket_mb": mb, "ms": round(sec * 1e3, 4),
+                rows.append({"transport": tr, "channels": ch, "wire": wire, "bucket_mb": mb, "ms": round(sec * 1e3, 4),
                              "algbw_GBps": round(alg, 2), "busbw_GBps": round(alg * 2 * (world - 1) / world, 2),
                              "ok": bool(good.item() > 0)})
             del buf
     return rows
+
+
+def _arm_rows(rows, transport, channels, wire="fp32"):
+    return [r for r in rows if r["transport"] == transport and r["wire"] == wire and r["ok"]
+            and (transport != "native" or r.get("channels", 0) == channels)]
+
+
+def plan(rows: list[dict], grad_bytes: int, backward_ms: float | None = None, margin: float = 1.03,
+         bf16_gain: float = 1.2) -> dict:
+    """The whole gradient-sync configuration from one sweep, each transport judged at ITS OWN size:
+
+    1. every correct (transport, channel count) arm gets its bucket size from :func:`choose_bucket`'s
+       rule (the smallest size within 90 % of that arm's best bus bandwidth);
+    2. the native communicator wins only if its best arm's bus bandwidth, at that arm's size, is
+       ≥ ``margin`` × c10d's at c10d's size (the channel count comes with the arm);
+    3. the wire: fp32 (the reference DDP's) unless the predicted fp32 all-reduce of the whole
+       gradient (``grad_bytes`` / algbw at the chosen size) exceeds ``backward_ms`` — it could not
+       hide behind the backward — and the bf16 wire of the same transport, correct at that size,
+       is ≥ ``bf16_gain`` × faster for the whole gradient.
+
+    Returns {"transport", "channels", "bucket_mb", "wire", "predicted_fp32_ms", ...,"reason"}."""
+    out = {"transport": "c10d", "channels": None, "bucket_mb": None, "wire": "fp32"}
+    c_rows = _arm_rows(rows, "c10d", None)
+    if not c_rows:
+        out["reason"] = "no correct c10d rows"
+        return out
+    arms = {("c10d", None): c_rows}
+    for ch in sorted({r.get("channels", 0) for r in rows if r["transport"] == "native"}):
+        nr = _arm_rows(rows, "native", ch)
+        if nr:
+            arms[("native", ch)] = nr
+    picked = {}
+    for key, ar in arms.items():
+        best = max(r["busbw_GBps"] for r in ar)
+        pick = min((r for r in ar if r["busbw_GBps"] >= 0.9 * best), key=lambda r: r["bucket_mb"])
+        picked[key] = pick
+    c = picked[("c10d", None)]
+    nat = [(k, r) for k, r in picked.items() if k[0] == "native"]
+    choice_key, choice = ("c10d", None), c
+    if nat:
+        nk, nr = max(nat, key=lambda kv: kv[1]["busbw_GBps"])
+        if nr["busbw_GBps"] >= margin * c["busbw_GBps"]:
+            choice_key, choice = nk, nr
+        out["reason"] = (f"native ({nk[1] or 'default'} channels) {nr['busbw_GBps']} GB/s at {nr['bucket_mb']} MB vs "
+                         f"c10d {c['busbw_GBps']} GB/s at {c['bucket_mb']} MB")
+    else:
+        out["reason"] = "no correct native arm"
+    out.update(transport=choice_key[0], channels=choice_key[1], bucket_mb=choice["bucket_mb"],
+               busbw_GBps=choice["busbw_GBps"])
+    fp32_ms = grad_bytes / (choice["algbw_GBps"] * 1e9) * 1e3
+    out["predicted_fp32_ms"] = round(fp32_ms, 3)
+    bf = [r for r in rows if r["transport"] == choice_key[0] and r["wire"] == "bf16" and r["ok"]
+          and r["bucket_mb"] == choice["bucket_mb"]
+          and (choice_key[0] != "native" or r.get("channels", 0) == choice_key[1])]
+    if bf:
+        bf16_ms = (grad_bytes / 2) / (bf[0]["algbw_GBps"] * 1e9) * 1e3
+        out["predicted_bf16_ms"] = round(bf16_ms, 3)
+        if backward_ms is not None and fp32_ms > backward_ms and fp32_ms >= bf16_gain * bf16_ms:
+            out["wire"] = "bf16"
+            out["wire_reason"] = (f"fp32 all-reduce {fp32_ms:.1f} ms > backward {backward_ms:.1f} ms; "
+                                  f"bf16 {bf16_ms:.1f} ms")
+    if "wire_reason" not in out:
+        out["wire_reason"] = ("no backward estimate" if backward_ms is None else
+                              f"fp32 all-reduce {fp32_ms:.1f} ms vs backward {backward_ms:.1f} ms")
+    return out
 
 
 def choose(rows: list[dict], bucket_mb: float, margin: float = 1.03) -> dict:

@@ -26,22 +26,37 @@ def load_module():
 class NativeComm:
     _instances: dict = {}
 
-    def __init__(self, group=None, key: str = "penroz_rccl_uid"):
+    def __init__(self, group=None, key: str = "penroz_rccl_uid", channels: int = 0):
         mod = load_module()
         rank, world = dist.get_rank(group), dist.get_world_size(group)
         store = dist.distributed_c10d._get_default_store()
+        key = f"{key}_c{channels}"  # one unique id per communicator
         if rank == 0:
             store.set(key, mod.RcclComm.unique_id())
         uid = store.get(key)
-        self.comm = mod.RcclComm(bytes(uid), rank, world, torch.cuda.current_device())
-        self.rank, self.world = rank, world
+        self.comm = mod.RcclComm(bytes(uid), rank, world, torch.cuda.current_device(), channels)
+        self.rank, self.world, self.channels = rank, world, channels
+
+    @staticmethod
+    def default_channels() -> int:
+        """Channel count for :meth:`get` without an explicit one: ``PENROZ_RCCL_CHANNELS`` (set
+        by the first-contact sweep when a fixed count beat RCCL's own choice), else 0 = RCCL's."""
+        return int(os.environ.get("PENROZ_RCCL_CHANNELS", "0") or 0)
 
     @classmethod
-    def get(cls, group=None) -> "NativeComm":
-        k = id(group)
+    def get(cls, group=None, channels: int | None = None) -> "NativeComm":
+        ch = cls.default_channels() if channels is None else channels
+        k = (id(group), ch)
         if k not in cls._instances:
-            cls._instances[k] = NativeComm(group)
+            cls._instances[k] = NativeComm(group, channels=ch)
         return cls._instances[k]
+
+    @classmethod
+    def release(cls, group=None, keep: int | None = None):
+        """Destroy this group's communicators except the one with ``keep`` channels (the sweep
+        builds one per channel count; only the chosen one stays alive)."""
+        for k in [k for k in cls._instances if k[0] == id(group) and k[1] != keep]:
+            del cls._instances[k]
 
     def all_reduce_avg_async(self, t: torch.Tensor) -> int:
         """Launch; returns the handle :meth:`wait` takes."""

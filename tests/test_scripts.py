@@ -108,7 +108,9 @@ def test_bench_self_launches_ranks_cpu_gloo():
     sweep = d["comm"]["sweep"]
     assert {r["bucket_mb"] for r in sweep} == {1, 4} and {r["wire"] for r in sweep} == {"fp32", "bf16"}
     assert all(r["ok"] and r["busbw_GBps"] > 0 and r["transport"] == "c10d" for r in sweep)
-    assert d["comm"]["choice"]["transport"] == "c10d"
+    pl = d["comm"]["plan"]
+    assert pl["transport"] == "c10d" and pl["wire"] == "fp32" and pl["channels"] is None
+    assert pl["grad_bytes"] > 0 and pl["backward_ms_estimate"] > 0 and "predicted_fp32_ms" in pl
     assert set(d["comm"]["rccl"]) == {"coll_channels", "log"}
 
 
@@ -131,6 +133,54 @@ def test_comm_choice_rules():
     # nearest swept size to the reducer's bucket decides
     rows = [row("c10d", 100, mb=32), row("native", 90, mb=32), row("c10d", 100, mb=128), row("native", 150, mb=128)]
     assert choose(rows, 100)["transport"] == "native" and choose(rows, 40)["transport"] == "c10d"
+
+
+def _prow(tr, mb, bw, ok=True, wire="fp32", ch=None):
+    # busbw at world 8 = algbw * 2 * 7 / 8
+    return {"transport": tr, "channels": ch if tr == "native" else None, "wire": wire, "bucket_mb": mb,
+            "busbw_GBps": bw, "algbw_GBps": bw * 8 / 14, "ok": ok}
+
+
+def test_comm_plan_judges_each_transport_at_its_own_bucket():
+    """the transport is compared at each arm's own chosen bucket size, not at a fixed 64 MB."""
+    from penroz.parallel.commtune import plan
+    rows = [_prow("c10d", 16, 100), _prow("c10d", 64, 104),
+            _prow("native", 16, 70, ch=0), _prow("native", 64, 130, ch=0)]
+    p = plan(rows, grad_bytes=652 * 2**20)
+    # c10d's size is 16 MB (within 90 % of its best), native's 64 MB: 130 vs 100 -> native at 64 MB
+    assert p["transport"] == "native" and p["bucket_mb"] == 64 and p["channels"] == 0
+    rows = [_prow("c10d", 16, 120), _prow("native", 16, 70, ch=0), _prow("native", 64, 121, ch=0)]
+    assert plan(rows, grad_bytes=1)["transport"] == "c10d"  # inside the 3 % margin
+    rows = [_prow("c10d", 16, 120), _prow("native", 64, 300, ok=False, ch=0)]
+    assert plan(rows, grad_bytes=1)["transport"] == "c10d"  # wrong sums never win
+
+
+def test_comm_plan_picks_channel_count():
+    """The channel count comes with the winning native arm (NCCL_MIN/MAX_NCHANNELS)."""
+    from penroz.parallel.commtune import plan
+    rows = [_prow("c10d", 64, 100), _prow("native", 64, 110, ch=0), _prow("native", 64, 160, ch=16),
+            _prow("native", 64, 140, ch=32), _prow("native", 32, 170, ok=False, ch=8)]
+    p = plan(rows, grad_bytes=652 * 2**20)
+    assert p["transport"] == "native" and p["channels"] == 16 and p["busbw_GBps"] == 160
+    assert "16 channels" in p["reason"]
+
+
+def test_comm_plan_bf16_wire_only_when_exposed():
+    """bf16 wire only when the predicted fp32 all-reduce of the whole gradient exceeds the backward
+    and the bf16 arm is correct and clearly faster."""
+    from penroz.parallel.commtune import plan
+    rows = [_prow("c10d", 64, 100), _prow("c10d", 64, 100, wire="bf16")]
+    g = 6550 * 2**20  # GPT-2 XL fp32 gradients
+    fp32_ms = g / (100 * 8 / 14 * 1e9) * 1e3
+    assert plan(rows, g, backward_ms=fp32_ms * 2)["wire"] == "fp32"     # hidden behind the backward
+    p = plan(rows, g, backward_ms=fp32_ms / 2)
+    assert p["wire"] == "bf16" and abs(p["predicted_bf16_ms"] * 2 - p["predicted_fp32_ms"]) < 0.01
+    assert plan(rows, g, backward_ms=None)["wire"] == "fp32"            # no estimate, no change
+    bad = [_prow("c10d", 64, 100), _prow("c10d", 64, 100, wire="bf16", ok=False)]
+    assert plan(bad, g, backward_ms=1.0)["wire"] == "fp32"              # wrong bf16 sums
+    slow = [_prow("c10d", 64, 100), _prow("c10d", 64, 40, wire="bf16")]
+    assert plan(slow, g, backward_ms=1.0)["wire"] == "fp32"             # bf16 not faster overall
+    assert plan([], g)["transport"] == "c10d"
 
 
 def test_comm_bucket_choice_rule(monkeypatch):
