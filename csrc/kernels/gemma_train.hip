@@ -269,7 +269,8 @@ using namespace penroz;
     else if (need <= 8) { constexpr int NCH = 8; __VA_ARGS__; } \
     else if (need <= 10) { constexpr int NCH = 10; __VA_ARGS__; } \
     else if (need <= 12) { constexpr int NCH = 12; __VA_ARGS__; } \
-    else { constexpr int NCH = 16; __VA_ARGS__; }               \
+    else if (need <= 16) { constexpr int NCH = 16; __VA_ARGS__; } \
+    else { constexpr int NCH = 24; __VA_ARGS__; }               \
   }()
 
 static void gm_check_rows(const torch::Tensor& t, int64_t N, int64_t C, c10::ScalarType dt, const char* what) {
@@ -295,7 +296,7 @@ void gemma_combine_fwd(int64_t mode, torch::Tensor x, c10::optional<torch::Tenso
                        c10::optional<torch::Tensor> s_save, c10::optional<torch::Tensor> r1, torch::Tensor r2) {
   TORCH_CHECK(mode >= 0 && mode <= 3, "gemma combine: mode 0..3");
   const int64_t N = x.size(0), C = x.size(1);
-  TORCH_CHECK(x.dim() == 2 && C % 4 == 0 && C <= 4096, "gemma combine: C % 4 == 0, C <= 4096");
+  TORCH_CHECK(x.dim() == 2 && C % 4 == 0 && C <= 6144, "gemma combine: C % 4 == 0, C <= 6144");
   gm_check_rows(x, N, C, torch::kFloat32, "x");
   gm_check_rows(y_out, N, C, torch::kBFloat16, "y");
   TORCH_CHECK(w2.is_contiguous() && w2.numel() == C && w2.scalar_type() == torch::kFloat32, "gemma combine: w2");
@@ -333,7 +334,7 @@ void gemma_combine_bwd(int64_t mode, torch::Tensor dy, c10::optional<torch::Tens
                        c10::optional<torch::Tensor> dw1, torch::Tensor dw2, c10::optional<torch::Tensor> dh_save) {
   TORCH_CHECK(mode >= 0 && mode <= 3, "gemma combine: mode 0..3");
   const int64_t N = h.size(0), C = h.size(1);
-  TORCH_CHECK(h.dim() == 2 && C % 4 == 0 && C <= 4096, "gemma combine: C % 4 == 0, C <= 4096");
+  TORCH_CHECK(h.dim() == 2 && C % 4 == 0 && C <= 6144, "gemma combine: C % 4 == 0, C <= 6144");
   gm_check_rows(dy, N, C, torch::kBFloat16, "dy");
   gm_check_rows(h, N, C, torch::kFloat32, "h");
   gm_check_rows(dx, N, C, torch::kFloat32, "dx");

@@ -63,6 +63,13 @@ class _GBlock:
     mlp: L.GatedMLP
     post_attn: L.RMSNorm | None
     post_mlp: L.RMSNorm | None
+    # this block's shapes: Gemma 4 layer lists are heterogeneous (full-attention layers with
+    # global_head_dim / their own KV-head count, double-wide MLPs on KV-shared layers:
+    # reference mappers.py:206-233)
+    H: int = 0
+    Hkv: int = 0
+    D: int = 0
+    F: int = 0
 
 
 @dataclass
@@ -74,10 +81,11 @@ class GemmaSpec:
     head: nn.Linear
     blocks: list = field(default_factory=list)
     mode: int = 2            # 0: post-norm on the residual (Gemma 3+), 1: on the branch (Gemma 2), 2: none
-    H: int = 0
+    H: int = 0               # the first block's shapes (every block's when ``uniform``)
     Hkv: int = 0
     D: int = 0
     F: int = 0
+    uniform: bool = True
     act: int = 1
     param_dtype: torch.dtype = torch.float32
 
@@ -103,7 +111,7 @@ class GemmaExecutor(GPTExecutor):
         if head.weight is emb.weight:  # a tied head would be one parameter in two flat slots
             return None
         C = emb.embedding_dim
-        if C % 8 or C > 4096 or head.in_features != C or ls[-2].weight.numel() != C:
+        if C % 8 or C > 6144 or head.in_features != C or ls[-2].weight.numel() != C:
             return None
         spec = GemmaSpec(V=emb.num_embeddings, C=C, emb=emb, norm_f=ls[-2], head=head)
         modes, shapes, acts = set(), set(), set()
@@ -140,11 +148,14 @@ class GemmaExecutor(GPTExecutor):
             modes.add(mode)
             shapes.add((H, Hkv, D, F))
             acts.add(mlp.act_kind)
-            spec.blocks.append(_GBlock(in_norm, qkv, attn, o, pre, mlp, blk.post_attn_norm, blk.post_mlp_norm))
-        if not spec.blocks or len(modes) != 1 or len(shapes) != 1 or len(acts) != 1:
+            spec.blocks.append(_GBlock(in_norm, qkv, attn, o, pre, mlp, blk.post_attn_norm, blk.post_mlp_norm,
+                                       H, Hkv, D, F))
+        if not spec.blocks or len(modes) != 1 or len(acts) != 1:
             return None
         spec.mode = modes.pop()
-        spec.H, spec.Hkv, spec.D, spec.F = shapes.pop()
+        b0 = spec.blocks[0]
+        spec.H, spec.Hkv, spec.D, spec.F = b0.H, b0.Hkv, b0.D, b0.F
+        spec.uniform = len(shapes) == 1
         spec.act = _ACT_KIND[acts.pop()]
         dtypes = {p.dtype for p in model.parameters()}
         if len(dtypes) != 1 or not dtypes <= ({torch.float32} if require_fp32 else {torch.float32, torch.bfloat16}):
@@ -191,12 +202,12 @@ class GemmaExecutor(GPTExecutor):
     def gu_bf16(self, b: _GBlock) -> Tensor:
         """The [gate; up] bf16 weight [2F, C] (adjacent in the flat buffer)."""
         off = self.offsets[id(b.mlp.gate_proj.weight)]
-        F, C = self.spec.F, self.spec.C
+        F, C = b.F, self.spec.C
         return self.shadow[off:off + 2 * F * C].view(2 * F, C)
 
     def gu_grad(self, b: _GBlock) -> Tensor:
         off = self.offsets[id(b.mlp.gate_proj.weight)]
-        F, C = self.spec.F, self.spec.C
+        F, C = b.F, self.spec.C
         return self.flat_grad[off:off + 2 * F * C].view(2 * F, C)
 
     # ---- transposed bf16 weight copies for the data-gradient GEMMs (see GPTExecutor) ---------
@@ -253,22 +264,22 @@ class GemmaExecutor(GPTExecutor):
         if self._acts_shape == (B, T):
             return
         s, dev = self.spec, self.device
-        N, C, F, V = B * T, s.C, s.F, s.V
-        QKV = (s.H + 2 * s.Hkv) * s.D
-        A = s.H * s.D
+        N, C, V = B * T, s.C, s.V
+        bs = s.blocks
         bf, f32 = torch.bfloat16, torch.float32
         Lc = self.L
         e = lambda *shape, dt=bf: torch.empty(*shape, dtype=dt, device=dev)  # noqa: E731
+        qkv_w = lambda b: (b.H + 2 * b.Hkv) * b.D  # noqa: E731
         # resid[l]: block l input (fp32); mid[l]: after the attention combine
         self.resid = [e(N, C, dt=f32) for _ in range(Lc + 1)]
         self.mid = [e(N, C, dt=f32) for _ in range(Lc)]
         self.y_in = [e(N, C) for _ in range(Lc)]       # input norm outputs (QKV GEMM inputs)
         self.y_mlp = [e(N, C) for _ in range(Lc)]      # pre-MLP norm outputs (gate|up inputs)
-        self.qkv = [e(N, QKV) for _ in range(Lc)]      # post-RoPE (attention inputs)
-        self.att = [e(N, A) for _ in range(Lc)]
-        self.lse = [e(B, s.H, T, dt=f32) for _ in range(Lc)]
-        self.gu = [e(N, 2 * F) for _ in range(Lc)]
-        self.g = [e(N, F) for _ in range(Lc)]
+        self.qkv = [e(N, qkv_w(b)) for b in bs]         # post-RoPE (attention inputs)
+        self.att = [e(N, b.H * b.D) for b in bs]
+        self.lse = [e(B, b.H, T, dt=f32) for b in bs]
+        self.gu = [e(N, 2 * b.F) for b in bs]
+        self.g = [e(N, b.F) for b in bs]
         mode = s.mode
         # norm statistics: r_in[l] (input norm of block l), r_pa / r_pre (attention combine),
         # r_pm (post-MLP combine's post-norm); the post-norm inputs the backward re-reads
@@ -289,16 +300,25 @@ class GemmaExecutor(GPTExecutor):
         self.head_chunk = _head_chunk_rows(N, V)
         self._head_bufs = [e(self.head_chunk, (V + 7) // 8 * 8) for _ in range(2 if self.head_chunk < N else 1)]
         self.tmp_c = e(N, C)                               # branch outputs (O / down GEMMs)
-        self.qkv_raw = e(N, QKV)                           # QKV GEMM output before RoPE
+        # per-block scratch shared by all blocks: flat buffers sized for the widest block, viewed
+        # per block as [N, width] (``_rows``); a view keeps the buffer's data_ptr, so the
+        # side-stream reuse events (``_reuse``) still key on the buffer
+        QKV, A, F = max(qkv_w(b) for b in bs), max(b.H * b.D for b in bs), max(b.F for b in bs)
+        self.qkv_raw = e(N * QKV)                          # QKV GEMM output before RoPE
         self.dresid = e(N, C, dt=f32)
         self.d_branch2 = [e(N, C) for _ in range(2)]       # rotating: read by side-stream wgrads
-        self.d_g = e(N, F)
-        self.d_gu2 = [e(N, 2 * F) for _ in range(2)]
-        self.d_att2 = [e(N, A) for _ in range(2)]
-        self.d_qkv = e(N, QKV)
-        self.d_qkv_raw2 = [e(N, QKV) for _ in range(2)]
+        self.d_g = e(N * F)
+        self.d_gu2 = [e(N * 2 * F) for _ in range(2)]
+        self.d_att2 = [e(N * A) for _ in range(2)]
+        self.d_qkv = e(N * QKV)
+        self.d_qkv_raw2 = [e(N * QKV) for _ in range(2)]
         self.d_c = e(N, C)
         self._acts_shape = (B, T)
+
+    @staticmethod
+    def _rows(buf: Tensor, N: int, width: int) -> Tensor:
+        """[N, width] view of the front of a flat per-block scratch buffer."""
+        return buf[: N * width].view(N, width)
 
     def free_buffers(self):
         for name in ("resid", "mid", "y_in", "y_mlp", "qkv", "att", "lse", "gu", "g", "r_in", "r_pre", "r_pa",
@@ -310,10 +330,10 @@ class GemmaExecutor(GPTExecutor):
 
     def _rope(self, b: _GBlock, T: int):
         a = b.attn
-        key = (a.rope_theta, self.spec.D, T)
+        key = (a.rope_theta, b.D, T)
         tab = self._rope_tables.get(key)
         if tab is None:
-            inv = a._inv_freq(self.spec.D, self.device)
+            inv = a._inv_freq(b.D, self.device)
             tab = self._rope_tables[key] = rope_ops.rope_table(inv, 0, T, self.device)
         return tab
 
@@ -328,7 +348,8 @@ class GemmaExecutor(GPTExecutor):
         s = self.spec
         B, T = idx.shape
         self._alloc(B, T)
-        H, Hkv, D, C, mode = s.H, s.Hkv, s.D, s.C, s.mode
+        C, mode = s.C, s.mode
+        N = B * T
         f = self.f32
         k = _ext.kernels()
         # scaled embedding (fp32 rows of the master table)
@@ -337,9 +358,11 @@ class GemmaExecutor(GPTExecutor):
         self._combine_fwd(3, self.resid[0], None, None, f(b0.in_norm.weight), 0.0, b0.in_norm.eps, None,
                           self.y_in[0], None, None, self.r_in[0])
         for l, b in enumerate(s.blocks):
-            self._mm(self.y_in[l], self.bf16(b.qkv.weight), self.qkv_raw)
+            H, Hkv, D = b.H, b.Hkv, b.D
+            qkv_raw = self._rows(self.qkv_raw, N, (H + 2 * Hkv) * D)
+            self._mm(self.y_in[l], self.bf16(b.qkv.weight), qkv_raw)
             cos, sin = self._rope(b, T)
-            k.rope_qkv(self.qkv_raw.view(B, T, -1), cos, sin, H, Hkv, D, False, self.qkv[l])
+            k.rope_qkv(qkv_raw.view(B, T, -1), cos, sin, H, Hkv, D, False, self.qkv[l])
             p = b.attn.dropout if training else 0.0
             attn_ops.flash_fwd(self.qkv[l].view(B, T, -1), H, Hkv, D, p, dropout_seed + l,
                                out=self.att[l].view(B, T, H * D), lse=self.lse[l])
@@ -374,7 +397,6 @@ class GemmaExecutor(GPTExecutor):
         s = self.spec
         B, T = idx.shape
         N, C, mode = B * T, s.C, s.mode
-        H, Hkv, D = s.H, s.Hkv, s.D
         seed = self._step_seed
         self._step_seed += 1000
         f, gr = self.f32, self.grad
@@ -422,12 +444,15 @@ class GemmaExecutor(GPTExecutor):
             layer_range = trace_range(f"backward.block{l}")
             layer_range.__enter__()
             b = s.blocks[l]
+            H, Hkv, D = b.H, b.Hkv, b.D
+            QKV = (H + 2 * Hkv) * D
             db = self.d_branch2[rb]
             # ---- MLP: down dgrad / wgrad, packed gated backward, gate|up dgrad / wgrad
-            torch.mm(db, self._dgrad(b.mlp.down_proj.weight, self.bf16(b.mlp.down_proj.weight)), out=self.d_g)
+            d_g = self._rows(self.d_g, N, b.F)
+            torch.mm(db, self._dgrad(b.mlp.down_proj.weight, self.bf16(b.mlp.down_proj.weight)), out=d_g)
             self._wgrad(db, self.g[l], b.mlp.down_proj.weight)
-            dgu = self._reuse(self.d_gu2[l & 1])
-            k.gated_act_bwd_packed(self.d_g, self.gu[l], dgu, s.act)
+            dgu = self._rows(self._reuse(self.d_gu2[l & 1]), N, 2 * b.F)
+            k.gated_act_bwd_packed(d_g, self.gu[l], dgu, s.act)
             torch.mm(dgu, self._dgrad(b.mlp.gate_proj.weight, self.gu_bf16(b)), out=self.d_c)
             self._wgrad_into(id(b.mlp.gate_proj.weight), dgu, self.y_mlp[l], self.gu_grad(b))
             # ---- attention combine: dy = d(pre-MLP norm output), dh_in = dresid (grad of mid[l])
@@ -439,14 +464,15 @@ class GemmaExecutor(GPTExecutor):
                               f(pa.weight) if pa is not None else None, f(b.pre_mlp.weight), self.dresid, db,
                               gr(pa.weight) if pa is not None else None, gr(b.pre_mlp.weight))
             # ---- attention: O dgrad / wgrad, flash backward, inverse RoPE, QKV dgrad / wgrad
-            datt = self._reuse(self.d_att2[l & 1])
+            datt = self._rows(self._reuse(self.d_att2[l & 1]), N, H * D)
             torch.mm(db, self._dgrad(b.o.weight, self.bf16(b.o.weight)), out=datt)
             self._wgrad(db, self.att[l], b.o.weight)
+            d_qkv = self._rows(self.d_qkv, N, QKV)
             attn_ops.flash_bwd(datt.view(B, T, H * D), self.qkv[l].view(B, T, -1), self.att[l].view(B, T, H * D),
-                               self.lse[l], H, Hkv, D, b.attn.dropout, seed + l, dqkv=self.d_qkv.view(B, T, -1))
+                               self.lse[l], H, Hkv, D, b.attn.dropout, seed + l, dqkv=d_qkv.view(B, T, -1))
             cos, sin = self._rope(b, T)
-            dqr = self._reuse(self.d_qkv_raw2[l & 1])
-            k.rope_qkv(self.d_qkv.view(B, T, -1), cos, sin, H, Hkv, D, True, dqr)
+            dqr = self._rows(self._reuse(self.d_qkv_raw2[l & 1]), N, QKV)
+            k.rope_qkv(d_qkv.view(B, T, -1), cos, sin, H, Hkv, D, True, dqr)
             torch.mm(dqr, self._dgrad(b.qkv.weight, self.bf16(b.qkv.weight)), out=self.d_c)
             self._wgrad(dqr, self.y_in[l], b.qkv.weight)
             # ---- the combine that produced y_in[l]: block l-1's MLP combine (or the embedding norm)

@@ -87,12 +87,14 @@ def build_module(name: str, sources: list[str], extra_libs: list[str], jobs: int
     _, tlib, _ = _torch_paths()
     target = os.path.join(OUT, name + _ext_suffix())
     if todo or not os.path.exists(target):
-        link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", target] + objs + [
+        tmp = target + ".tmp"  # link aside, then rename: a snapshot of the tree never sees half a .so
+        link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs + [
             f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
             "-lamdhip64", f"-Wl,-rpath,{tlib}"] + extra_libs
         r = subprocess.run(link, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed for {name}\n{' '.join(link)}\n{r.stdout}\n{r.stderr}")
+        os.replace(tmp, target)
         print(f"[build] linked {target}", flush=True)
     return target
 

@@ -75,3 +75,27 @@ def test_gemma_executor_pattern_match_modes():
     import bench
     g = NeuralNetworkModel("t", Mapper(bench.gpt2_layers(V=64, C=64, L=1, H=1, P=32), {"adamw": {"lr": 1e-3}}))
     assert GemmaExecutor.match(g) is None
+
+
+def test_gemma_executor_matches_heterogeneous_gemma4_layer_list():
+    """Gemma 4 layer lists (reference mappers.py:206-233) lower to the fused executor with
+    per-block shapes: global_head_dim / KV heads on full-attention layers, double-wide MLPs on
+    KV-shared layers; C up to 6144 (Gemma-3 27B: 5376)."""
+    from types import SimpleNamespace
+    from penroz.models.gemma_executor import GemmaExecutor
+    from penroz.models.mapper import Mapper
+    from penroz.models.model import NeuralNetworkModel
+    cfg = SimpleNamespace(model_type="gemma4", vocab_size=64, hidden_size=64, intermediate_size=128,
+                          num_hidden_layers=4, num_attention_heads=2, num_key_value_heads=2, head_dim=64,
+                          rms_norm_eps=1e-6, rope_theta=10000.0, attention_dropout=0.0,
+                          hidden_activation="gelu_pytorch_tanh",
+                          layer_types=["sliding_attention", "full_attention"] * 2, global_head_dim=128,
+                          num_global_key_value_heads=1, num_kv_shared_layers=2, use_double_wide_mlp=True)
+    m = NeuralNetworkModel("g4", Mapper(Mapper.from_hf_config(cfg), {"adamw": {"lr": 1e-3}}))
+    spec = GemmaExecutor.match(m)
+    assert spec is not None and not spec.uniform
+    assert [(b.H, b.Hkv, b.D, b.F) for b in spec.blocks] == [(2, 2, 64, 128), (2, 1, 128, 128), (2, 2, 64, 256),
+                                                            (2, 1, 128, 256)]
+    wide = SimpleNamespace(**{**vars(cfg), "hidden_size": 5376, "num_hidden_layers": 1, "layer_types": None,
+                              "intermediate_size": 64, "vocab_size": 16})
+    assert GemmaExecutor.match(NeuralNetworkModel("w", Mapper(Mapper.from_hf_config(wide), {"adamw": {}}))) is not None

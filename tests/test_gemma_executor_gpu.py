@@ -27,12 +27,13 @@ from penroz.ops import _ext
 DEV = "cuda"
 
 
-def _gemma(model_type="gemma3_text", V=512, C=256, L=2, H=4, Hkv=2, D=64, F=512, seed=0, act="gelu_pytorch_tanh"):
+def _gemma(model_type="gemma3_text", V=512, C=256, L=2, H=4, Hkv=2, D=64, F=512, seed=0, act="gelu_pytorch_tanh",
+           **extra):
     torch.manual_seed(seed)
     cfg = SimpleNamespace(model_type=model_type, vocab_size=V, hidden_size=C, intermediate_size=F, num_hidden_layers=L,
                           num_attention_heads=H, num_key_value_heads=Hkv, head_dim=D, rms_norm_eps=1e-6,
                           rope_theta=10000.0, rope_local_base_freq=10000.0, attention_dropout=0.0,
-                          hidden_activation=act, query_pre_attn_scalar=D, sliding_window=512)
+                          hidden_activation=act, query_pre_attn_scalar=D, sliding_window=512, **extra)
     m = NeuralNetworkModel("g", Mapper(Mapper.from_hf_config(cfg), {"adamw": {"lr": 1e-3, "betas": [0.9, 0.95]}}))
     with torch.no_grad():  # non-trivial norm weights, so every dγ path carries signal
         for n, p in m.named_parameters():
@@ -74,6 +75,67 @@ def test_one_step_matches_fp32_reference(model_type):
         worst = max(worst, rel)
         assert rel < 5e-2, f"{model_type} {n}: rel grad err {rel}"
     print(f"{model_type}: loss {loss.item():.5f} vs {loss_ref.item():.5f}, worst rel grad err {worst:.4f}")
+
+
+# Gemma-4-like heterogeneous layer list (reference mappers.py:206-233): alternating sliding / full
+# attention, the full layers with global_head_dim and their own KV-head count, the last two layers
+# KV-shared with double-wide MLPs
+GEMMA4 = dict(layer_types=["sliding_attention", "full_attention", "sliding_attention", "full_attention"],
+              global_head_dim=128, num_global_key_value_heads=1, num_kv_shared_layers=2, use_double_wide_mlp=True)
+
+
+def test_match_heterogeneous_gemma4_layer_list():
+    spec = GemmaExecutor.match(_gemma("gemma4", L=4, F=256, **GEMMA4))
+    assert spec is not None and not spec.uniform and spec.mode == 0
+    assert [(b.H, b.Hkv, b.D, b.F) for b in spec.blocks] == [(4, 2, 64, 256), (4, 1, 128, 256), (4, 2, 64, 512),
+                                                            (4, 1, 128, 512)]
+
+
+def test_heterogeneous_gemma4_one_step_matches_fp32_reference():
+    m = _gemma("gemma4", L=4, F=256, **GEMMA4).to(DEV)
+    ref = copy.deepcopy(m)
+    B, T = 2, 128
+    g = torch.Generator(device=DEV).manual_seed(3)
+    x = torch.randint(0, 512, (B, T), device=DEV, generator=g)
+    y = torch.randint(0, 512, (B, T), device=DEV, generator=g)
+    _ext.FORCE_TORCH = True
+    try:
+        _, loss_ref = ref(x, y, skip_softmax=True)
+        loss_ref.backward()
+    finally:
+        _ext.FORCE_TORCH = False
+    ex = GemmaExecutor(m, torch.device(DEV))
+    ex.setup_training(False)
+    ex.zero_grad()
+    loss = ex.train_micro_step(x, y, 1.0)
+    assert abs(loss.item() - loss_ref.item()) < 2e-2, (loss.item(), loss_ref.item())
+    for (n, p), (_, r) in zip(m.named_parameters(), ref.named_parameters()):
+        rel = ((ex.grad(p) - r.grad).norm() / (r.grad.norm() + 1e-12)).item()
+        assert rel < 5e-2, f"gemma4 {n}: rel grad err {rel}"
+
+
+def test_heterogeneous_gemma4_loss_curve_matches_generic_engine():
+    g = torch.Generator(device=DEV).manual_seed(4)
+    base = torch.randint(0, 400, (2, 129), device=DEV, generator=g)
+    data = [(base[:, :-1].contiguous(), base[:, 1:].contiguous())]
+    curves = {}
+    for engine in ("fused", "generic"):
+        m = _gemma("gemma4", L=4, F=256, seed=1, **GEMMA4).to(DEV)
+        runner = _make_runner(m, engine, torch.device(DEV), False)
+        if engine == "fused":
+            assert isinstance(runner.exec, GemmaExecutor)
+        m.train()
+        losses = []
+        for i in range(100):
+            x, y = data[0]
+            runner.zero_grad()
+            losses.append(float(runner.micro_step(x, y, 1.0, True, True, False)))
+            runner.step()
+        curves[engine] = losses
+    fused, generic = curves["fused"], curves["generic"]
+    assert fused[-1] < fused[0] - 2.0 and generic[-1] < generic[0] - 2.0
+    for i in range(0, 100, 10):
+        assert abs(fused[i] - generic[i]) < 0.05 * max(1.0, generic[i]) + 0.05, (i, fused[i], generic[i])
 
 
 def _rms(v, w, eps):
