@@ -289,8 +289,10 @@ def _first_contact(args, device, world: int, rccl_log) -> dict:
         rows = commtune.sweep(device, sizes_mb=sizes, iters=args.comm_probe_iters or 3, channels=channels)
         out["sweep"] = rows
         grad_bytes, bwd_ms = _grad_plan_inputs(args)
+        if device.type != "cuda":
+            bwd_ms = None  # the 1 PF/s planning rate means nothing for the CPU plumbing config
         pl = commtune.plan(rows, grad_bytes, bwd_ms)
-        pl["grad_bytes"], pl["backward_ms_estimate"] = grad_bytes, round(bwd_ms, 4)
+        pl["grad_bytes"], pl["backward_ms_estimate"] = grad_bytes, None if bwd_ms is None else round(bwd_ms, 4)
         # the gloo plumbing config keeps the reference DDP's 25 MB buckets and fp32 wire: the sweep's
         # sizes do not model its TCP transfers
         applied = {"PENROZ_COMM": pl["transport"]}

@@ -20,6 +20,11 @@
 //               forward-shaped, a wave keeps 32 query rows' Q, dO and dQᵀ in registers.
 // At D = 256 the register-resident operands exceed 256 VGPRs: those kernels run one wave per
 // SIMD with the accumulators in the AGPR half of the unified 512-entry register file.
+// D = 512 (Gemma-4 full-attention layers, global_head_dim): the forward keeps Q in registers
+// (128 VGPRs) beside the Oᵀ accumulators (256, the AGPR half); the backward splits D across
+// workgroups — the dK / dV kernel into four column quarters (K / V fragments 256 VGPRs,
+// dKᵀ / dVᵀ quarters 128), the dQ kernel into two halves (Q, dO 256 VGPRs, dQᵀ half 128) — each
+// part recomputing S and dP over the full D.
 #include "attn_common.h"
 #include <type_traits>
 #include <torch/extension.h>
@@ -62,6 +67,12 @@ __device__ __forceinline__ void dma_rows(const bf16* base, size_t RS, int r0, in
 // D = 256 runs 4 waves per workgroup (128 query rows): its LDS (K/V double buffer + the Q image,
 // 128 KB) admits one workgroup per CU, and 4 waves then occupy all four SIMDs.
 template <int D> constexpr int fwd_waves() { return D >= 256 ? 4 : 2; }
+// column parts of the backward kernels (grid z): dK / dV and dQ accumulators per part
+template <int D> constexpr int kv_parts() { return D >= 512 ? 4 : (D >= 256 ? 2 : 1); }
+template <int D> constexpr int dq_parts() { return D >= 512 ? 2 : 1; }
+// forward: Oᵀ column halves per workgroup at D = 512 (grid z; S recomputed by both halves) —
+// Q (128 VGPRs) beside a full Oᵀ (256 accumulators) spilled 2 KB per lane
+template <int D> constexpr int fwd_parts() { return D >= 512 ? 2 : 1; }
 
 template <int D, bool DROPOUT>
 __global__ void __launch_bounds__(64 * fwd_waves<D>(), (D >= 256 ? 1 : 2))
@@ -70,8 +81,12 @@ __global__ void __launch_bounds__(64 * fwd_waves<D>(), (D >= 256 ? 1 : 2))
   constexpr int NP = D / 64, NS = D / 16, ND = D / 32, NW = fwd_waves<D>();
   constexpr int BM = 32 * NW, BN = 32, TILE = BN * 128 * NP;
   // D = 256: the 32 Q fragments would not fit beside Oᵀ (128 accumulators) in registers; the
-  // workgroup's query rows sit in LDS instead (read as B-operand row fragments per tile)
-  constexpr bool QLDS = D >= 256;
+  // workgroup's query rows sit in LDS instead (read as B-operand row fragments per tile).
+  // D = 512: the K / V double buffer alone is 128 KB, so Q (128 VGPRs) stays in registers and
+  // each workgroup accumulates one half of Oᵀ (fwd_parts)
+  constexpr bool QLDS = D == 256;
+  constexpr int NDO = ND / fwd_parts<D>();
+  const int do0 = fwd_parts<D>() > 1 ? (int)blockIdx.z * NDO : 0;
   constexpr int QTILE = QLDS ? BM * 128 * NP : 16;
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE + QTILE];
   const int nqb = (T + BM - 1) / BM;
@@ -110,9 +125,9 @@ __global__ void __launch_bounds__(64 * fwd_waves<D>(), (D >= 256 ? 1 : 2))
 
   const int kend = min(T, qb * BM + BM);
   const int ntiles = (kend + BN - 1) / BN;
-  f32x16 o[ND];
+  f32x16 o[NDO];
 #pragma unroll
-  for (int dh = 0; dh < ND; ++dh)
+  for (int dh = 0; dh < NDO; ++dh)
 #pragma unroll
     for (int i = 0; i < 16; ++i) o[dh][i] = 0.f;
   float m = -1e30f, l = 0.f;
@@ -160,7 +175,7 @@ __global__ void __launch_bounds__(64 * fwd_waves<D>(), (D >= 256 ? 1 : 2))
           m = mnew;
           l *= alpha;
 #pragma unroll
-          for (int dh = 0; dh < ND; ++dh)
+          for (int dh = 0; dh < NDO; ++dh)
 #pragma unroll
             for (int i = 0; i < 16; ++i) o[dh][i] *= alpha;
         }
@@ -186,9 +201,10 @@ __global__ void __launch_bounds__(64 * fwd_waves<D>(), (D >= 256 ? 1 : 2))
       for (int ss = 0; ss < 2; ++ss) {
         const uint4 pf = acc_frag(st, ss);
 #pragma unroll
-        for (int dh = 0; dh < ND; ++dh) {
-          o[dh] = mfma32(tr_frag(panel(Vt, BN, dh >> 1), 16 * ss, 32 * (dh & 1), lane), pf, o[dh]);
-          if (dh & 1) d_fence<D>();
+        for (int j = 0; j < NDO; ++j) {
+          const int dh = do0 + j;
+          o[j] = mfma32(tr_frag(panel(Vt, BN, dh >> 1), 16 * ss, 32 * (dh & 1), lane), pf, o[j]);
+          if (j & 1) d_fence<D>();
         }
       }
     }
@@ -200,12 +216,12 @@ __global__ void __launch_bounds__(64 * fwd_waves<D>(), (D >= 256 ? 1 : 2))
   if (qrow < T) {
     bf16* orow = out + ((size_t)b * T + qrow) * H * D + (size_t)h * D;
 #pragma unroll
-    for (int dh = 0; dh < ND; ++dh)
+    for (int j = 0; j < NDO; ++j)
 #pragma unroll
       for (int g = 0; g < 4; ++g)
-        store4(orow + 32 * dh + 8 * g + 4 * hh, o[dh][4 * g] * inv, o[dh][4 * g + 1] * inv, o[dh][4 * g + 2] * inv,
-               o[dh][4 * g + 3] * inv);
-    if (hh == 0) lse[((size_t)b * H + h) * T + qrow] = (m + log2f(l)) * kLn2;
+        store4(orow + 32 * (do0 + j) + 8 * g + 4 * hh, o[j][4 * g] * inv, o[j][4 * g + 1] * inv,
+               o[j][4 * g + 2] * inv, o[j][4 * g + 3] * inv);
+    if (hh == 0 && do0 == 0) lse[((size_t)b * H + h) * T + qrow] = (m + log2f(l)) * kLn2;
   }
 }
 
@@ -257,9 +273,8 @@ __global__ void __launch_bounds__(128, 1)
   // stay in registers: no per-slice K / V LDS reads, and 65 KB of LDS per workgroup lets two
   // workgroups (all four SIMDs) share a CU. (Keeping K / V in LDS for one workgroup per CU left
   // two SIMDs idle, spilled 72 registers and was LDS-bandwidth-bound at 87 TF.)
-  constexpr bool DSPLIT = D >= 256;
-  constexpr int NDH = DSPLIT ? ND / 2 : ND;  // dKᵀ / dVᵀ column blocks of 32 owned here
-  const int dh0 = DSPLIT ? (int)blockIdx.z * NDH : 0;
+  constexpr int NDH = ND / kv_parts<D>();  // dKᵀ / dVᵀ column blocks of 32 owned here (D = 512: a quarter)
+  const int dh0 = kv_parts<D>() > 1 ? (int)blockIdx.z * NDH : 0;
   constexpr bool KVLDS = false;
   constexpr int KVT = BK * 128 * NP;           // 64 key rows
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + (KVLDS ? 2 * KVT : 16)];
@@ -478,6 +493,8 @@ __global__ void __launch_bounds__(128, (D >= 256 ? 1 : 2))
   const float c = scale * kLog2e;
   const float inv_keep = DROPOUT ? 1.f / (1.f - p_drop) : 1.f;
 
+  constexpr int NDQ = ND / dq_parts<D>();  // dQᵀ column blocks of 32 owned here (D = 512: a half)
+  const int dq0 = dq_parts<D>() > 1 ? (int)blockIdx.z * NDQ : 0;
   uint4 qf[NS], dof[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
@@ -501,9 +518,9 @@ __global__ void __launch_bounds__(128, (D >= 256 ? 1 : 2))
 
   const int kend = min(T, qb * BM + BM);
   const int ntiles = (kend + BN - 1) / BN;
-  f32x16 dq[ND];
+  f32x16 dq[NDQ];
 #pragma unroll
-  for (int dh = 0; dh < ND; ++dh)
+  for (int dh = 0; dh < NDQ; ++dh)
 #pragma unroll
     for (int i = 0; i < 16; ++i) dq[dh][i] = 0.f;
 
@@ -555,9 +572,10 @@ __global__ void __launch_bounds__(128, (D >= 256 ? 1 : 2))
       for (int ss = 0; ss < 2; ++ss) {
         const uint4 sf = acc_frag(st, ss);
 #pragma unroll
-        for (int dh = 0; dh < ND; ++dh) {
-          dq[dh] = mfma32(tr_frag(panel(Kt, BN, dh >> 1), 16 * ss, 32 * (dh & 1), lane), sf, dq[dh]);
-          if (dh & 1) d_fence<D>();
+        for (int j = 0; j < NDQ; ++j) {
+          const int dh = dq0 + j;
+          dq[j] = mfma32(tr_frag(panel(Kt, BN, dh >> 1), 16 * ss, 32 * (dh & 1), lane), sf, dq[j]);
+          if (j & 1) d_fence<D>();
         }
       }
     }
@@ -567,11 +585,11 @@ __global__ void __launch_bounds__(128, (D >= 256 ? 1 : 2))
   if (qok) {
     bf16* dqrow = dqkv + ((size_t)b * T + qrow) * RS + (size_t)h * D;
 #pragma unroll
-    for (int dh = 0; dh < ND; ++dh)
+    for (int j = 0; j < NDQ; ++j)
 #pragma unroll
       for (int g = 0; g < 4; ++g)
-        store4(dqrow + 32 * dh + 8 * g + 4 * hh, dq[dh][4 * g] * scale, dq[dh][4 * g + 1] * scale,
-               dq[dh][4 * g + 2] * scale, dq[dh][4 * g + 3] * scale);
+        store4(dqrow + 32 * (dq0 + j) + 8 * g + 4 * hh, dq[j][4 * g] * scale, dq[j][4 * g + 1] * scale,
+               dq[j][4 * g + 2] * scale, dq[j][4 * g + 3] * scale);
   }
 }
 
@@ -585,7 +603,9 @@ using namespace penroz;
   else if ((D) == 128) { constexpr int DD = 128; constexpr bool DR = false; __VA_ARGS__; }       \
   else if ((D) == 256 && (DROP)) { constexpr int DD = 256; constexpr bool DR = true; __VA_ARGS__; } \
   else if ((D) == 256) { constexpr int DD = 256; constexpr bool DR = false; __VA_ARGS__; }       \
-  else TORCH_CHECK(false, "generic flash attention supports head_dim 128 and 256, got ", (D));
+  else if ((D) == 512 && (DROP)) { constexpr int DD = 512; constexpr bool DR = true; __VA_ARGS__; } \
+  else if ((D) == 512) { constexpr int DD = 512; constexpr bool DR = false; __VA_ARGS__; }       \
+  else TORCH_CHECK(false, "generic flash attention supports head_dim 128, 256 and 512, got ", (D));
 
 void flash_attn_gen_fwd(torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int64_t H, int64_t Hkv, int64_t D,
                         double scale, double p_drop, int64_t seed) {
@@ -601,7 +621,7 @@ void flash_attn_gen_fwd(torch::Tensor qkv, torch::Tensor out, torch::Tensor lse,
   bf16* o = reinterpret_cast<bf16*>(out.data_ptr());
   FA_GEN_DISPATCH(D, p_drop > 0.0, {
     constexpr int NW = fwd_waves<DD>();
-    dim3 g((T + 32 * NW - 1) / (32 * NW), B * H);
+    dim3 g((T + 32 * NW - 1) / (32 * NW), B * H, fwd_parts<DD>());
     hipLaunchKernelGGL((fa_gen_fwd_kernel<DD, DR>), g, dim3(64 * NW), 0, stream, q, o, lse.data_ptr<float>(), T,
                        (int)H, (int)Hkv, (float)scale, (float)p_drop, (uint64_t)seed);
   })
@@ -629,7 +649,8 @@ void flash_attn_gen_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out
   const bool split = G > 1 && (int64_t)B * Hkv * nkb < 1024;
   torch::Tensor part;
   if (split) part = torch::empty({(int64_t)G * B * T, 2 * Hkv * D}, qkv.options().dtype(torch::kFloat32));
-  dim3 gkv(nkb, B * Hkv * (split ? G : 1), D >= 256 ? 2 : 1), gq((T + 63) / 64, B * H);  // z: the D halves
+  // z: the column parts of D (dK / dV: 2 at D = 256, 4 at 512; dQ: 2 at 512)
+  dim3 gkv(nkb, B * Hkv * (split ? G : 1), D >= 512 ? 4 : (D >= 256 ? 2 : 1)), gq((T + 63) / 64, B * H, D >= 512 ? 2 : 1);
   FA_GEN_DISPATCH(D, p_drop > 0.0, {
     hipLaunchKernelGGL((fa_gen_bwd_pre_kernel<DD>), dim3(((int64_t)rows * (DD / 8) + 255) / 256), dim3(256), 0,
                        stream, d, reinterpret_cast<const bf16*>(out.data_ptr()), delta.data_ptr<float>(), B, T,

@@ -1,8 +1,8 @@
 """Causal self-attention over a fused QKV tensor, and KV-cache (decode) attention.
 
 GPU: hand-written CDNA4 flash attention — ``csrc/kernels/flash_attn.hip`` (head_dim 64, GPT-2)
-and ``csrc/kernels/flash_attn_gen.hip`` (head_dim 128 / 256, Gemma; the same algebra over
-64-column LDS panels):
+and ``csrc/kernels/flash_attn_gen.hip`` (head_dim 128 / 256 / 512, Gemma; the same algebra over
+64-column LDS panels, D = 512 split over column parts):
   * forward reads Q/K/V straight out of the fused ``[B, T, (H + 2·Hkv)·D]`` projection (no
     split/transpose copies), keeps Q in registers, stages K/V tiles through XOR-swizzled LDS,
     computes Sᵀ = K·Qᵀ with ``v_mfma_f32_32x32x16_bf16`` so each lane owns one query row's
@@ -30,13 +30,12 @@ import torch.nn.functional as F
 from penroz.ops._ext import use_kernels, kernels
 
 # head dims with a native kernel: prefill / training flash attention (flash_attn.hip: 64;
-# flash_attn_gen.hip: 128, 256) and decode attention (csrc/kernels/decode_attn.hip: also 32 and
-# Gemma-4's global_head_dim 512). Prefill / training at any other head dim <= 256 runs the next
-# wider kernel on zero-padded heads (see _padded_dim); wider heads (512: Gemma-4 full-attention
-# layers) run torch SDPA for prefill / training — their O accumulator alone (32 query rows × 512
-# fp32 per wave) would fill a wave's whole 512-entry register file — and the native kernel for
-# decode.
-SUPPORTED_HEAD_DIMS = (64, 128, 256)
+# flash_attn_gen.hip: 128, 256 and Gemma-4's global_head_dim 512 — whose O accumulator alone (32
+# query rows × 512 fp32 per wave) would fill a wave's whole register file, so the 512 kernels split
+# D over column parts: grid z) and decode attention (csrc/kernels/decode_attn.hip: also 32).
+# Prefill / training at any other head dim <= 512 runs the next wider kernel on zero-padded heads
+# (see _padded_dim); only heads wider than 512 fall back to torch SDPA.
+SUPPORTED_HEAD_DIMS = (64, 128, 256, 512)
 DECODE_HEAD_DIMS = (32, 64, 128, 256, 512)
 
 

@@ -81,14 +81,14 @@ def test_one_step_matches_fp32_reference(model_type):
 # attention, the full layers with global_head_dim and their own KV-head count, the last two layers
 # KV-shared with double-wide MLPs
 GEMMA4 = dict(layer_types=["sliding_attention", "full_attention", "sliding_attention", "full_attention"],
-              global_head_dim=128, num_global_key_value_heads=1, num_kv_shared_layers=2, use_double_wide_mlp=True)
+              global_head_dim=512, num_global_key_value_heads=1, num_kv_shared_layers=2, use_double_wide_mlp=True)
 
 
 def test_match_heterogeneous_gemma4_layer_list():
     spec = GemmaExecutor.match(_gemma("gemma4", L=4, F=256, **GEMMA4))
     assert spec is not None and not spec.uniform and spec.mode == 0
-    assert [(b.H, b.Hkv, b.D, b.F) for b in spec.blocks] == [(4, 2, 64, 256), (4, 1, 128, 256), (4, 2, 64, 512),
-                                                            (4, 1, 128, 512)]
+    assert [(b.H, b.Hkv, b.D, b.F) for b in spec.blocks] == [(4, 2, 64, 256), (4, 1, 512, 256), (4, 2, 64, 512),
+                                                            (4, 1, 512, 512)]
 
 
 def test_heterogeneous_gemma4_one_step_matches_fp32_reference():
@@ -112,6 +112,25 @@ def test_heterogeneous_gemma4_one_step_matches_fp32_reference():
     for (n, p), (_, r) in zip(m.named_parameters(), ref.named_parameters()):
         rel = ((ex.grad(p) - r.grad).norm() / (r.grad.norm() + 1e-12)).item()
         assert rel < 5e-2, f"gemma4 {n}: rel grad err {rel}"
+
+
+def test_no_sdpa_for_gemma4_head_dims(monkeypatch):
+    """Every head dim of the Gemma-4 layer list (64 sliding, 512 full) runs a native flash kernel:
+    torch SDPA is never called in the fused step (nor in the generic engine's forward/backward)."""
+    import torch.nn.functional as Fn
+    calls = []
+    real = Fn.scaled_dot_product_attention
+    monkeypatch.setattr(Fn, "scaled_dot_product_attention", lambda *a, **k: calls.append(1) or real(*a, **k))
+    m = _gemma("gemma4", L=4, F=256, **GEMMA4).to(DEV)
+    x = torch.randint(0, 512, (2, 64), device=DEV)
+    ex = GemmaExecutor(m, torch.device(DEV))
+    ex.setup_training(False)
+    ex.zero_grad()
+    ex.train_micro_step(x, torch.roll(x, -1, 1), 1.0)
+    _, c = m(x, torch.roll(x, -1, 1), skip_softmax=True)
+    c.backward()
+    torch.cuda.synchronize()
+    assert not calls
 
 
 def test_heterogeneous_gemma4_loss_curve_matches_generic_engine():

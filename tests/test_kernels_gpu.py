@@ -375,8 +375,9 @@ def _dropout_masked_reference():
     assert rel < 0.02, rel
 
 
-# ---- head_dim 128 / 256 (csrc/kernels/flash_attn_gen.hip): Gemma-3 1B is H=4, Hkv=1, D=256
-@pytest.mark.parametrize("D", [128, 256])
+# ---- head_dim 128 / 256 / 512 (csrc/kernels/flash_attn_gen.hip): Gemma-3 1B is H=4, Hkv=1, D=256;
+# 512 is Gemma-4's global_head_dim (full-attention layers)
+@pytest.mark.parametrize("D", [128, 256, 512])
 @pytest.mark.parametrize("B,T,H,Hkv", [(2, 512, 4, 1), (1, 200, 3, 3), (2, 130, 4, 2), (1, 5, 2, 2), (1, 1024, 4, 1),
                                        (1, 96, 8, 2)])
 def test_flash_gen_fwd_bwd(D, B, T, H, Hkv):
@@ -399,7 +400,7 @@ def test_flash_gen_fwd_bwd(D, B, T, H, Hkv):
         assert rel < 0.02, f"D={D} {name} relative error {rel}"
 
 
-@pytest.mark.parametrize("D", [32, 80, 96, 160])
+@pytest.mark.parametrize("D", [32, 80, 96, 160, 384])
 @pytest.mark.parametrize("B,T,H,Hkv,p", [(2, 130, 4, 2, 0.0), (1, 300, 3, 3, 0.0), (2, 64, 4, 1, 0.1)])
 def test_flash_padded_head_dims(D, B, T, H, Hkv, p):
     """Head dims without their own kernel run the next wider one on zero-padded heads: forward
@@ -424,7 +425,7 @@ def test_flash_padded_head_dims(D, B, T, H, Hkv, p):
         assert torch.isfinite(qkv.grad.float()).all() and qkv.grad.abs().sum() > 0
 
 
-@pytest.mark.parametrize("D", [128, 256])
+@pytest.mark.parametrize("D", [128, 256, 512])
 def test_flash_gen_rescale_branch(D):
     """One key spiking far above the rest at a late tile forces the online-softmax rescale."""
     torch.manual_seed(1)
@@ -438,7 +439,7 @@ def test_flash_gen_rescale_branch(D):
     _close(lse, rl, 5e-3, 1e-4, "lse")
 
 
-@pytest.mark.parametrize("D", [128, 256])
+@pytest.mark.parametrize("D", [128, 256, 512])
 def test_flash_gen_dropout_matches_masked_reference(D):
     """One-hot V rows (V[k] = e_k, T <= D) make the forward output reveal each head's dropout mask;
     the backward must reproduce the fp32 gradients of softmax -> mask/(1-p) -> @V with it."""

@@ -110,7 +110,7 @@ def test_bench_self_launches_ranks_cpu_gloo():
     assert all(r["ok"] and r["busbw_GBps"] > 0 and r["transport"] == "c10d" for r in sweep)
     pl = d["comm"]["plan"]
     assert pl["transport"] == "c10d" and pl["wire"] == "fp32" and pl["channels"] is None
-    assert pl["grad_bytes"] > 0 and pl["backward_ms_estimate"] > 0 and "predicted_fp32_ms" in pl
+    assert pl["grad_bytes"] > 0 and pl["backward_ms_estimate"] is None and "predicted_fp32_ms" in pl
     assert set(d["comm"]["rccl"]) == {"coll_channels", "log"}
 
 
