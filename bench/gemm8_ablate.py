@@ -1,8 +1,9 @@
 """gemm8 timing ablations (results wrong in ablated modes), interleaved rounds, median µs / TF, GPT-2 shapes.
 
-ablate bits: 1 = epilogue without global stores; (ablate >> 4) & 3 = store cache policy (0 plain, 1 sc0,
-2 nt, 3 sc0|nt); ablate >> 8 = odd workgroups start that many `s_sleep 127` late (de-synchronised
-epilogues).
+ablate bits: 1 = epilogue without global stores; 4 = one workgroup per tile instead of one persistent
+workgroup per CU (the dispatcher refills CUs as tiles finish); 8 = GELU epilogue with the branch-free
+A&S erf; (ablate >> 4) & 3 = store cache policy (0 plain, 1 sc0, 2 nt, 3 sc0|nt); ablate >> 8 = odd
+workgroups start that many `s_sleep 127` late (de-synchronised epilogues).
 
     python bench/gemm8_ablate.py [--arms 0,1,32,256,768]
 """
@@ -32,7 +33,7 @@ def timed(fn, iters=20):
 
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--arms", default="0,1,32,512,768,1024,800")
+ap.add_argument("--arms", default="0,1,4,8,12,32,512,768,1024")
 ap.add_argument("--rounds", type=int, default=5)
 args = ap.parse_args()
 arms = [int(a) for a in args.arms.split(",")]
