@@ -9,6 +9,8 @@ tail -5 gpurun_out/pytest_gemm_epi.log; ok_or_stop $rc
 if [ $rc -eq 0 ]; then
   timeout -k 10 300 python bench/gemm_epi_bench.py > gpurun_out/gemm_epi_bench.log 2>&1; rc=$?
   tail -8 gpurun_out/gemm_epi_bench.log; ok_or_stop $rc
+  bash bench/gpu.sh ab PENROZ_EPI_GEMM=0 PENROZ_EPI_GEMM=1 > gpurun_out/ab_epi_gemm.log 2>&1; rc=$?
+  cat gpurun_out/ab_epi_gemm.log; ok_or_stop $rc
 fi
 timeout -k 10 700 python -u -m pytest tests/test_gemma_executor_gpu.py tests/test_kernels_gpu.py \
   -k "gen or padded or gemma or match or combine" -v --timeout 300 --timeout-method thread \

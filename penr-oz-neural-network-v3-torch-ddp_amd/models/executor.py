@@ -8,7 +8,8 @@ per-module autograd it runs an explicit forward and backward:
 forward, per layer (N = B·T tokens, fp32 residual stream — the reference's autocast numerics)
   LN1 (HIP, → bf16) → QKV GEMM+bias (hipBLASLt) → flash attention (HIP, reads the fused QKV
   tensor, writes head-merged O + LSE) → proj GEMM+bias → residual-add+LN2 (one HIP pass)
-  → fc GEMM+bias → GELU (HIP) → fc2 GEMM+bias → (residual-add fused into the next LN)
+  → fc GEMM+bias+GELU (HIP deferred-epilogue GEMM writing pre-activation and activation) → fc2
+  GEMM+bias → (residual-add fused into the next LN)
 head: final LN → lm_head GEMM → cross-entropy (HIP: one LDS-resident pass per row, writes
   the logits gradient in place, no fp32 logits). The head can run in token chunks
   (``_head_chunk_rows``: automatic above 8 GiB of logits, or ``PENROZ_HEAD_CHUNK`` rows):
@@ -420,8 +421,9 @@ class GPTExecutor:
             dp, ds = self._drop(training, dropout_seed, l, 0)
             norm_ops.add_ln_fwd(self.resid[l], self.tmp_c, self.resid_mid[l], f(b.ln2.weight), f(b.ln2.bias),
                                 b.ln2.eps, y=self.ln2[l], mean=mean2, rstd=rstd2, dropout_p=dp, dropout_seed=ds)
-            self._linear(self.ln2[l], b.fc, out=self.fcpre[l])
-            act_ops.gelu_fwd(self.fcpre[l], s.gelu_approx, out=self.fcact[l])
+            # fc + GELU: one kernel writing pre-activation and activation (ops/gemm.py linear_gelu)
+            gemm_ops.linear_gelu(self.ln2[l], self.bf16(b.fc.weight), self.bf16(b.fc.bias), self.fcpre[l],
+                                 self.fcact[l], s.gelu_approx)
             self._linear(self.fcact[l], b.fc2, out=self.tmp_c)
         Lc = self.L
         meanf, rstdf = self.statsf

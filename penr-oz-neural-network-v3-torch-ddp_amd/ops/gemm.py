@@ -80,44 +80,36 @@ def load_tuned_gemms() -> bool:
     return ok
 
 
-# ---- forward / dgrad GEMMs (csrc/kernels/gemm8.hip) -----------------------------------------
-# EXPERIMENTAL native path: persistent 256×256-tile MFMA kernel on the 8-phase ping-pong schedule
-# (one LDS-DMA unit per phase behind one counted wait, buffer-resource DMA with range-checked edges,
-# bias / bias+GELU epilogues). Measured at 0.79-1.00× hipBLASLt per GPT-2 shape, 0.87× summed over a
-# layer (profiles/gemm8_r3.md: the K = 768 tiles lose ~25 % to the lock-step epilogue store burst),
-# so the forward / dgrad GEMMs stay on hipBLASLt; PENROZ_NATIVE_GEMM=1 routes linear_fwd /
-# linear_dgrad through it.
-NATIVE_GEMM = os.environ.get("PENROZ_NATIVE_GEMM", "0")
+# ---- fused linear + GELU (csrc/kernels/gemm_epi.hip) -----------------------------------------
+# The fc linear of a GPT-2 MLP and its GELU in ONE kernel: the deferred-epilogue GEMM writes the
+# pre-activation (the backward's GELU' input) and the activation (fc2's input) while its next tile
+# computes, instead of hipBLASLt's GEMM followed by the memory-bound GELU kernel (a full extra read
+# and write of the [N, 4C] activation). PENROZ_EPI_GEMM=0 restores GEMM + GELU kernel (same-box A/B).
+EPI_GEMM = os.environ.get("PENROZ_EPI_GEMM", "1") != "0"
 
 
-def _gemm_ok(a: Tensor, b: Tensor) -> bool:
-    return (NATIVE_GEMM == "1" and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16
-            and a.shape[1] % 128 == 0 and b.shape[0] % 8 == 0 and a.stride(1) == 1 and b.stride(1) == 1
-            and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0)
+def epi_gemm_ok(x: Tensor, w: Tensor) -> bool:
+    """The fused kernel's shape / layout contract (K % 128 == 0, K >= 640, N % 8 == 0, bf16,
+    unit column stride, 16-B aligned rows)."""
+    return (EPI_GEMM and use_kernels(x) and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and x.dim() == 2 and w.dim() == 2 and x.stride(1) == 1 and w.stride(1) == 1
+            and x.stride(0) % 8 == 0 and w.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
+            and kernels().gemm_epi_supported(x.shape[0], w.shape[0], x.shape[1]))
 
 
-def linear_fwd(x: Tensor, w: Tensor, bias: Tensor | None, out: Tensor, act: Tensor | None = None,
-               gelu_approx: str = "none") -> Tensor:
-    """out = x·wᵀ (+ bias); with ``act``: out = pre-activation, act = GELU(out) (one pass)."""
-    if use_kernels(x) and _gemm_ok(x, w):
-        kernels().gemm8_bf16(x, w, bias, out, act, 1 if gelu_approx == "tanh" else 0)
-        return out
-    if bias is not None:
-        torch.addmm(bias, x, w.t(), out=out)
+def linear_gelu(x: Tensor, w: Tensor, bias: Tensor, pre: Tensor, act: Tensor, approximate: str = "none"):
+    """pre = x·wᵀ + bias, act = GELU(pre) (bf16; ``approximate`` "none" = erf, "tanh" = gelu_new),
+    in one kernel when ``epi_gemm_ok``; otherwise the library GEMM and the GELU kernel."""
+    if epi_gemm_ok(x, w) and pre.stride(1) == 1 and pre.stride(0) % 8 == 0 and act.stride() == pre.stride():
+        kernels().gemm_epi_bf16(x, w, bias, pre, act, 1 if approximate == "tanh" else 0)
+        return pre, act
+    torch.addmm(bias, x, w.t(), out=pre)
+    if use_kernels(pre):
+        from penroz.ops import activations as act_ops
+        act_ops.gelu_fwd(pre, approximate, out=act)
     else:
-        torch.mm(x, w.t(), out=out)
-    if act is not None:
-        act.copy_(torch.nn.functional.gelu(out.float(), approximate=gelu_approx))
-    return out
-
-
-def linear_dgrad(dy: Tensor, wt: Tensor, out: Tensor) -> Tensor:
-    """out = dy·w, the input gradient of y = x·wᵀ, from the transposed weight ``wt`` = wᵀ [in, out]
-    (the executor's copy: both operands reduction-contiguous)."""
-    if use_kernels(dy) and _gemm_ok(dy, wt):
-        kernels().gemm8_bf16(dy, wt, None, out)
-        return out
-    return torch.mm(dy, wt.t(), out=out)
+        act.copy_(torch.nn.functional.gelu(pre.float(), approximate=approximate))
+    return pre, act
 
 
 # ---- decode-shaped GEMMs (csrc/kernels/skinny_gemm.hip) --------------------------------------
