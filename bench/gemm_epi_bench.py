@@ -35,12 +35,12 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--M", type=int, default=65536)
-ap.add_argument("--shapes", default="fc_gelu,qkv,proj,fc2,fc2_dgrad,fc_dgrad,lm_head")
+ap.add_argument("--shapes", default="fc_gelu,fc2_dgrad_dgelu,qkv,proj,fc2,fc2_dgrad,fc_dgrad,lm_head")
 args = ap.parse_args()
 k = _ext.kernels()
 G.load_tuned_gemms()
 M = args.M
-SHAPES = {"fc_gelu": (768, 3072, True, True), "qkv": (768, 2304, True, False), "proj": (768, 768, True, False),
+SHAPES = {"fc_gelu": (768, 3072, True, True), "fc2_dgrad_dgelu": (768, 3072, False, "dgelu"), "qkv": (768, 2304, True, False), "proj": (768, 768, True, False),
           "fc2": (3072, 768, True, False), "fc2_dgrad": (768, 3072, False, False),
           "fc_dgrad": (3072, 768, False, False), "lm_head": (768, 50304, False, False)}
 for name in args.shapes.split(","):
@@ -51,6 +51,22 @@ for name in args.shapes.split(","):
     bias = (torch.rand(N, device="cuda") - 0.5).to(torch.bfloat16) if has_bias else None
     out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
     act = torch.empty_like(out) if gelu else None
+    if gelu == "dgelu":  # fc2 dgrad through GELU': library GEMM + the GELU-backward / bias-column kernel
+        pre = (torch.randn(M, N, device="cuda") * 2).to(torch.bfloat16)
+        dbias = torch.zeros(N, device="cuda")
+        arms = {"epi": lambda: k.gemm_epi_dgelu(a, b, pre, out, dbias, 0),
+                "epi_nostore": lambda: k.gemm_epi_dgelu(a, b, pre, out, dbias, 0, 1),
+                "blas": lambda: (torch.mm(a, b.t(), out=out), Ac.gelu_bwd(out, pre, "none", dbias, out=out))}
+        res = {n: [] for n in arms}
+        for _ in range(args.rounds):
+            for n, f in arms.items():
+                res[n].append(timed(f, args.iters))
+        fl = 2 * M * K * N
+        med = {n: statistics.median(v) for n, v in res.items()}
+        print(json.dumps({"shape": name, "M": M, "K": K, "N": N,
+                          **{n: {"us": round(t, 1), "TF": round(fl / t / 1e6, 1)} for n, t in med.items()},
+                          "epi_vs_blas": round(med["blas"] / med["epi"], 3)}), flush=True)
+        continue
     arms = {"epi": lambda: k.gemm_epi_bf16(a, b, bias, out, act, 0),
             "epi_nostore": lambda: k.gemm_epi_bf16(a, b, bias, out, act, 0, 1),
             "gemm8": lambda: k.gemm8_bf16(a, b, bias, out, act, 0, 32)}

@@ -76,6 +76,8 @@ torch::Tensor gemm8_dma_probe(torch::Tensor src, int64_t bytes, int64_t lds_off,
 bool gemm_epi_supported(int64_t M, int64_t N, int64_t K);
 void gemm_epi_bf16(torch::Tensor a, torch::Tensor b, c10::optional<torch::Tensor> bias, torch::Tensor out,
                    c10::optional<torch::Tensor> act, int64_t gelu_approx, int64_t flags);
+void gemm_epi_dgelu(torch::Tensor dy, torch::Tensor wt, torch::Tensor pre, torch::Tensor out,
+                    c10::optional<torch::Tensor> dbias, int64_t gelu_approx, int64_t flags);
 // skinny_gemm.hip
 int64_t skinny_gemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> bias, torch::Tensor out,
                     torch::Tensor ws, torch::Tensor cnt, int64_t splitk);
@@ -173,6 +175,10 @@ PYBIND11_MODULE(penroz_kernels, m) {
         pybind11::arg("out"), pybind11::arg("act") = pybind11::none(), pybind11::arg("gelu_approx") = 0,
         pybind11::arg("flags") = 0,
         "out = a·bᵀ (+bias) (act = GELU(out)); 4-wave 256x256 MFMA GEMM whose epilogue streams inside the next tile");
+  m.def("gemm_epi_dgelu", &gemm_epi_dgelu, pybind11::arg("dy"), pybind11::arg("wt"), pybind11::arg("pre"),
+        pybind11::arg("out"), pybind11::arg("dbias") = pybind11::none(), pybind11::arg("gelu_approx") = 0,
+        pybind11::arg("flags") = 0,
+        "out = bf16(dy·wtᵀ)·GELU'(pre), dbias += column sums of out (deferred-epilogue GEMM)");
   m.def("skinny_gemm", &skinny_gemm, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("bias"),
         pybind11::arg("out"), pybind11::arg("ws"), pybind11::arg("cnt"), pybind11::arg("splitk") = 0,
         "decode-shaped out[M<=64, N] = x·wᵀ (+bias), bf16; returns the split-K factor used");

@@ -719,9 +719,10 @@ class GPTExecutor:
             d_f, dqkv = self._reuse(self.d_f2[l & 1]), self._reuse(self.dqkv2[l & 1])
             dres_bf = self.dresid_bf2[rb]
             # ---- MLP branch
-            torch.mm(dres_bf, self._dgrad_w(b.fc2.weight), out=d_f)
+            # fc2 data gradient, GELU backward and the fc bias gradient in one kernel (ops/gemm.py)
+            gemm_ops.dgrad_gelu(dres_bf, self._dgrad_w(b.fc2.weight).t(), self.fcpre[l], d_f, self.grad(b.fc.bias),
+                                s.gelu_approx)
             self._wgrad(dres_bf, self.fcact[l], b.fc2.weight)
-            act_ops.gelu_bwd(d_f, self.fcpre[l], s.gelu_approx, self.grad(b.fc.bias), out=d_f)
             torch.mm(d_f, self._dgrad_w(b.fc.weight), out=self.d_c)
             self._wgrad(d_f, self.ln2[l], b.fc.weight)
             _, _, mean, rstd = self.stats[l]

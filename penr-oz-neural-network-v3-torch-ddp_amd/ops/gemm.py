@@ -84,7 +84,8 @@ def load_tuned_gemms() -> bool:
 # The fc linear of a GPT-2 MLP and its GELU in ONE kernel: the deferred-epilogue GEMM writes the
 # pre-activation (the backward's GELU' input) and the activation (fc2's input) while its next tile
 # computes, instead of hipBLASLt's GEMM followed by the memory-bound GELU kernel (a full extra read
-# and write of the [N, 4C] activation). PENROZ_EPI_GEMM=0 restores GEMM + GELU kernel (same-box A/B).
+# and write of the [N, 4C] activation); in the backward, fc2's data gradient, the GELU backward and
+# the fc bias gradient likewise (dgrad_gelu). PENROZ_EPI_GEMM=0 restores GEMM + GELU kernels (A/B).
 EPI_GEMM = os.environ.get("PENROZ_EPI_GEMM", "1") != "0"
 
 
@@ -110,6 +111,21 @@ def linear_gelu(x: Tensor, w: Tensor, bias: Tensor, pre: Tensor, act: Tensor, ap
     else:
         act.copy_(torch.nn.functional.gelu(pre.float(), approximate=approximate))
     return pre, act
+
+
+def dgrad_gelu(dy: Tensor, wt: Tensor, pre: Tensor, out: Tensor, dbias: Tensor | None, approximate: str = "none"):
+    """Data gradient into a GELU's input: out = bf16(dy·wtᵀ) · GELU'(pre) and dbias (fp32) += the
+    column sums of out, in one kernel when ``epi_gemm_ok`` (``wt`` = the transposed weight copy,
+    [in, out] row-major); otherwise the library GEMM and the GELU-backward / bias-column kernel.
+    The GPT executor's fc2 data gradient + GELU backward + fc bias gradient."""
+    if (epi_gemm_ok(dy, wt) and out.stride(1) == 1 and out.stride(0) % 8 == 0 and pre.stride() == out.stride()
+            and pre.data_ptr() != out.data_ptr()):
+        kernels().gemm_epi_dgelu(dy, wt, pre, out, dbias, 1 if approximate == "tanh" else 0)
+        return out
+    torch.mm(dy, wt.t(), out=out)
+    from penroz.ops import activations as act_ops
+    act_ops.gelu_bwd(out, pre, approximate, dbias, out=out)
+    return out
 
 
 # ---- decode-shaped GEMMs (csrc/kernels/skinny_gemm.hip) --------------------------------------

@@ -86,3 +86,27 @@ def test_gemm_epi_rejects_bad_shapes():
     with pytest.raises(RuntimeError):
         k.gemm_epi_bf16(a, torch.zeros(64, 512, device=DEV, dtype=torch.bfloat16), None,
                         torch.empty(64, 64, device=DEV, dtype=torch.bfloat16))
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 512, 768), (300, 264, 640), (4096, 3072, 768), (777, 1000, 768),
+                                   (8192, 3072, 768)])
+@pytest.mark.parametrize("approx", [0, 1])
+def test_gemm_epi_dgelu_matches_unfused(M, N, K, approx):
+    """out = bf16(dy·wtᵀ)·GELU'(pre) and dbias += column sums of out, against the unfused pair
+    (fp32 GEMM rounded to bf16, then the GELU backward in fp32, rounded to bf16)."""
+    torch.manual_seed(M + N + K + approx)
+    dy = (torch.rand(M, K, device=DEV) * 2 - 1).to(torch.bfloat16)
+    wt = ((torch.rand(N, K, device=DEV) * 2 - 1) * 0.1 + torch.arange(N, device=DEV).view(-1, 1) * 1e-3).to(torch.bfloat16)
+    pre = (torch.randn(M, N, device=DEV) * 2).to(torch.bfloat16)
+    out = torch.full((M, N), 7.0, device=DEV, dtype=torch.bfloat16)
+    dbias = torch.full((N,), 0.5, device=DEV)
+    _ext.kernels().gemm_epi_dgelu(dy, wt, pre, out, dbias, approx)
+    torch.cuda.synchronize()
+    dact = (dy.float() @ wt.float().t()).to(torch.bfloat16).float()
+    x = pre.float().requires_grad_()
+    torch.nn.functional.gelu(x, approximate="tanh" if approx else "none").backward(dact)
+    ref = x.grad
+    rel = ((out.float() - ref).norm() / ref.norm()).item()
+    assert rel < 8e-3, rel
+    want_b = 0.5 + out.float().sum(0)  # the kernel sums the values it stored
+    assert ((dbias - want_b).abs().max() / want_b.abs().max()).item() < 1e-4
