@@ -85,8 +85,10 @@ def load_tuned_gemms() -> bool:
 # pre-activation (the backward's GELU' input) and the activation (fc2's input) while its next tile
 # computes, instead of hipBLASLt's GEMM followed by the memory-bound GELU kernel (a full extra read
 # and write of the [N, 4C] activation); in the backward, fc2's data gradient, the GELU backward and
-# the fc bias gradient likewise (dgrad_gelu). PENROZ_EPI_GEMM=0 restores GEMM + GELU kernels (A/B).
-EPI_GEMM = os.environ.get("PENROZ_EPI_GEMM", "1") != "0"
+# the fc bias gradient likewise (dgrad_gelu). OFF by default: measured on the headline step
+# (profiles/gemm_epi_r4.log) the fused path is SLOWER than hipBLASLt + the standalone GELU kernels
+# (66.4 / 65.9 ms vs 64.1 / 63.8 ms), so PENROZ_EPI_GEMM=1 is an opt-in A/B arm only.
+EPI_GEMM = os.environ.get("PENROZ_EPI_GEMM", "0") == "1"
 
 
 def epi_gemm_ok(x: Tensor, w: Tensor) -> bool:
