@@ -55,7 +55,10 @@ constexpr int B_OFF = 65536;            // B k-tile buffers
 constexpr int KBUF = 32768;             // one operand's k-tile
 constexpr int BIAS_OFF = 131072;        // [tile parity][256] bf16
 constexpr int BIAS_SINK = BIAS_OFF + 1024;  // waves 2-3's bias piece (uniform VMEM counts)
-constexpr int LDS_BYTES = BIAS_SINK + 512;
+// non-DGELU: per-wave staging of 4 deferred units (32 rows x 64 columns bf16), read back as
+// full 128-B row segments for the stores
+constexpr int STAGE_OFF = BIAS_SINK + 512;
+constexpr int LDS_BYTES = STAGE_OFF + 4 * 4096;
 // EG_DGELU (no bias): the P chunks of the deferred units ride with the k-tile stream into
 // [k-tile parity][unit step][wave][64 lanes × 16 B] after the operand buffers (exactly 160 KiB)
 constexpr int P_OFF = 131072;
@@ -320,16 +323,16 @@ __global__ void __launch_bounds__(256, 1) gemm_epi_kernel(const bf16* __restrict
   // ---- fragment reads: row 32·f + (lane & 31) of the wave's 128-row half, chunk 2s + hh
   const int rl = lane & 31;
   const int swl = (((rl >> 1) & 1) << 2) | ((rl >> 2) & 3);
-  // per-lane fragment base per k-step s (the wave's half of A / B included): every fragment read
-  // is then base + an immediate (buffer parity, fragment row block) of at most 45 056 bytes
-  unsigned ab[4], bb[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const unsigned fo = (unsigned)(rl * 128 + (((2 * s + hh) ^ swl) << 4));
-    ab[s] = (unsigned)(A_OFF + wr * 128 * 128) + fo;
-    bb[s] = (unsigned)(B_OFF + wc * 128 * 128) + fo;
-    asm volatile("" : "+v"(ab[s]), "+v"(bb[s]));
-  }
+  // per-lane fragment bases of k-step 0 (the wave's half of A / B included); k-step s reads chunk
+  // 2s + hh ^ swz = that of k-step 0 XOR 2s, i.e. base XOR (s << 5) (the added constants have
+  // bits 5-6 clear). Every fragment read is then base + an immediate (buffer parity, fragment row
+  // block) of at most 45 056 bytes. The XOR is redone per k-step on an opaque copy: 2 live
+  // registers instead of 8 precomputed bases (the tile-end peak is 12 registers short)
+  unsigned ab0 = (unsigned)(A_OFF + wr * 128 * 128 + rl * 128 + ((hh ^ swl) << 4));
+  unsigned bb0 = (unsigned)(B_OFF + wc * 128 * 128 + rl * 128 + ((hh ^ swl) << 4));
+  asm volatile("" : "+v"(ab0), "+v"(bb0));
+  auto abase = [&](int S) { unsigned x = ab0; asm volatile("" : "+v"(x)); return S ? x ^ (unsigned)(S << 5) : x; };
+  auto bbase = [&](int S) { unsigned x = bb0; asm volatile("" : "+v"(x)); return S ? x ^ (unsigned)(S << 5) : x; };
   auto lds16 = [&](unsigned off) -> uint4 { return __builtin_bit_cast(uint4, *(const lds_u32x4e*)(smem + off)); };
 
   f32x16 acc[4][4];
@@ -345,12 +348,13 @@ __global__ void __launch_bounds__(256, 1) gemm_epi_kernel(const bf16* __restrict
   uint4 fa[2][4], fb[2][4];
   auto load_a = [&](auto par_c, auto s_c, auto slot_c, int f) {
     constexpr int PAR = decltype(par_c)::value, S = decltype(s_c)::value, SL = decltype(slot_c)::value;
-    fa[SL][f] = lds16(ab[S] + PAR * KBUF + f * 32 * 128);
+    fa[SL][f] = lds16(abase(S) + PAR * KBUF + f * 32 * 128);
   };
   auto load_b = [&](auto par_c, auto s_c, auto slot_c) {
     constexpr int PAR = decltype(par_c)::value, S = decltype(s_c)::value, SL = decltype(slot_c)::value;
+    const unsigned b0 = bbase(S);
 #pragma unroll
-    for (int f = 0; f < 4; ++f) fb[SL][f] = lds16(bb[S] + PAR * KBUF + f * 32 * 128);
+    for (int f = 0; f < 4; ++f) fb[SL][f] = lds16(b0 + PAR * KBUF + f * 32 * 128);
   };
   auto load_frags = [&](auto par_c, auto s_c, auto slot_c) {
     load_b(par_c, s_c, slot_c);
@@ -375,8 +379,11 @@ __global__ void __launch_bounds__(256, 1) gemm_epi_kernel(const bf16* __restrict
   const bf16* c2pan = C2;
   unsigned crec = 0;      // resource size: 0 before the first tile (its units are dropped)
   int ncols = 0;          // live columns of the deferred tile
-  unsigned vrow = (unsigned)(((wr * 128 + rl) * ldc + wc * 128 + 8 * hh) * 2);
-  int vcol = wc * 128 + 8 * hh;
+  // DGELU stores a unit per lane pair and row (16 B at column 8·hh); the others store 4 staged
+  // units as 8 rows x 128 B per instruction (lane -> row lane >> 3, 8 columns at 8·(lane & 7))
+  unsigned vrow = DGELU ? (unsigned)(((wr * 128 + rl) * ldc + wc * 128 + 8 * hh) * 2)
+                        : (unsigned)(((wr * 128 + (lane >> 3)) * ldc + wc * 128 + 8 * (lane & 7)) * 2);
+  int vcol = DGELU ? wc * 128 + 8 * hh : wc * 128 + 8 * (lane & 7);
   asm volatile("" : "+v"(vrow), "+v"(vcol));
   int pcol2 = 0;  // byte offset of the deferred tile's first column (its panel starts at column 0)
   // unit U: C[row block IM, 8 columns at CO + 8·hh] of the deferred tile. DGELU: `pr` is the unit's
@@ -430,13 +437,35 @@ __global__ void __launch_bounds__(256, 1) gemm_epi_kernel(const bf16* __restrict
                                                     __float_as_uint(v[7])}, rsrc_of(colpart, cprec),
                                              (int)(writer ? co + 16u : 0x80000000u), 0, 0);
     } else {
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4e, dout[U]), rsrc_of(cpan, crec), (int)off, soff, 0);
-    }
-    if constexpr (GELU) {
-      constexpr bool TH = EPI == EG_GELU_TANH;
-      const uint4 d = dout[U];
-      const uint4 q = uint4{gelu_pair<TH>(d.x), gelu_pair<TH>(d.y), gelu_pair<TH>(d.z), gelu_pair<TH>(d.w)};
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4e, q), rsrc_of(c2pan, crec), (int)off, soff, 0);
+      // unit U = (IM, column pair JP, G = 2·jn-in-pair + kp): stage it as columns 16·G + 8·hh of a
+      // [32 rows][64 columns] image (16-B chunks XOR-swizzled by row); after the 4th unit of the
+      // group the wave reads the image back 8 rows at a time and stores full 128-B row segments
+      // (the lane-pair layout of the MFMA output would store 32-B segments: a quarter of a line)
+      (void)off;
+      (void)soff;
+      constexpr int G = U & 3, JP = (U >> 2) & 1, IMS = U >> 3;
+      const int ln = opaque_lane_id(), r = ln & 31, h = ln >> 5;
+      const unsigned sw = (unsigned)(STAGE_OFF + w * 4096 + r * 128 + (((2 * G + h) ^ (r & 7)) << 4));
+      *(lds_u32x4e*)(smem + sw) = __builtin_bit_cast(u32x4e, dout[U]);
+      if constexpr (G == 3) {
+        const unsigned rd0 = (unsigned)(STAGE_OFF + w * 4096 + (ln >> 3) * 128 + (((ln & 7) ^ (ln >> 3)) << 4));
+        const unsigned soff0 = (unsigned)(IMS * ld32 + pc2);
+        const unsigned off2 = vc + 64 * JP < nc ? vr + (unsigned)(128 * JP) : 0x80000000u;
+        // one 8-row piece at a time (sched barriers: hoisting the 4 reads costs 16 registers the
+        // deferred units do not leave)
+#pragma unroll
+        for (int q8 = 0; q8 < 4; ++q8) {
+          __builtin_amdgcn_sched_barrier(0);
+          const uint4 d = lds16(rd0 + q8 * 1024);
+          const int so = (int)(soff0 + q8 * (ld32 >> 2));
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4e, d), rsrc_of(cpan, crec), (int)off2, so, 0);
+          if constexpr (GELU) {
+            constexpr bool TH = EPI == EG_GELU_TANH;
+            const uint4 q = uint4{gelu_pair<TH>(d.x), gelu_pair<TH>(d.y), gelu_pair<TH>(d.z), gelu_pair<TH>(d.w)};
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4e, q), rsrc_of(c2pan, crec), (int)off2, so, 0);
+          }
+        }
+      }
     }
   };
   // DGELU: this lane's P chunk of unit step S of k-tile parity PAR (LDS, staged by the DMA stream)
@@ -506,9 +535,10 @@ __global__ void __launch_bounds__(256, 1) gemm_epi_kernel(const bf16* __restrict
   load_frags(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
 
   for (int ct = 0; ct < my_tiles; ++ct) {
-    PE_KT(0, 0, 3 * OPS); PE_KT(1, 1, 4 * OPS); PE_KT(0, 2, 4 * OPS); PE_KT(1, 3, 4 * OPS);
+    // (non-DGELU: a k-tile's 4·OPS stores all issue at its k-step 3)
+    PE_KT(0, 0, DGELU ? 3 * OPS : 0); PE_KT(1, 1, 4 * OPS); PE_KT(0, 2, 4 * OPS); PE_KT(1, 3, 4 * OPS);
     PE_KT(0, 4, 4 * OPS); PE_KT(1, 5, 4 * OPS); PE_KT(0, 6, 4 * OPS); PE_KT(1, 7, 4 * OPS);
-    PE_KT(0, 8, OPS); PE_KT(1, 9, 0);
+    PE_KT(0, 8, DGELU ? OPS : 4 * OPS); PE_KT(1, 9, 0);
     for (int kt = 10; kt < nk; kt += 2) {
       PE_KT(0, 8 + 2, 0);
       PE_KT(1, 8 + 2, 0);
@@ -553,7 +583,11 @@ __global__ void __launch_bounds__(256, 1) gemm_epi_kernel(const bf16* __restrict
           uint32_t by = pack_bf16x2(v[4 * kb + 2] + bv[kb][2], v[4 * kb + 3] + bv[kb][3]);
           const auto sx = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
           const auto sy = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
-          dout[jn * 8 + kp * 4 + im] = uint4{sx[0], sy[0], sx[1], sy[1]};
+          dout[DGELU ? jn * 8 + kp * 4 + im : im * 8 + (jn >> 1) * 4 + (jn & 1) * 2 + kp] =
+              uint4{sx[0], sy[0], sx[1], sy[1]};
+          // accumulator by accumulator: left free, the scheduler hoists the AGPR reads of many
+          // accumulators ahead of their packing and spills deferred units
+          __builtin_amdgcn_sched_barrier(0);
         }
     }
     zero_acc();
