@@ -1,6 +1,5 @@
 """Forward / data-gradient GEMMs of a fused executor step, one by one: hipBLASLt as the executor
-calls it (TunableOp-tuned table loaded) vs the native 8-phase kernel (csrc/kernels/gemm8.hip),
-median of interleaved rounds, TF per call and ms per step.
+calls it (TunableOp-tuned table loaded), median of interleaved rounds, TF per call and ms per step.
 
     python bench/gemm_shapes.py [--model gemma3-1b|gpt2] [--tokens N] [--iters 10]
 
@@ -17,7 +16,7 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-from penroz.ops import _ext, gemm as G  # noqa: E402
+from penroz.ops import gemm as G  # noqa: E402
 
 # (k = in_features, n = out_features, calls per step)
 MODELS = {
@@ -48,9 +47,8 @@ def main():
     a = ap.parse_args()
     cfg = MODELS[a.model]
     T = a.tokens or cfg["tokens"]
-    k8 = _ext.kernels()
     G.load_tuned_gemms()
-    step = {"blas": 0.0, "native": 0.0, "best": 0.0}
+    step = {"blas": 0.0}
     for name, (kin, nout, per_step) in cfg["shapes"].items():
         torch.manual_seed(0)
         x = (torch.rand(T, kin, device="cuda") * 2 - 1).to(torch.bfloat16)
@@ -61,10 +59,6 @@ def main():
         dx = torch.empty(T, kin, device="cuda", dtype=torch.bfloat16)
         arms = {"fwd_blas": lambda: torch.mm(x, w.t(), out=y),
                 "dgrad_blas": lambda: torch.mm(dy, wt.t(), out=dx)}
-        if kin % 128 == 0:
-            arms["fwd_native"] = lambda: k8.gemm8_bf16(x, w, None, y, None, 0)
-        if nout % 128 == 0:
-            arms["dgrad_native"] = lambda: k8.gemm8_bf16(dy, wt, None, dx, None, 0)
         res = {k: [] for k in arms}
         for _ in range(a.rounds):
             for k, fn in arms.items():
@@ -77,11 +71,7 @@ def main():
             row[k + "_us"] = round(t * 1e6, 1)
             row[k + "_TF"] = round(fl / t / 1e12, 1)
         for d in ("fwd", "dgrad"):
-            b = row[f"{d}_blas_us"]
-            n = row.get(f"{d}_native_us", float("inf"))
-            step["blas"] += b * per_step / 1e3
-            step["native"] += (n if n != float("inf") else b) * per_step / 1e3
-            step["best"] += min(b, n) * per_step / 1e3
+            step["blas"] += row[f"{d}_blas_us"] * per_step / 1e3
         print(json.dumps(row), flush=True)
     print(json.dumps({"ms_per_step": {k: round(v, 2) for k, v in step.items()}}), flush=True)
 

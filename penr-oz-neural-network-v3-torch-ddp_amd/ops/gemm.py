@@ -80,32 +80,15 @@ def load_tuned_gemms() -> bool:
     return ok
 
 
-# ---- fused linear + GELU (csrc/kernels/gemm_epi.hip) -----------------------------------------
-# The fc linear of a GPT-2 MLP and its GELU in ONE kernel: the deferred-epilogue GEMM writes the
-# pre-activation (the backward's GELU' input) and the activation (fc2's input) while its next tile
-# computes, instead of hipBLASLt's GEMM followed by the memory-bound GELU kernel (a full extra read
-# and write of the [N, 4C] activation); in the backward, fc2's data gradient, the GELU backward and
-# the fc bias gradient likewise (dgrad_gelu). OFF by default: measured on the headline step
-# (profiles/gemm_epi_r4.log) the fused path is SLOWER than hipBLASLt + the standalone GELU kernels
-# (66.4 / 65.9 ms vs 64.1 / 63.8 ms), so PENROZ_EPI_GEMM=1 is an opt-in A/B arm only.
-EPI_GEMM = os.environ.get("PENROZ_EPI_GEMM", "0") == "1"
-
-
-def epi_gemm_ok(x: Tensor, w: Tensor) -> bool:
-    """The fused kernel's shape / layout contract (K % 128 == 0, K >= 640, N % 8 == 0, bf16,
-    unit column stride, 16-B aligned rows)."""
-    return (EPI_GEMM and use_kernels(x) and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
-            and x.dim() == 2 and w.dim() == 2 and x.stride(1) == 1 and w.stride(1) == 1
-            and x.stride(0) % 8 == 0 and w.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
-            and kernels().gemm_epi_supported(x.shape[0], w.shape[0], x.shape[1]))
-
-
+# ---- linear + GELU / GELU backward (library GEMM + the HIP GELU kernels) -------------------
+# Two native fused designs were built and measured against this pair (round 3-4): an 8-phase
+# persistent MFMA GEMM with a bias/GELU epilogue and a 4-wave deferred-epilogue GEMM whose
+# stores (and GELU' / bias-column work) stream inside the next tile. Both lost on every GPT-2
+# shape and on the headline step (profiles/gemm_epi_r4.log, profiles/native_gemm_r4.md), so the
+# forward / dgrad GEMMs are hipBLASLt and the GELU work stays in elementwise.hip.
 def linear_gelu(x: Tensor, w: Tensor, bias: Tensor, pre: Tensor, act: Tensor, approximate: str = "none"):
-    """pre = x·wᵀ + bias, act = GELU(pre) (bf16; ``approximate`` "none" = erf, "tanh" = gelu_new),
-    in one kernel when ``epi_gemm_ok``; otherwise the library GEMM and the GELU kernel."""
-    if epi_gemm_ok(x, w) and pre.stride(1) == 1 and pre.stride(0) % 8 == 0 and act.stride() == pre.stride():
-        kernels().gemm_epi_bf16(x, w, bias, pre, act, 1 if approximate == "tanh" else 0)
-        return pre, act
+    """pre = x·wᵀ + bias (library GEMM), act = GELU(pre) (bf16; ``approximate`` "none" = erf,
+    "tanh" = gelu_new; the HIP GELU kernel)."""
     torch.addmm(bias, x, w.t(), out=pre)
     if use_kernels(pre):
         from penroz.ops import activations as act_ops
@@ -116,14 +99,10 @@ def linear_gelu(x: Tensor, w: Tensor, bias: Tensor, pre: Tensor, act: Tensor, ap
 
 
 def dgrad_gelu(dy: Tensor, wt: Tensor, pre: Tensor, out: Tensor, dbias: Tensor | None, approximate: str = "none"):
-    """Data gradient into a GELU's input: out = bf16(dy·wtᵀ) · GELU'(pre) and dbias (fp32) += the
-    column sums of out, in one kernel when ``epi_gemm_ok`` (``wt`` = the transposed weight copy,
-    [in, out] row-major); otherwise the library GEMM and the GELU-backward / bias-column kernel.
-    The GPT executor's fc2 data gradient + GELU backward + fc bias gradient."""
-    if (epi_gemm_ok(dy, wt) and out.stride(1) == 1 and out.stride(0) % 8 == 0 and pre.stride() == out.stride()
-            and pre.data_ptr() != out.data_ptr()):
-        kernels().gemm_epi_dgelu(dy, wt, pre, out, dbias, 1 if approximate == "tanh" else 0)
-        return out
+    """Data gradient into a GELU's input: out = bf16(dy·wtᵀ) (library GEMM; ``wt`` = the
+    transposed weight copy, [in, out] row-major), then out *= GELU'(pre) and dbias (fp32) += the
+    column sums of out in one HIP kernel. The GPT executor's fc2 data gradient + GELU backward +
+    fc bias gradient."""
     torch.mm(dy, wt.t(), out=out)
     from penroz.ops import activations as act_ops
     act_ops.gelu_bwd(out, pre, approximate, dbias, out=out)
