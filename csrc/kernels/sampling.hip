@@ -10,6 +10,7 @@
 // and batches of >= 16 rows (greedy / top-k <= 64, V <= 256 Ki) go through the two-stage
 // sample_part_kernel + sample_merge_kernel.
 #include "common.h"
+#include <cstdlib>
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 
@@ -745,9 +746,16 @@ static void launch_sample(const torch::Tensor& logits, const SampleIO& io, doubl
   const bool fits = chunks <= (logits.scalar_type() == torch::kBFloat16 ? 16 : 8);
   const float tt = (float)temperature;
   const int kk = (int)top_k;
-  // the two-stage form for rows too wide for registers, and for many rows (a batch-64 decode
-  // step: P x B part workgroups fill the chip where B one-row workgroups leave most CUs idle)
-  if (V % 8 == 0 && (!fits || B >= 16) && logits.scalar_type() != torch::kFloat16 &&
+  // the two-stage form for rows too wide for registers, and for any number of rows from
+  // kTwoStageMinRows on (P x B part workgroups spread a row over P CUs where one workgroup per row
+  // leaves most of the chip idle: a batch-64 decode step, and a batch-1 step whose single-workgroup
+  // register sampler took ~38 µs of a ~600 µs GPT-2 token). PENROZ_SAMPLE_TWO_STAGE_MIN_ROWS
+  // moves the switch (A/B; the register kernel serves the rows below it)
+  static const int kTwoStageMinRows = [] {
+    const char* e = std::getenv("PENROZ_SAMPLE_TWO_STAGE_MIN_ROWS");
+    return e ? std::atoi(e) : 1;
+  }();
+  if (V % 8 == 0 && (!fits || B >= kTwoStageMinRows) && logits.scalar_type() != torch::kFloat16 &&
       V <= kPartMaxP * kPartN && (temperature == 0.0 || (top_k > 0 && top_k <= kPartK))) {
     const int P = (V + kPartN - 1) / kPartN;
     const bool topk = temperature != 0.0;
