@@ -511,7 +511,9 @@ __device__ __forceinline__ void ring_tail(F&& f, int base, int total, std::integ
   ((base + S < total ? f(base + S, std::integral_constant<int, S>{}) : void()), ...);
 }
 
-template <bool DROPOUT, int NST>
+// GC: the query-group size H/Hkv when known at compile time (1: multi-head attention — the
+// slice counter then maps to (head, slice) without the per-iteration division), 0 = any
+template <bool DROPOUT, int NST, int GC>
 __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv3_kernel(const bf16* __restrict__ qkv,
                                                               const bf16* __restrict__ dout,
                                                               const float* __restrict__ lse,
@@ -525,7 +527,7 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv3_kernel(const bf16* __rest
   int kb, bh;
   xcd_head_block(kb, bh);
   const int b = bh / Hkv, hk = bh % Hkv;
-  const int G = H / Hkv;
+  const int G = GC ? GC : H / Hkv;
   const int lane = threadIdx.x & 63, w = wave_id(), hh = lane >> 5;
   const size_t RS = (size_t)(H + 2 * Hkv) * kD;
   const size_t ORS = (size_t)H * kD;
@@ -595,8 +597,8 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv3_kernel(const bf16* __rest
   }
   auto dma = [&](int it) {
     const int itc = min(it, total - 1);  // beyond the end: refetch the last slice (uniform counts)
-    const int hq = hk * G + itc / per_head;
-    const int qs0 = (s_first + itc % per_head) * QS;
+    const int hq = GC == 1 ? hk : hk * G + itc / per_head;
+    const int qs0 = (s_first + (GC == 1 ? itc : itc % per_head)) * QS;
     const unsigned st = __builtin_amdgcn_readfirstlane(lds_addr_of(smem + (it % NST) * STAGE));
     const bf16* src = is_do ? dout + (size_t)b * T * ORS + (size_t)hq * kD : qkv + (size_t)b * T * RS + (size_t)hq * kD;
     const size_t rs = is_do ? ORS : RS;
@@ -640,8 +642,8 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv3_kernel(const bf16* __rest
     const char* stg = smem + ST * STAGE;
     const float* lse_s = reinterpret_cast<const float*>(stg + 2 * TILE);
     const float* del_s = lse_s + QS;
-    const int hq = hk * G + it / per_head;
-    const int qs0 = (s_first + it % per_head) * QS;
+    const int hq = GC == 1 ? hk : hk * G + it / per_head;
+    const int qs0 = (s_first + (GC == 1 ? it : it % per_head)) * QS;
     bool act[2];
     f32x16 sp[2], dp[2];
 #pragma unroll
@@ -661,10 +663,18 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv3_kernel(const bf16* __rest
             dp[half][4 * g + k] = DROPOUT ? 0.f : -dl[k];
           }
         }
+        // all 8 operand fragments requested first, then the 8 MFMAs: one LDS latency per half
+        // instead of one per MFMA pair
+        uint4 qa[4], da[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          sp[half] = mfma32(rowf(Qt, s), kf[s], sp[half]);
-          dp[half] = mfma32(rowf(Dt, s), vf[s], dp[half]);
+          qa[s] = rowf(Qt, s);
+          da[s] = rowf(Dt, s);
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          sp[half] = mfma32(qa[s], kf[s], sp[half]);
+          dp[half] = mfma32(da[s], vf[s], dp[half]);
         }
       }
     }
@@ -676,6 +686,18 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv3_kernel(const bf16* __rest
         const char* Dt = stg + TILE + half * 32 * 128;
         const bool need_mask = (kw0 + 31 > qh0) || (qh0 + 32 > T) || (kw0 + 32 > T);
         const uint32_t drow0 = DROPOUT ? (uint32_t)((b * H + hq) * T + qh0 + 4 * hh) * kDropRowMul : 0u;
+        // the dV / dK operand fragments (transposed reads) go out before the softmax-gradient VALU
+        // (not with dropout: its hash registers leave no room — 42 spilled — so it reads at use)
+        uint4 tdo[2][2], tqq[2][2];
+        if constexpr (!DROPOUT) {
+#pragma unroll
+          for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+            for (int dh = 0; dh < 2; ++dh) {
+              tdo[ss][dh] = trf(Dt + 16 * ss * 128, dh);
+              tqq[ss][dh] = trf(Qt + 16 * ss * 128, dh);
+            }
+        }
         auto grads = [&](auto mask_tag) {
           constexpr bool MASK = decltype(mask_tag)::value;
 #pragma unroll
@@ -709,8 +731,8 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv3_kernel(const bf16* __rest
           const uint4 pf = acc_frag(sp[half], ss), sf = acc_frag(dp[half], ss);
 #pragma unroll
           for (int dh = 0; dh < 2; ++dh) {
-            dv[dh] = mfma32(trf(Dt + 16 * ss * 128, dh), pf, dv[dh]);
-            dk[dh] = mfma32(trf(Qt + 16 * ss * 128, dh), sf, dk[dh]);
+            dv[dh] = mfma32(DROPOUT ? trf(Dt + 16 * ss * 128, dh) : tdo[ss][dh], pf, dv[dh]);
+            dk[dh] = mfma32(DROPOUT ? trf(Qt + 16 * ss * 128, dh) : tqq[ss][dh], sf, dk[dh]);
           }
         }
       }
@@ -894,16 +916,27 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dq4_kernel(const bf16* __restri
           s[kh][i] = -l2;  // S accumulates onto −LSE·log2(e) of this lane's query row: P = exp2(S)
           dp[kh][i] = DROPOUT ? 0.f : -dl;
         }
+        uint4 ka[4], va[4];  // fragments first, then the MFMAs (one LDS latency per 32 keys)
 #pragma unroll
         for (int st = 0; st < 4; ++st) {
-          s[kh] = mfma32(rowf(Kt + 32 * kh * 128, st), qf[st], s[kh]);
-          dp[kh] = mfma32(rowf(Vt + 32 * kh * 128, st), dof[st], dp[kh]);
+          ka[st] = rowf(Kt + 32 * kh * 128, st);
+          va[st] = rowf(Vt + 32 * kh * 128, st);
+        }
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+          s[kh] = mfma32(ka[st], qf[st], s[kh]);
+          dp[kh] = mfma32(va[st], dof[st], dp[kh]);
         }
       }
       const bool need_mask = (kt0 + BN - 1 > q0) || (kt0 + BN > T) || (q0 + 32 > T);
       const uint32_t kpair0 = DROPOUT ? (uint32_t)((kt0 + 4 * hh) >> 1) * kDropKeyMul : 0u;
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh) {
+        uint4 tk[2][2];  // the dQ operand fragments (transposed K reads) before the VALU
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+          for (int dh = 0; dh < 2; ++dh) tk[ss][dh] = trf(Kt + (32 * kh + 16 * ss) * 128, dh);
         auto grads = [&](auto mask_tag) {
           constexpr bool MASK = decltype(mask_tag)::value;
 #pragma unroll
@@ -928,7 +961,7 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dq4_kernel(const bf16* __restri
         for (int ss = 0; ss < 2; ++ss) {
           const uint4 sf = acc_frag(s[kh], ss);
 #pragma unroll
-          for (int dh = 0; dh < 2; ++dh) dq[dh] = mfma32(trf(Kt + (32 * kh + 16 * ss) * 128, dh), sf, dq[dh]);
+          for (int dh = 0; dh < 2; ++dh) dq[dh] = mfma32(tk[ss][dh], sf, dq[dh]);
         }
       }
     }
@@ -1037,7 +1070,10 @@ void flash_attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, to
   const bool drop = p_drop > 0.0;
   BwdKernel kv;
   DqKernel dq;
-  kv = drop ? fa_bwd_dkdv3_kernel<true, 3> : fa_bwd_dkdv3_kernel<false, 3>;
+  if (H == Hkv)
+    kv = drop ? fa_bwd_dkdv3_kernel<true, 3, 1> : fa_bwd_dkdv3_kernel<false, 3, 1>;
+  else
+    kv = drop ? fa_bwd_dkdv3_kernel<true, 3, 0> : fa_bwd_dkdv3_kernel<false, 3, 0>;
   dq = drop ? fa_bwd_dq4_kernel<true, 3> : fa_bwd_dq4_kernel<false, 3>;
   const float pd = drop ? (float)p_drop : 0.f;
   const bool want_bias = dbias.has_value() && dbias->defined();
