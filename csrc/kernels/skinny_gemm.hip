@@ -17,6 +17,7 @@
 // C/D layout of mfma_f32_16x16x32_bf16: col = lane & 15 (row m of x), row = 4·(lane >> 4) + r
 // (output column n), so each lane ends with 4 consecutive outputs of one row.
 #include "common.h"
+#include <vector>
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 
@@ -620,6 +621,26 @@ void skinny_gated(torch::Tensor x, torch::Tensor gu, torch::Tensor out, int64_t 
 #undef PENROZ_SKG
 }
 
+// The fused QKV + RoPE kernel's automatic split-K (workgroups ~ 192 when the 32-column tiles alone
+// are too few) and the fp32 workspace it then needs: ONE rule, used by the launcher below and
+// exported (skinny_qkv_rope_plan) for the Python-side admission check (ops/gemm.py
+// skinny_qkv_rope_ok), which must refuse a shape before a graph capture rather than let this
+// launcher's workspace check throw inside it.
+static int qkv_rope_auto_split(int N, int K) {
+  const int ntiles = N / 32, steps = K / 32;
+  return ntiles >= 128 ? 1 : std::max(1, std::min({(192 + ntiles - 1) / ntiles, steps / 4, 16}));
+}
+static int64_t qkv_rope_ws_floats(int M, int N, int splitk) {
+  const int MB = M <= 16 ? 1 : M <= 32 ? 2 : 4;
+  return splitk > 1 ? (int64_t)splitk * (N / 32) * MB * 512 : 0;
+}
+
+// (split-K, fp32 workspace floats, counters) of skinny_qkv_rope at M rows, N = heads·D, K
+std::vector<int64_t> skinny_qkv_rope_plan(int64_t M, int64_t N, int64_t K) {
+  const int split = qkv_rope_auto_split((int)N, (int)K);
+  return {split, qkv_rope_ws_floats((int)M, (int)N, split), split > 1 ? N / 32 : 0};
+}
+
 // out[M, (H + 2Hkv)·D] = x · wᵀ with RoPE (cos / sin [D/2] of the one decode position) applied to
 // the first nrot = H + Hkv heads; M <= 64, D % 32 == 0. Returns the split-K factor used.
 int64_t skinny_qkv_rope(torch::Tensor x, torch::Tensor w, torch::Tensor cosv, torch::Tensor sinv, int64_t D,
@@ -640,14 +661,11 @@ int64_t skinny_qkv_rope(torch::Tensor x, torch::Tensor w, torch::Tensor cosv, to
               "skinny_qkv_rope: fp32 cos / sin [D/2]");
   const int ntiles = N / 32, steps = K / 32;
   const int MB = M <= 16 ? 1 : M <= 32 ? 2 : 4;
-  if (splitk <= 0) {
-    splitk = 1;
-    if (ntiles < 128) splitk = std::max(1, std::min({(192 + ntiles - 1) / ntiles, steps / 4, 16}));
-  }
+  if (splitk <= 0) splitk = qkv_rope_auto_split(N, K);
   TORCH_CHECK(splitk >= 1 && splitk <= steps, "skinny_qkv_rope: bad split");
   if (splitk > 1) {
-    TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == torch::kFloat32 &&
-                    ws.numel() >= (int64_t)splitk * ntiles * MB * 512, "skinny_qkv_rope: workspace too small");
+    TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == torch::kFloat32 && ws.numel() >= qkv_rope_ws_floats(M, N, (int)splitk),
+                "skinny_qkv_rope: workspace too small");
     TORCH_CHECK(cnt.is_cuda() && cnt.scalar_type() == torch::kInt32 && cnt.numel() >= ntiles,
                 "skinny_qkv_rope: counters too small");
   }

@@ -166,10 +166,14 @@ def skinny_qkv_rope_ok(x: Tensor, w: Tensor, D: int) -> bool:
     its split-K slabs fit the shared workspace."""
     if not (skinny_ok(x, w) and D % 32 == 0 and w.shape[0] % D == 0):
         return False
-    rows, ntiles, steps = x.numel() // x.shape[-1], w.shape[0] // 32, x.shape[-1] // 32
-    mb = 1 if rows <= 16 else 2 if rows <= 32 else 4
-    split = 1 if ntiles >= 128 else max(1, min(-(-192 // ntiles), steps // 4, 16))
-    return split * ntiles * mb * 512 <= (1 << 19) and ntiles <= (1 << 12)
+    return qkv_rope_plan_fits(x.numel() // x.shape[-1], w.shape[0], x.shape[-1])
+
+
+def qkv_rope_plan_fits(rows: int, n: int, k: int) -> bool:
+    """The kernel's own split-K plan (csrc/kernels/skinny_gemm.hip skinny_qkv_rope_plan: the rule
+    its launcher applies) fits the shared workspace and counters of ``skinny_workspace``."""
+    _, ws_floats, counters = kernels().skinny_qkv_rope_plan(rows, n, k)
+    return ws_floats <= (1 << 19) and counters <= (1 << 12)
 
 
 def skinny_qkv_rope(x: Tensor, w: Tensor, cos: Tensor, sin: Tensor, D: int, nrot: int) -> Tensor:
