@@ -228,18 +228,32 @@ class HookedReducer:
         self.sparse = [p for p in order if id(p) in ids and p.dim() == 2]
         segments = []
         off = 0
+        esz = self.flat_grad.element_size()
+        # a parameter larger than a bucket is cut into bucket-sized pieces, each its own bucket
+        # (the CPU plumbing config's 147 MB lm_head weight: one collective of that size held every
+        # later bucket behind it); all pieces launch when the parameter's gradient lands
+        piece = max(1, int(bucket_mb * 2**20) // esz)
+        if os.environ.get("PENROZ_SPLIT_BIG_PARAMS", "1") == "0":  # A/B: whole parameters only
+            piece = 1 << 62
         for p in order:
             n = p.numel()
             self.offsets[p] = off
             if not any(p is q for q in self.sparse):
-                segments.append((off, off + n))
+                if n > piece:
+                    segments.extend((s0, min(off + n, s0 + piece)) for s0 in range(off, off + n, piece))
+                else:
+                    segments.append((off, off + n))
             off += n
-        self.reducer = GradReducer(self.flat_grad, plan_buckets(segments, bucket_mb * 2**20,
-                                                                self.flat_grad.element_size()), group)
+        self.reducer = GradReducer(self.flat_grad, plan_buckets(segments, bucket_mb * 2**20, esz), group)
         self.group = group
-        self._param_bucket = {}
+        self._param_bucket = {}  # parameter -> the buckets holding (pieces of) its gradient
         for p in order:
-            self._param_bucket[p] = -1 if any(p is q for q in self.sparse) else self.reducer.bucket_of(self.offsets[p])
+            if any(p is q for q in self.sparse):
+                self._param_bucket[p] = []
+                continue
+            first = self.reducer.bucket_of(self.offsets[p])
+            last = self.reducer.bucket_of(self.offsets[p] + p.numel() - 1)
+            self._param_bucket[p] = list(range(first, last + 1))
         self._rows_pending: list = []
         self.sync = True
         self._handles = [p.register_post_accumulate_grad_hook(self._hook) for p in order]
@@ -254,18 +268,17 @@ class HookedReducer:
     def _reset_counts(self):
         self._pending = [0] * len(self.reducer.buckets)
         for p in self.params:
-            if self._param_bucket[p] >= 0:
-                self._pending[self._param_bucket[p]] += 1
+            for b in self._param_bucket[p]:
+                self._pending[b] += 1
 
     def _hook(self, p):
         if not self.sync:
             return
-        b = self._param_bucket[p]
-        if b < 0:  # row-sparse tables reduce in finish(): same collective order on every rank
-            return
-        self._pending[b] -= 1
-        if self._pending[b] == 0:
-            self.reducer.bucket_ready(b)
+        # (row-sparse tables hold no bucket: they reduce in finish(), same order on every rank)
+        for b in self._param_bucket[p]:
+            self._pending[b] -= 1
+            if self._pending[b] == 0:
+                self.reducer.bucket_ready(b)
 
     def _reduce_rows(self, p):
         """All-reduce only the rows of ``p.grad`` that some rank touched: one small all-reduce of

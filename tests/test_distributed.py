@@ -84,6 +84,9 @@ def _hooked_worker(rank, world, port, out, sparse=False):
     if sparse:
         assert len(tables) == 2  # token + position tables (the lm_head is untied)
     red = HookedReducer(list(m.parameters()), bucket_mb=0.001, sparse_rows=tables)
+    # ~1 KB buckets: parameters larger than a bucket are cut into several (their pieces reduce
+    # as separate collectives once the parameter's gradient lands)
+    assert any(len(bs) > 1 for bs in red._param_bucket.values())
     torch.manual_seed(100 + rank)
     for micro in range(2):  # grad accumulation: the row union covers both micro-steps
         red.sync = micro == 1
