@@ -34,6 +34,9 @@ SWEEP_SIZES_MB = (16, 32, 64, 128, 256)
 # native communicator channel counts tried on first contact (0 = RCCL's own choice); an MI355X
 # node has 7 xGMI links per GPU, so the useful counts are multiples of the rings RCCL lays over them
 SWEEP_CHANNELS = (0, 8, 16, 32)
+# protocols forced on a native communicator at RCCL's own channel count ("" = RCCL's per-size
+# choice): Simple (bandwidth) vs LL128 (latency / mid sizes); LL is for small messages, not buckets
+SWEEP_PROTOS = ("", "Simple", "LL128")
 _LOG_DIR = "/tmp"
 
 
@@ -88,9 +91,9 @@ def _sync(device):
         torch.cuda.synchronize(device)
 
 
-def _native_or_none(device, channels: int = 0):
-    """The C++ communicator (``channels`` > 0: built with exactly that many RCCL channels) on every
-    rank, or None on every rank (agreed over the c10d group).
+def _native_or_none(device, channels: int = 0, proto: str = ""):
+    """The C++ communicator (``channels`` > 0: built with exactly that many RCCL channels; ``proto``:
+    with that RCCL protocol forced) on every rank, or None on every rank (agreed over the c10d group).
 
     A rank that refuses right away (module missing, duplicate device, init error) makes every
     rank fall back. A rank that BLOCKS inside ncclCommInitRank while another refused cannot be
@@ -125,10 +128,11 @@ def _native_or_none(device, channels: int = 0):
         guard.start()
         built = torch.zeros(1, device=device)
         try:
-            native = rccl.NativeComm.get(channels=channels)
+            native = rccl.NativeComm.get(channels=channels, proto=proto)
             built += 1
         except RuntimeError as e:  # refused right away on this rank: everybody falls back to c10d
-            log.warning(f"native RCCL communicator ({channels or 'default'} channels) unavailable: {e}")
+            log.warning(f"native RCCL communicator ({channels or 'default'} channels, protocol "
+                        f"{proto or 'default'}) unavailable: {e}")
         finally:
             guard.cancel()
         dist.all_reduce(built, op=dist.ReduceOp.MIN)
@@ -138,13 +142,14 @@ def _native_or_none(device, channels: int = 0):
 
 
 def sweep(device: torch.device, sizes_mb=SWEEP_SIZES_MB, wires=("fp32", "bf16"), transports=("c10d", "native"),
-          iters: int = 3, warmup: int = 1, channels=(0,)) -> list[dict]:
+          iters: int = 3, warmup: int = 1, channels=(0,), protos=("",)) -> list[dict]:
     """Time every (transport, wire, bucket size); max over ranks; correctness-checked.
 
     ``channels``: the native communicator is swept once per channel count (0 = RCCL's own
     choice; others build a communicator with exactly that many channels — the per-communicator
-    form of ``NCCL_MIN/MAX_NCHANNELS``); the extra counts are swept at fp32 only. Every row says
-    which (``channels``: None for c10d).
+    form of ``NCCL_MIN/MAX_NCHANNELS``); ``protos``: at the first channel count, once more per
+    forced protocol (the per-communicator form of ``NCCL_PROTO``). The extra arms are swept at
+    fp32 only. Every row says which (``channels`` / ``proto``: None for c10d, "" = RCCL's).
 
     The input on rank r is r + 1 everywhere, so the average is (n + 1) / 2 exactly in fp32 and
     bf16 (n ≤ 255); ``ok`` records whether the result matched on every rank."""
@@ -152,24 +157,26 @@ def sweep(device: torch.device, sizes_mb=SWEEP_SIZES_MB, wires=("fp32", "bf16"),
     gloo = dist.get_backend() != "nccl"
     natives = {}
     if "native" in transports:
-        for ch in channels:
-            c = _native_or_none(device, ch)
-            if c is None and ch == channels[0]:
+        native_arms = [(ch, protos[0]) for ch in channels] + [(channels[0], pr) for pr in protos[1:]]
+        for ch, pr in native_arms:
+            c = _native_or_none(device, ch, pr)
+            if c is None and (ch, pr) == native_arms[0]:
                 break  # the communicator cannot be built at all
             if c is not None:
-                natives[ch] = c
+                natives[(ch, pr)] = c
     expect = (world + 1) / 2.0
-    arms = [(tr, None) for tr in transports if tr != "native"] + [("native", ch) for ch in natives]
+    arms = [(tr, None) for tr in transports if tr != "native"] + [("native", k) for k in natives]
     rows = []
     for wire in wires:
         dt = {"fp32": torch.float32, "bf16": torch.bfloat16}[wire]
         for mb in sizes_mb:
             n = int(mb * 2**20) // 4  # elements of an fp32 gradient bucket of that size
             buf = torch.empty(n, device=device, dtype=dt)
-            for tr, ch in arms:
-                if tr == "native" and wire != "fp32" and ch != channels[0]:
+            for tr, key in arms:
+                if tr == "native" and wire != "fp32" and key != (channels[0], protos[0]):
                     continue
-                native = natives.get(ch)
+                native = natives.get(key)
+                ch, pr = key if key is not None else (None, None)
 
                 def one():
                     if tr == "native":
@@ -200,16 +207,17 @@ def sweep(device: torch.device, sizes_mb=SWEEP_SIZES_MB, wires=("fp32", "bf16"),
                 sec = float(t.item())
                 nbytes = buf.numel() * buf.element_size()
                 alg = nbytes / sec / 1e9
-                rows.append({"transport": tr, "channels": ch, "wire": wire, "bucket_mb": mb, "ms": round(sec * 1e3, 4),
+                rows.append({"transport": tr, "channels": ch, "proto": pr, "wire": wire, "bucket_mb": mb,
+                             "ms": round(sec * 1e3, 4),
                              "algbw_GBps": round(alg, 2), "busbw_GBps": round(alg * 2 * (world - 1) / world, 2),
                              "ok": bool(good.item() > 0)})
             del buf
     return rows
 
 
-def _arm_rows(rows, transport, channels, wire="fp32"):
+def _arm_rows(rows, transport, channels, wire="fp32", proto=""):
     return [r for r in rows if r["transport"] == transport and r["wire"] == wire and r["ok"]
-            and (transport != "native" or r.get("channels", 0) == channels)]
+            and (transport != "native" or (r.get("channels", 0) == channels and (r.get("proto") or "") == proto))]
 
 
 def plan(rows: list[dict], grad_bytes: int, backward_ms: float | None = None, margin: float = 1.03,
@@ -225,40 +233,43 @@ def plan(rows: list[dict], grad_bytes: int, backward_ms: float | None = None, ma
        hide behind the backward — and the bf16 wire of the same transport, correct at that size,
        is ≥ ``bf16_gain`` × faster for the whole gradient.
 
-    Returns {"transport", "channels", "bucket_mb", "wire", "predicted_fp32_ms", ...,"reason"}."""
-    out = {"transport": "c10d", "channels": None, "bucket_mb": None, "wire": "fp32"}
+    The native arms are (channel count, protocol) pairs; the winning arm brings both.
+
+    Returns {"transport", "channels", "proto", "bucket_mb", "wire", "predicted_fp32_ms", ...,"reason"}."""
+    out = {"transport": "c10d", "channels": None, "proto": None, "bucket_mb": None, "wire": "fp32"}
     c_rows = _arm_rows(rows, "c10d", None)
     if not c_rows:
         out["reason"] = "no correct c10d rows"
         return out
-    arms = {("c10d", None): c_rows}
-    for ch in sorted({r.get("channels", 0) for r in rows if r["transport"] == "native"}):
-        nr = _arm_rows(rows, "native", ch)
+    arms = {("c10d", None, None): c_rows}
+    for ch, pr in sorted({(r.get("channels", 0), r.get("proto") or "") for r in rows if r["transport"] == "native"}):
+        nr = _arm_rows(rows, "native", ch, proto=pr)
         if nr:
-            arms[("native", ch)] = nr
+            arms[("native", ch, pr)] = nr
     picked = {}
     for key, ar in arms.items():
         best = max(r["busbw_GBps"] for r in ar)
         pick = min((r for r in ar if r["busbw_GBps"] >= 0.9 * best), key=lambda r: r["bucket_mb"])
         picked[key] = pick
-    c = picked[("c10d", None)]
+    c = picked[("c10d", None, None)]
     nat = [(k, r) for k, r in picked.items() if k[0] == "native"]
-    choice_key, choice = ("c10d", None), c
+    choice_key, choice = ("c10d", None, None), c
     if nat:
         nk, nr = max(nat, key=lambda kv: kv[1]["busbw_GBps"])
         if nr["busbw_GBps"] >= margin * c["busbw_GBps"]:
             choice_key, choice = nk, nr
-        out["reason"] = (f"native ({nk[1] or 'default'} channels) {nr['busbw_GBps']} GB/s at {nr['bucket_mb']} MB vs "
-                         f"c10d {c['busbw_GBps']} GB/s at {c['bucket_mb']} MB")
+        out["reason"] = (f"native ({nk[1] or 'default'} channels, protocol {nk[2] or 'default'}) {nr['busbw_GBps']} "
+                         f"GB/s at {nr['bucket_mb']} MB vs c10d {c['busbw_GBps']} GB/s at {c['bucket_mb']} MB")
     else:
         out["reason"] = "no correct native arm"
-    out.update(transport=choice_key[0], channels=choice_key[1], bucket_mb=choice["bucket_mb"],
+    out.update(transport=choice_key[0], channels=choice_key[1], proto=choice_key[2], bucket_mb=choice["bucket_mb"],
                busbw_GBps=choice["busbw_GBps"])
     fp32_ms = grad_bytes / (choice["algbw_GBps"] * 1e9) * 1e3
     out["predicted_fp32_ms"] = round(fp32_ms, 3)
     bf = [r for r in rows if r["transport"] == choice_key[0] and r["wire"] == "bf16" and r["ok"]
           and r["bucket_mb"] == choice["bucket_mb"]
-          and (choice_key[0] != "native" or r.get("channels", 0) == choice_key[1])]
+          and (choice_key[0] != "native" or (r.get("channels", 0) == choice_key[1]
+                                             and (r.get("proto") or "") == choice_key[2]))]
     if bf:
         bf16_ms = (grad_bytes / 2) / (bf[0]["algbw_GBps"] * 1e9) * 1e3
         out["predicted_bf16_ms"] = round(bf16_ms, 3)
