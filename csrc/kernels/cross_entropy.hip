@@ -13,6 +13,7 @@
 // the logits buffer, e.g. HF GPT-2's V = 50257 → ld 50264), so every 16-B chunk stays inside its
 // row's allocation; elements at or past V count as −∞ logits and get a zero gradient.
 #include "common.h"
+#include <type_traits>
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 
@@ -42,6 +43,73 @@ __global__ void __launch_bounds__(kCEThreads) ce_kernel(T* __restrict__ logits, 
   const int64_t tgt = targets[row];
   PZ_DEVICE_CHECK(tgt == ignore_index || (tgt >= 0 && tgt < V));
   const int t = threadIdx.x;
+  if constexpr (std::is_same<T, bf16>::value) {
+    // bf16 rows stay PACKED in registers (CPT × 4 VGPRs instead of CPT × 8 fp32): at GPT-2's
+    // vocabulary (CPT = 7) the fp32 copy took the kernel to 76 VGPRs — 6 waves per SIMD, ONE
+    // 16-wave workgroup (one row) per CU, so each row's load, two block reductions and store ran
+    // back to back with the CU's memory pipe idle in between. Packed, two rows share a CU. The
+    // exponentials are recomputed in the gradient pass (VALU is idle in this HBM-bound kernel).
+    uint4 u[CPT];
+    float m = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      const int c = 8 * (t + kCEThreads * k);
+      u[k] = uint4{0xff80ff80u, 0xff80ff80u, 0xff80ff80u, 0xff80ff80u};  // bf16 -inf pairs
+      if (c < V) {
+        u[k] = *reinterpret_cast<const uint4*>(rp + c);
+        if (c + 8 > V) {  // the row's last, partial chunk: elements past V become -inf
+          uint32_t w[4] = {u[k].x, u[k].y, u[k].z, u[k].w};
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (c + j >= V) w[j >> 1] = (j & 1) ? (w[j >> 1] & 0x0000ffffu) | 0xff800000u : (w[j >> 1] & 0xffff0000u) | 0xff80u;
+          u[k] = uint4{w[0], w[1], w[2], w[3]};
+        }
+      }
+      const uint32_t w[4] = {u[k].x, u[k].y, u[k].z, u[k].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) m = fmaxf(m, fmaxf(__uint_as_float(w[q] << 16), __uint_as_float(w[q] & 0xffff0000u)));
+    }
+    // the packed words are made opaque before each later pass: left alone, hipcc keeps the unpacked
+    // fp32 values of the max pass alive for the other two (common subexpressions) — 78 VGPRs again
+    auto opaque = [&]() {
+#pragma unroll
+      for (int k = 0; k < CPT; ++k) asm volatile("" : "+v"(u[k].x), "+v"(u[k].y), "+v"(u[k].z), "+v"(u[k].w));
+    };
+    m = block_reduce(m, sh, true);
+    opaque();
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      const uint32_t w[4] = {u[k].x, u[k].y, u[k].z, u[k].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        s += __expf(__uint_as_float(w[q] << 16) - m) + __expf(__uint_as_float(w[q] & 0xffff0000u) - m);
+    }
+    s = block_reduce(s, sh, false);
+    const float lse = m + __logf(s);
+    const bool valid = tgt != ignore_index && tgt >= 0 && tgt < V;
+    if (t == 0) loss[row] = valid ? lse - to_f(rp[tgt]) : 0.f;
+    if (scale == 0.f) return;
+    const float sc = valid ? scale : 0.f;
+    const float ps = sc / s;
+    __syncthreads();  // the target logit is read before any thread overwrites it
+    opaque();
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      const int c = 8 * (t + kCEThreads * k);
+      if (c < V) {
+        const uint32_t w[4] = {u[k].x, u[k].y, u[k].z, u[k].w};
+        float g[8];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          g[2 * q] = fmaf(__expf(__uint_as_float(w[q] << 16) - m), ps, c + 2 * q == tgt ? -sc : 0.f);
+          g[2 * q + 1] = fmaf(__expf(__uint_as_float(w[q] & 0xffff0000u) - m), ps, c + 2 * q + 1 == tgt ? -sc : 0.f);
+        }
+        Vec8<T>::store(gp + c, g);
+      }
+    }
+    return;
+  }
   float v[CPT][8];
   float m = -INFINITY;
 #pragma unroll

@@ -215,10 +215,10 @@ def test_combine_kernels_match_autograd(mode, C):
         assert rel(dw1, w1.grad) < 1e-4
 
 
-def test_gated_bwd_packed_matches_unpacked():
+@pytest.mark.parametrize("N,F", [(77, 512), (1100, 6912)])  # the second: several grid trips, unrolled
+def test_gated_bwd_packed_matches_unpacked(N, F):
     torch.manual_seed(0)
     k = _ext.kernels()
-    N, F = 77, 512
     gu = torch.randn(N, 2 * F, device=DEV).to(torch.bfloat16)
     dy = torch.randn(N, F, device=DEV).to(torch.bfloat16)
     for kind in (0, 1, 2):
@@ -229,6 +229,8 @@ def test_gated_bwd_packed_matches_unpacked():
         y = torch.empty(N, F, device=DEV, dtype=torch.bfloat16)
         k.gated_act_packed(gu, kind, y)
         assert torch.equal(y, k.gated_act_packed(gu, kind))
+        ref = k.gated_act_fwd(gu[:, :F].contiguous(), gu[:, F:].contiguous(), kind)
+        assert torch.equal(y, ref)
 
 
 def _curve(engine, steps, data, seed=0):

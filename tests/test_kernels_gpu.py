@@ -106,6 +106,23 @@ def test_gelu(approx):
     _close(dbias, out.float().sum(0), 0.05, 1e-3)
 
 
+@pytest.mark.parametrize("rows", [8192, 8191])
+def test_gelu_wide_grid_stride_and_row_pairs(rows):
+    """Sizes past one trip of the grid: the GELU forward's 4-chunk unrolled trips and its tail, the
+    backward + column-sum kernel's two-rows-per-trip loop with odd row counts per wave."""
+    torch.manual_seed(rows)
+    x = (torch.randn(rows, 3072, device=DEV) * 3).to(torch.bfloat16)
+    y = Ac.gelu_fwd(x, "none")
+    _close(y, F.gelu(x.float()), 0.03, 0.01)
+    dy = torch.randn_like(x)
+    ref = Ac.reference_gelu_bwd(dy, x, "none")
+    dbias = torch.zeros(3072, device=DEV)
+    out = dy.clone()
+    Ac.gelu_bwd(out, x, "none", dbias, out=out)
+    _close(out, ref, 0.05, 0.01)
+    _close(dbias, out.float().sum(0), 0.05, 1e-3)
+
+
 @pytest.mark.parametrize("N,V", [(64, 50304), (37, 262144), (5, 1000)])
 def test_fused_cross_entropy_autograd_matches_torch(N, V):
     """fused_ops.cross_entropy (bf16 logits, separate gradient buffer, device-side mean over the
@@ -224,9 +241,9 @@ def test_cross_entropy_any_vocab_padded_rows(V):
     _close(logits, x.float() @ w.float().t(), 0.1, 0.01)
 
 
-def test_adamw_flat_matches_torch():
+@pytest.mark.parametrize("n", [10007, 10_000_003])  # the second runs the 2-group unrolled trips
+def test_adamw_flat_matches_torch(n):
     torch.manual_seed(0)
-    n = 10007
     p = torch.randn(n, device=DEV)
     ref = p.clone().requires_grad_()
     opt = torch.optim.AdamW([ref], lr=1e-2, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
