@@ -26,7 +26,14 @@
 // dKᵀ / dVᵀ quarters 128), the dQ kernel into two halves (Q, dO 256 VGPRs, dQᵀ half 128) — each
 // part recomputing S and dP over the full D.
 #include "attn_common.h"
+#include <algorithm>
+#include <cstdlib>
+#include <map>
+#include <mutex>
+#include <queue>
+#include <tuple>
 #include <type_traits>
+#include <vector>
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 
@@ -74,10 +81,61 @@ template <int D> constexpr int dq_parts() { return D >= 512 ? 2 : 1; }
 // Q (128 VGPRs) beside a full Oᵀ (256 accumulators) spilled 2 KB per lane
 template <int D> constexpr int fwd_parts() { return D >= 512 ? 2 : 1; }
 
+// ---- work lists (causal balance) ---------------------------------------------------------
+// A causal query block's cost grows with its index, so a grid that fits in ONE round of
+// workgroups (Gemma-3 1B at B = 8: 256 forward workgroups on 256 CUs) runs as long as its
+// heaviest block — about 1.8× the mean. The forward and dQ kernels therefore take a per-head
+// work list, heaviest item first: block qb whole, or (qb >= split0) one of the two halves of its
+// key-tile range, each half writing fp32 partials that fa_gen_combine merges (forward: the
+// online-softmax (m, l) merge; dQ: a plain sum). The host picks split0 by simulating the
+// workgroup dispatch (attn_plan below). Launch order is item-major across the heads of an XCD, so
+// every XCD runs its heaviest items first (a head-major order dealt a whole second plane of
+// workgroups to CUs in head order rather than by size).
+constexpr int kMaxItems = 480;
+struct WorkList {
+  int n;       // items per head
+  int split0;  // first split block (>= number of blocks: nothing split, item i = block n-1-i)
+  int it[kMaxItems];  // block | part << 16 (part 0 whole, 1 first half, 2 second half)
+};
+
+// blockIdx.x over n_items × (zp·heads) workgroups -> (item, virtual head vh = z·heads + head):
+// virtual heads are dealt to the 8 XCDs round-robin (a head's z parts share an XCD when heads is
+// a multiple of 8), items outermost within an XCD
+__device__ __forceinline__ void item_head(int nitems, int& item, int& vh) {
+  const int nvh = gridDim.x / nitems, id = blockIdx.x;
+  const int hp = nvh >> 3, full = hp * nitems;
+  const int xcd = id & 7, slot = id >> 3;
+  if (slot < full) {
+    item = slot / hp;
+    vh = (slot - item * hp) * 8 + xcd;
+  } else {
+    const int r = id - 8 * full, nt = nvh & 7;
+    item = r / nt;
+    vh = (nvh & ~7) + (r - item * nt);
+  }
+}
+
+// item -> (block, part); the part's key tiles: [0, n) whole, [0, n/2) first, [n/2, n) second half
+__device__ __forceinline__ void item_block(const WorkList& wl, int nblk, int item, int& blk, int& part) {
+  if (wl.split0 >= nblk) {
+    blk = nblk - 1 - item;
+    part = 0;
+  } else {
+    const int e = wl.it[item];
+    blk = e & 0xffff;
+    part = e >> 16;
+  }
+}
+
+__device__ __forceinline__ void part_tiles(int part, int n, int& j0, int& j1) {
+  j0 = part == 2 ? n / 2 : 0;
+  j1 = part == 1 ? n / 2 : n;
+}
+
 template <int D, bool DROPOUT>
 __global__ void __launch_bounds__(64 * fwd_waves<D>(), (D >= 256 ? 1 : 2))
     fa_gen_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out, float* __restrict__ lse, int T, int H,
-                      int Hkv, float scale, float p_drop, uint64_t seed) {
+                      int Hkv, float scale, float p_drop, uint64_t seed, const WorkList wl, float* __restrict__ ws) {
   constexpr int NP = D / 64, NS = D / 16, ND = D / 32, NW = fwd_waves<D>();
   constexpr int BM = 32 * NW, BN = 32, TILE = BN * 128 * NP;
   // D = 256: the 32 Q fragments would not fit beside Oᵀ (128 accumulators) in registers; the
@@ -86,13 +144,15 @@ __global__ void __launch_bounds__(64 * fwd_waves<D>(), (D >= 256 ? 1 : 2))
   // each workgroup accumulates one half of Oᵀ (fwd_parts)
   constexpr bool QLDS = D == 256;
   constexpr int NDO = ND / fwd_parts<D>();
-  const int do0 = fwd_parts<D>() > 1 ? (int)blockIdx.z * NDO : 0;
   constexpr int QTILE = QLDS ? BM * 128 * NP : 16;
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE + QTILE];
   const int nqb = (T + BM - 1) / BM;
-  int qi, bh;
-  xcd_head_block(qi, bh);
-  const int qb = nqb - 1 - qi;
+  int item, vh, qb, part;
+  item_head(wl.n, item, vh);
+  item_block(wl, nqb, item, qb, part);
+  const int nbh = gridDim.x / (wl.n * fwd_parts<D>());
+  const int z = vh / nbh, bh = vh - z * nbh;
+  const int do0 = z * NDO;
   const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
   const int lane = threadIdx.x & 63, w = wave_id(), hh = lane >> 5;
   const size_t RS = (size_t)(H + 2 * Hkv) * D;
@@ -124,7 +184,8 @@ __global__ void __launch_bounds__(64 * fwd_waves<D>(), (D >= 256 ? 1 : 2))
   };
 
   const int kend = min(T, qb * BM + BM);
-  const int ntiles = (kend + BN - 1) / BN;
+  int j0, j1;
+  part_tiles(part, (kend + BN - 1) / BN, j0, j1);
   f32x16 o[NDO];
 #pragma unroll
   for (int dh = 0; dh < NDO; ++dh)
@@ -140,12 +201,12 @@ __global__ void __launch_bounds__(64 * fwd_waves<D>(), (D >= 256 ? 1 : 2))
     dma_rows<NPW>(((w & 1) == 0 ? kbase : vbase) + 64 * p0, RS, j * BN, T, dst, lane);
   };
 
-  dma(0);
+  if (j0 < j1) dma(j0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int j = 0; j < ntiles; ++j) {
+  for (int j = j0; j < j1; ++j) {
     const int kt0 = j * BN;
-    if (j + 1 < ntiles) dma(j + 1);  // buffer (j+1)&1 was released by the previous barrier
+    if (j + 1 < j1) dma(j + 1);  // buffer (j+1)&1 was released by the previous barrier
     const char* Kt = smem + (j & 1) * 2 * TILE;
     const char* Vt = Kt + TILE;
     if (kt0 <= q0 + 31 && q0 < T) {
@@ -212,6 +273,22 @@ __global__ void __launch_bounds__(64 * fwd_waves<D>(), (D >= 256 ? 1 : 2))
     __syncthreads();
   }
   l = halves_sum(l);
+  if (part != 0) {  // half of a split block: raw Oᵀ, m, l (fp32) for fa_gen_combine
+    if (qrow < T) {
+      const size_t nsr = (size_t)(nqb - wl.split0) * BM;  // split rows per head
+      const size_t r = ((size_t)(part - 1) * nbh + bh) * nsr + (qrow - wl.split0 * BM);
+      float* orow = ws + r * D;
+#pragma unroll
+      for (int j = 0; j < NDO; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<float4*>(orow + 32 * (do0 + j) + 8 * g + 4 * hh) =
+              float4{o[j][4 * g], o[j][4 * g + 1], o[j][4 * g + 2], o[j][4 * g + 3]};
+      if (hh == 0 && do0 == 0)
+        *reinterpret_cast<float2*>(ws + 2 * nbh * nsr * D + 2 * r) = float2{m, l};
+    }
+    return;
+  }
   const float inv = l > 0.f ? 1.f / l : 0.f;
   if (qrow < T) {
     bf16* orow = out + ((size_t)b * T + qrow) * H * D + (size_t)h * D;
@@ -274,12 +351,15 @@ __global__ void __launch_bounds__(128, 1)
   // workgroups (all four SIMDs) share a CU. (Keeping K / V in LDS for one workgroup per CU left
   // two SIMDs idle, spilled 72 registers and was LDS-bandwidth-bound at 87 TF.)
   constexpr int NDH = ND / kv_parts<D>();  // dKᵀ / dVᵀ column blocks of 32 owned here (D = 512: a quarter)
-  const int dh0 = kv_parts<D>() > 1 ? (int)blockIdx.z * NDH : 0;
   constexpr bool KVLDS = false;
   constexpr int KVT = BK * 128 * NP;           // 64 key rows
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + (KVLDS ? 2 * KVT : 16)];
-  int kb, bhx;
-  xcd_head_block(kb, bhx);  // key block kb ascending = heaviest first (causal)
+  // 1-D grid: key block kb ascending = heaviest first (causal) across every (column part, head)
+  int kb, vh;
+  item_head((T + BK - 1) / BK, kb, vh);
+  const int nbhx = gridDim.x / (((T + BK - 1) / BK) * kv_parts<D>());
+  const int zc = vh / nbhx, bhx = vh - zc * nbhx;
+  const int dh0 = zc * NDH;
   const int G = H / Hkv;
   const int GS = part != nullptr ? G : 1;  // workgroups per KV group (query-head split)
   const int gi = bhx % GS, bh = bhx / GS;
@@ -420,7 +500,7 @@ __global__ void __launch_bounds__(128, 1)
     __syncthreads();
   }
   if (key < T && part != nullptr) {  // fp32 partials of this query head: [gi][b·T + key][K | V][hk·D + d]
-    const int Bn = gridDim.y / (Hkv * GS);
+    const int Bn = nbhx / (Hkv * GS);
     float* prow = part + ((size_t)gi * Bn * T + (size_t)b * T + key) * (2 * Hkv * D) + (size_t)hk * D;
 #pragma unroll
     for (int j = 0; j < NDH; ++j)
@@ -466,6 +546,47 @@ __global__ void __launch_bounds__(256) fa_gen_kv_reduce(const float* __restrict_
   }
 }
 
+// Split-block partials -> the final rows. FWD: O = Σ_p o_p·2^(m_p − m) / Σ_p l_p·2^(m_p − m)
+// (bf16, head-merged) and the LSE; otherwise dQ = Σ_p dQ_p (bf16, the Q columns of dqkv).
+// ws: [2][nbh][nsr][D] fp32 (+ FWD: [2][nbh][nsr] (m, l)); split row rr of head bh is query
+// row r0 + rr. One thread per 8 columns.
+template <bool FWD>
+__global__ void __launch_bounds__(256) fa_gen_combine(const float* __restrict__ ws, bf16* __restrict__ dst,
+                                                      float* __restrict__ lse, int nbh, int nsr, int r0, int T, int H,
+                                                      int D, int64_t RS) {
+  const int c8 = D / 8;
+  const int64_t n8 = (int64_t)nbh * nsr * c8, plane = (int64_t)nbh * nsr;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = i / c8;
+    const int c = 8 * (int)(i - row * c8);
+    const int bh = (int)(row / nsr), rr = (int)(row - (int64_t)bh * nsr), q = r0 + rr;
+    if (q >= T) continue;
+    const int b = bh / H, h = bh - b * H;
+    const float* p0 = ws + row * D + c;
+    const float* p1 = p0 + plane * D;
+    const float4 a0 = *reinterpret_cast<const float4*>(p0), a1 = *reinterpret_cast<const float4*>(p0 + 4);
+    const float4 b0 = *reinterpret_cast<const float4*>(p1), b1 = *reinterpret_cast<const float4*>(p1 + 4);
+    float w0 = 1.f, w1 = 1.f;
+    bf16* o;
+    if constexpr (FWD) {
+      const float2 ml0 = reinterpret_cast<const float2*>(ws + 2 * plane * D)[row];
+      const float2 ml1 = reinterpret_cast<const float2*>(ws + 2 * plane * D)[plane + row];
+      const float m = fmaxf(ml0.x, ml1.x);
+      const float e0 = fexp2(ml0.x - m), e1 = fexp2(ml1.x - m);
+      const float l = ml0.y * e0 + ml1.y * e1;
+      const float inv = l > 0.f ? 1.f / l : 0.f;
+      w0 = e0 * inv;
+      w1 = e1 * inv;
+      if (c == 0) lse[(size_t)bh * T + q] = (m + log2f(l)) * kLn2;
+      o = dst + (((size_t)b * T + q) * H + h) * D + c;
+    } else {
+      o = dst + ((size_t)b * T + q) * RS + (size_t)h * D + c;
+    }
+    store4(o, a0.x * w0 + b0.x * w1, a0.y * w0 + b0.y * w1, a0.z * w0 + b0.z * w1, a0.w * w0 + b0.w * w1);
+    store4(o + 4, a1.x * w0 + b1.x * w1, a1.y * w0 + b1.y * w1, a1.z * w0 + b1.z * w1, a1.w * w0 + b1.w * w1);
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // dQ: grid (ceil(T/64) query blocks, heaviest first, B*H); forward-shaped: a wave keeps 32
 // query rows' Q, dO, LSE, δ and dQᵀ in registers while sweeping 32-key K/V tiles.
@@ -473,14 +594,16 @@ template <int D, bool DROPOUT>
 __global__ void __launch_bounds__(128, (D >= 256 ? 1 : 2))
     fa_gen_bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
                          const float* __restrict__ delta, bf16* __restrict__ dqkv, int T, int H, int Hkv, float scale,
-                         float p_drop, uint64_t seed) {
+                         float p_drop, uint64_t seed, const WorkList wl, float* __restrict__ ws) {
   constexpr int NP = D / 64, NS = D / 16, ND = D / 32;
   constexpr int BM = 64, BN = 32, TILE = BN * 128 * NP;
   __shared__ __attribute__((aligned(16))) char smem[2][2][TILE];
   const int nqb = (T + BM - 1) / BM;
-  int qi, bh;
-  xcd_head_block(qi, bh);
-  const int qb = nqb - 1 - qi;
+  int item, vh, qb, part;
+  item_head(wl.n, item, vh);
+  item_block(wl, nqb, item, qb, part);
+  const int nbh = gridDim.x / (wl.n * dq_parts<D>());
+  const int z = vh / nbh, bh = vh - z * nbh;
   const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
   const int lane = threadIdx.x & 63, w = wave_id(), hh = lane >> 5;
   const size_t RS = (size_t)(H + 2 * Hkv) * D;
@@ -494,7 +617,7 @@ __global__ void __launch_bounds__(128, (D >= 256 ? 1 : 2))
   const float inv_keep = DROPOUT ? 1.f / (1.f - p_drop) : 1.f;
 
   constexpr int NDQ = ND / dq_parts<D>();  // dQᵀ column blocks of 32 owned here (D = 512: a half)
-  const int dq0 = dq_parts<D>() > 1 ? (int)blockIdx.z * NDQ : 0;
+  const int dq0 = z * NDQ;
   uint4 qf[NS], dof[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
@@ -517,7 +640,8 @@ __global__ void __launch_bounds__(128, (D >= 256 ? 1 : 2))
   asm volatile("" : "+v"(l2), "+v"(dl));
 
   const int kend = min(T, qb * BM + BM);
-  const int ntiles = (kend + BN - 1) / BN;
+  int j0, j1;
+  part_tiles(part, (kend + BN - 1) / BN, j0, j1);
   f32x16 dq[NDQ];
 #pragma unroll
   for (int dh = 0; dh < NDQ; ++dh)
@@ -528,12 +652,12 @@ __global__ void __launch_bounds__(128, (D >= 256 ? 1 : 2))
     const unsigned dst = __builtin_amdgcn_readfirstlane(lds_addr_of(smem[j & 1][w]));
     dma_rows<NP>(w == 0 ? kbase : vbase, RS, j * BN, T, dst, lane);
   };
-  dma(0);
+  if (j0 < j1) dma(j0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int j = 0; j < ntiles; ++j) {
+  for (int j = j0; j < j1; ++j) {
     const int kt0 = j * BN;
-    if (j + 1 < ntiles) dma(j + 1);
+    if (j + 1 < j1) dma(j + 1);
     const char* Kt = smem[j & 1][0];
     const char* Vt = smem[j & 1][1];
     if (kt0 <= q0 + 31 && q0 < T) {
@@ -582,7 +706,17 @@ __global__ void __launch_bounds__(128, (D >= 256 ? 1 : 2))
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
-  if (qok) {
+  if (qok && part != 0) {  // half of a split block: fp32 partial dQ for fa_gen_combine
+    const size_t nsr = (size_t)(nqb - wl.split0) * BM;
+    float* prow = ws + (((size_t)(part - 1) * nbh + bh) * nsr + (qrow - wl.split0 * BM)) * D;
+#pragma unroll
+    for (int j = 0; j < NDQ; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<float4*>(prow + 32 * (dq0 + j) + 8 * g + 4 * hh) =
+            float4{dq[j][4 * g] * scale, dq[j][4 * g + 1] * scale, dq[j][4 * g + 2] * scale,
+                   dq[j][4 * g + 3] * scale};
+  } else if (qok) {
     bf16* dqrow = dqkv + ((size_t)b * T + qrow) * RS + (size_t)h * D;
 #pragma unroll
     for (int j = 0; j < NDQ; ++j)
@@ -607,6 +741,105 @@ using namespace penroz;
   else if ((D) == 512) { constexpr int DD = 512; constexpr bool DR = false; __VA_ARGS__; }       \
   else TORCH_CHECK(false, "generic flash attention supports head_dim 128, 256 and 512, got ", (D));
 
+namespace {
+
+// resident workgroups of `kernel` on the whole chip (CUs × occupancy), cached per kernel
+int chip_slots(const void* kernel, int block) {
+  static std::mutex mu;
+  static std::map<const void*, int> cache;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find(kernel);
+  if (it != cache.end()) return it->second;
+  int dev = 0, ncu = 256, nb = 1;
+  hipDeviceProp_t prop;
+  if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess) ncu = prop.multiProcessorCount;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, block, 0) != hipSuccess || nb < 1) nb = 1;
+  return cache[kernel] = nb * ncu;
+}
+
+// PENROZ_ATTN_KV_SPLIT: 0 = never split, 2 = split every block but the first (tests), else auto
+int split_mode() {
+  const char* e = std::getenv("PENROZ_ATTN_KV_SPLIT");
+  return e && *e ? std::atoi(e) : 1;
+}
+
+// Work list for nblk causal blocks of BM query rows swept in BN-key tiles, over nvh virtual heads
+// on `slots` resident workgroups. Auto: list-schedule the sorted items per XCD (each XCD runs its
+// ceil(nvh / 8) heads on slots / 8 workgroup slots, a freed slot takes the next item) for every
+// split0, and keep the one whose makespan·tile_us plus the combine pass (its fp32 traffic at
+// ~4.5 TB/s plus a launch) is smallest.
+WorkList attn_plan(int nblk, int nvh, int slots, int BM, int BN, int T, int D, double tile_us) {
+  const int mode = split_mode();
+  using Key = std::tuple<int, int, int, int, int, int, int, int, long long>;
+  static std::mutex mu;
+  static std::map<Key, WorkList> cache;
+  const Key key{nblk, nvh, slots, BM, BN, T, D, mode, (long long)(tile_us * 1e3)};
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  auto ntiles = [&](int qb) { return (std::min(T, (qb + 1) * BM) + BN - 1) / BN; };
+  auto build = [&](int s0, WorkList* wl) -> double {  // returns the makespan in tiles
+    std::vector<std::pair<int, int>> items;  // (tiles, entry)
+    for (int qb = nblk - 1; qb >= 0; --qb) {
+      const int n = ntiles(qb);
+      if (qb >= s0) {
+        items.push_back({n - n / 2, qb | 2 << 16});
+        items.push_back({n / 2, qb | 1 << 16});
+      } else {
+        items.push_back({n, qb});
+      }
+    }
+    std::stable_sort(items.begin(), items.end(), [](auto& a, auto& b) { return a.first > b.first; });
+    if (wl) {
+      wl->n = (int)items.size();
+      wl->split0 = s0;
+      for (size_t i = 0; i < items.size(); ++i) wl->it[i] = items[i].second;
+    }
+    const int hx = (nvh + 7) / 8, sx = std::max(1, slots / 8);
+    std::priority_queue<long long, std::vector<long long>, std::greater<long long>> free_at;
+    for (int i = 0; i < sx; ++i) free_at.push(0);
+    long long span = 0;
+    for (auto& [n, e] : items)
+      for (int hh = 0; hh < hx; ++hh) {
+        const long long t = free_at.top() + n;
+        free_at.pop();
+        free_at.push(t);
+        span = std::max(span, t);
+      }
+    return (double)span;
+  };
+  WorkList wl;
+  wl.n = nblk;
+  wl.split0 = nblk;
+  const bool can_split = mode != 0 && nblk >= 2 && 2 * nblk - 1 <= kMaxItems;
+  if (can_split && mode == 2) {
+    build(1, &wl);
+  } else if (can_split && (long long)nblk * nvh <= 2LL * slots) {
+    double best = build(nblk, nullptr) * tile_us;
+    int best_s = nblk;
+    for (int s0 = nblk - 1; s0 >= 1; --s0) {
+      const double rows = (double)(nblk - s0) * BM * nvh;
+      const double comb_us = rows * D * 4.0 * 4.0 / 4.5e6 + 4.0;
+      const double c = build(s0, nullptr) * tile_us + comb_us;
+      if (c < best) best = c, best_s = s0;
+    }
+    if (best_s < nblk) build(best_s, &wl);
+  }
+  return cache[key] = wl;
+}
+
+void launch_combine(bool fwd, const float* ws, bf16* dst, float* lse, int nbh, int nsr, int r0, int T, int H, int D,
+                    int64_t RS, hipStream_t stream) {
+  const int64_t n8 = (int64_t)nbh * nsr * (D / 8);
+  const dim3 g((unsigned)std::min<int64_t>((n8 + 255) / 256, 8192));
+  if (fwd)
+    hipLaunchKernelGGL(fa_gen_combine<true>, g, dim3(256), 0, stream, ws, dst, lse, nbh, nsr, r0, T, H, D, RS);
+  else
+    hipLaunchKernelGGL(fa_gen_combine<false>, g, dim3(256), 0, stream, ws, dst, lse, nbh, nsr, r0, T, H, D, RS);
+}
+
+}  // namespace
+
 void flash_attn_gen_fwd(torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int64_t H, int64_t Hkv, int64_t D,
                         double scale, double p_drop, int64_t seed) {
   TORCH_CHECK(qkv.is_cuda() && qkv.is_contiguous() && qkv.dim() == 3 && qkv.scalar_type() == torch::kBFloat16,
@@ -620,10 +853,20 @@ void flash_attn_gen_fwd(torch::Tensor qkv, torch::Tensor out, torch::Tensor lse,
   const bf16* q = reinterpret_cast<const bf16*>(qkv.data_ptr());
   bf16* o = reinterpret_cast<bf16*>(out.data_ptr());
   FA_GEN_DISPATCH(D, p_drop > 0.0, {
-    constexpr int NW = fwd_waves<DD>();
-    dim3 g((T + 32 * NW - 1) / (32 * NW), B * H, fwd_parts<DD>());
-    hipLaunchKernelGGL((fa_gen_fwd_kernel<DD, DR>), g, dim3(64 * NW), 0, stream, q, o, lse.data_ptr<float>(), T,
-                       (int)H, (int)Hkv, (float)scale, (float)p_drop, (uint64_t)seed);
+    constexpr int NW = fwd_waves<DD>(), BM = 32 * NW, ZP = fwd_parts<DD>();
+    const int nqb = (T + BM - 1) / BM, nvh = B * (int)H * ZP;
+    // measured: ~2.7 µs per 32-key tile for a 128-row, D = 256 block (Gemma-3 1B step)
+    const double tile_us = 2.7 * (BM / 128.0) * (DD + DD / ZP) / 512.0;
+    const auto kern = fa_gen_fwd_kernel<DD, DR>;
+    const WorkList wl = attn_plan(nqb, nvh, chip_slots((const void*)kern, 64 * NW), BM, 32, T, DD, tile_us);
+    torch::Tensor ws;
+    const int nsr = (nqb - wl.split0) * BM;
+    if (wl.split0 < nqb) ws = torch::empty({2 * (int64_t)B * H * nsr * (DD + 2)}, lse.options());
+    float* wsp = wl.split0 < nqb ? ws.data_ptr<float>() : nullptr;
+    hipLaunchKernelGGL(kern, dim3(wl.n * nvh), dim3(64 * NW), 0, stream, q, o, lse.data_ptr<float>(), T, (int)H,
+                       (int)Hkv, (float)scale, (float)p_drop, (uint64_t)seed, wl, wsp);
+    if (wsp)
+      launch_combine(true, wsp, o, lse.data_ptr<float>(), B * (int)H, nsr, wl.split0 * BM, T, (int)H, DD, 0, stream);
   })
 }
 
@@ -649,22 +892,37 @@ void flash_attn_gen_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out
   const bool split = G > 1 && (int64_t)B * Hkv * nkb < 1024;
   torch::Tensor part;
   if (split) part = torch::empty({(int64_t)G * B * T, 2 * Hkv * D}, qkv.options().dtype(torch::kFloat32));
-  // z: the column parts of D (dK / dV: 2 at D = 256, 4 at 512; dQ: 2 at 512)
-  dim3 gkv(nkb, B * Hkv * (split ? G : 1), D >= 512 ? 4 : (D >= 256 ? 2 : 1)), gq((T + 63) / 64, B * H, D >= 512 ? 2 : 1);
+  // 1-D grids: items (key / query blocks) × the column parts of D (dK / dV: 2 at D = 256, 4 at
+  // 512; dQ: 2 at 512) × heads
+  const int64_t nkv = (int64_t)nkb * B * Hkv * (split ? G : 1) * (D >= 512 ? 4 : (D >= 256 ? 2 : 1));
   FA_GEN_DISPATCH(D, p_drop > 0.0, {
     hipLaunchKernelGGL((fa_gen_bwd_pre_kernel<DD>), dim3(((int64_t)rows * (DD / 8) + 255) / 256), dim3(256), 0,
                        stream, d, reinterpret_cast<const bf16*>(out.data_ptr()), delta.data_ptr<float>(), B, T,
                        (int)H);
-    hipLaunchKernelGGL((fa_gen_bwd_dkdv_kernel<DD, DR>), gkv, dim3(128), 0, stream, q, d, lse.data_ptr<float>(),
-                       delta.data_ptr<float>(), g, split ? part.data_ptr<float>() : nullptr, T, (int)H, (int)Hkv,
-                       (float)scale, (float)p_drop, (uint64_t)seed);
+    hipLaunchKernelGGL((fa_gen_bwd_dkdv_kernel<DD, DR>), dim3((unsigned)nkv), dim3(128), 0, stream, q, d,
+                       lse.data_ptr<float>(), delta.data_ptr<float>(), g, split ? part.data_ptr<float>() : nullptr, T,
+                       (int)H, (int)Hkv, (float)scale, (float)p_drop, (uint64_t)seed);
     if (split) {
       const int64_t n8 = (int64_t)B * T * (2 * Hkv * DD / 8);
       hipLaunchKernelGGL(fa_gen_kv_reduce, dim3((unsigned)std::min<int64_t>((n8 + 255) / 256, 4096)), dim3(256), 0,
                          stream, part.data_ptr<float>(), g, (int64_t)B * T, (int)(2 * Hkv * DD), G,
                          (int64_t)(H + 2 * Hkv) * DD, (int64_t)H * DD);
     }
-    hipLaunchKernelGGL((fa_gen_bwd_dq_kernel<DD, DR>), gq, dim3(128), 0, stream, q, d, lse.data_ptr<float>(),
-                       delta.data_ptr<float>(), g, T, (int)H, (int)Hkv, (float)scale, (float)p_drop, (uint64_t)seed);
+    constexpr int ZQ = dq_parts<DD>();
+    const int nqb = (T + 63) / 64, nvh = B * (int)H * ZQ;
+    // measured: ~2.9 µs per 32-key tile for a 64-row, D = 256 block (Gemma-3 1B step)
+    const double tile_us = 2.9 * (DD + DD / ZQ) / 512.0;
+    const auto kq = fa_gen_bwd_dq_kernel<DD, DR>;
+    const WorkList wl = attn_plan(nqb, nvh, chip_slots((const void*)kq, 128), 64, 32, T, DD, tile_us);
+    torch::Tensor ws;
+    const int nsr = (nqb - wl.split0) * 64;
+    if (wl.split0 < nqb) ws = torch::empty({2 * (int64_t)B * H * nsr * DD}, lse.options());
+    float* wsp = wl.split0 < nqb ? ws.data_ptr<float>() : nullptr;
+    hipLaunchKernelGGL(kq, dim3(wl.n * nvh), dim3(128), 0, stream, q, d, lse.data_ptr<float>(),
+                       delta.data_ptr<float>(), g, T, (int)H, (int)Hkv, (float)scale, (float)p_drop, (uint64_t)seed,
+                       wl, wsp);
+    if (wsp)
+      launch_combine(false, wsp, g, nullptr, B * (int)H, nsr, wl.split0 * 64, T, (int)H, DD,
+                     (int64_t)(H + 2 * Hkv) * DD, stream);
   })
 }

@@ -417,6 +417,33 @@ def test_flash_gen_fwd_bwd(D, B, T, H, Hkv):
         assert rel < 0.02, f"D={D} {name} relative error {rel}"
 
 
+@pytest.mark.parametrize("D", [128, 256, 512])
+@pytest.mark.parametrize("B,T,H,Hkv", [(8, 1024, 4, 1), (1, 300, 3, 3), (2, 130, 4, 2)])
+def test_flash_gen_kv_split(monkeypatch, D, B, T, H, Hkv):
+    """Work-list split (flash_attn_gen.hip attn_plan): every block but the first swept as two
+    key-range halves with fp32 partials merged by fa_gen_combine (PENROZ_ATTN_KV_SPLIT=2) vs no
+    split (=0): both match the fp32 reference, and with dropout the two agree (same mask)."""
+    torch.manual_seed(3)
+    qkv = _qkv(B, T, H, Hkv, D, scale=1.1)
+    dout = torch.randn(B, T, H * D, device=DEV).to(torch.bfloat16)
+    x = qkv.float().requires_grad_()
+    ro, rl = A.reference_attention_lse(x, H, Hkv, D)
+    (ro * dout.float()).sum().backward()
+    res = {}
+    for mode in ("0", "2"):
+        monkeypatch.setenv("PENROZ_ATTN_KV_SPLIT", mode)
+        out, lse = A.flash_fwd(qkv, H, Hkv, D)
+        _close(out, ro.detach(), 0.02, 0.01, f"out mode {mode}")
+        _close(lse, rl.detach(), 2e-3, 1e-4, f"lse mode {mode}")
+        g = A.flash_bwd(dout, qkv, out, lse, H, Hkv, D).float()
+        rel = (g - x.grad).norm() / x.grad.norm()
+        assert rel < 0.02, f"mode {mode} grad relative error {rel}"
+        od, ld = A.flash_fwd(qkv, H, Hkv, D, 0.1, seed=9)
+        res[mode] = (od.float(), A.flash_bwd(dout, qkv, od, ld, H, Hkv, D, 0.1, seed=9).float())
+    for a, b in zip(res["0"], res["2"]):
+        assert ((a - b).norm() / b.norm()) < 1e-2
+
+
 @pytest.mark.parametrize("D", [32, 80, 96, 160, 384])
 @pytest.mark.parametrize("B,T,H,Hkv,p", [(2, 130, 4, 2, 0.0), (1, 300, 3, 3, 0.0), (2, 64, 4, 1, 0.1)])
 def test_flash_padded_head_dims(D, B, T, H, Hkv, p):
