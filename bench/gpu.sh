@@ -60,9 +60,9 @@ case $cmd in
     timeout -k 10 400 rocprofv3 --kernel-trace -d gpurun_out/$tag -o run -- "$@" > gpurun_out/$tag.log 2>&1 \
       || { tail -20 gpurun_out/$tag.log; exit 1; }
     DB=$(find gpurun_out/$tag -name 'run_results.db' | head -n1)
-    python3 bench/prof_summary.py $DB --steps $steps --top 30 > gpurun_out/${tag}_summary.txt || exit 1
+    python3 bench/prof_summary.py $DB --steps $steps --top ${PROF_TOP:-30} $PROF_ARGS > gpurun_out/${tag}_summary.txt || exit 1
     rm -rf gpurun_out/$tag
-    head -n 40 gpurun_out/${tag}_summary.txt | cut -c1-160 ;;
+    head -n ${PROF_TOP:-40} gpurun_out/${tag}_summary.txt | cut -c1-160 ;;
   pmc)
     tag=$1; kernels=$2; shift 2; [ "$1" = "--" ] && shift
     mkdir -p gpurun_out/pmc_$tag

@@ -1,0 +1,21 @@
+# Same-box A/B of the streaming-kernel defaults (non-temporal + wider grids: AdamW, GELU, gated
+# activation, GELU backward + columns) against the old settings, headline bench then Gemma-3 1B B=8.
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+OLD="PENROZ_EW_NT=0 PENROZ_EW_GRID=2048 PENROZ_ADAM_NT=0 PENROZ_ADAM_GRID=4096"
+NEW="PENROZ_EW_NT=1"
+for i in 1 2; do
+  for e in "$OLD" "$NEW"; do
+    env $e timeout -k 10 200 python bench.py --steps 20 --warmup 5 --ref-steps 0 > gpurun_out/ab.log 2>&1 \
+      || { tail -20 gpurun_out/ab.log; exit 1; }
+    echo "gpt2 [$e] $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/ab.log)"
+  done
+done
+for i in 1 2; do
+  for e in "$OLD" "$NEW"; do
+    env $e timeout -k 10 300 python bench.py --model gemma3-1b --batch 8 --steps 10 --warmup 3 --ref-steps 0 \
+      > gpurun_out/ab.log 2>&1 || { tail -20 gpurun_out/ab.log; exit 1; }
+    echo "gemma3-1b B8 [$e] $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/ab.log)"
+  done
+done

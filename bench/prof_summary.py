@@ -46,11 +46,12 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--csv", default=None)
+    ap.add_argument("--by-grid", action="store_true", help="one row per (kernel, workgroup count)")
     a = ap.parse_args(argv)
     src = load_db(a.path) if a.path.endswith(".db") else load_csv(a.path)
     agg = collections.defaultdict(lambda: [0, 0.0, 0, 0, 0, 0])
     for name, dur, wgs, vg, ag, lds in src:
-        k = short(name)
+        k = f"{short(name)} [{wgs}]" if a.by_grid else short(name)
         e = agg[k]
         e[0] += 1
         e[1] += dur

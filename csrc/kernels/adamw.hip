@@ -13,6 +13,7 @@
 #include "common.h"
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
+#include <cstdlib>
 
 namespace penroz {
 
@@ -32,29 +33,42 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
   p -= h.step_size * m / denom;
 }
 
+// NT: 0 plain, 1 non-temporal loads and stores (default), 2 non-temporal stores only; every
+// operand is streamed once per step (PENROZ_ADAM_NT picks, see flat_step)
+template <int NT>
+__device__ __forceinline__ float4_t ld4(const float4_t* a) {
+  if constexpr (NT == 1) return __builtin_nontemporal_load(a);
+  else return *a;
+}
+template <int NT, typename V>
+__device__ __forceinline__ void st(V* a, V x) {
+  if constexpr (NT != 0) __builtin_nontemporal_store(x, a);
+  else *a = x;
+}
+
+template <int NT>
 __global__ void __launch_bounds__(256) adam_flat_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                         float* __restrict__ m, float* __restrict__ v,
                                                         bf16* __restrict__ shadow, int64_t n, AdamHyper h) {
   const int64_t n4 = n / 4;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-    float4_t pv = reinterpret_cast<float4_t*>(p)[i];
-    const float4_t gv = reinterpret_cast<const float4_t*>(g)[i];
-    float4_t mv = reinterpret_cast<float4_t*>(m)[i];
-    float4_t vv = reinterpret_cast<float4_t*>(v)[i];
+    float4_t pv = ld4<NT>(reinterpret_cast<float4_t*>(p) + i);
+    const float4_t gv = ld4<NT>(reinterpret_cast<const float4_t*>(g) + i);
+    float4_t mv = ld4<NT>(reinterpret_cast<float4_t*>(m) + i);
+    float4_t vv = ld4<NT>(reinterpret_cast<float4_t*>(v) + i);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       float pk = pv[k], mk = mv[k], vk = vv[k];
       adam_elem(pk, gv[k], mk, vk, h);
       pv[k] = pk; mv[k] = mk; vv[k] = vk;
     }
-    reinterpret_cast<float4_t*>(p)[i] = pv;
-    reinterpret_cast<float4_t*>(m)[i] = mv;
-    reinterpret_cast<float4_t*>(v)[i] = vv;
+    st<NT>(reinterpret_cast<float4_t*>(p) + i, pv);
+    st<NT>(reinterpret_cast<float4_t*>(m) + i, mv);
+    st<NT>(reinterpret_cast<float4_t*>(v) + i, vv);
     if (shadow) {
-      uint2 u;
-      u.x = pack_bf16x2(pv[0], pv[1]);
-      u.y = pack_bf16x2(pv[2], pv[3]);
-      reinterpret_cast<uint2*>(shadow)[i] = u;
+      typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+      const u32x2 u = {pack_bf16x2(pv[0], pv[1]), pack_bf16x2(pv[2], pv[3])};
+      st<NT>(reinterpret_cast<u32x2*>(shadow) + i, u);
     }
   }
   // scalar tail
@@ -127,8 +141,15 @@ static void flat_step(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::
     sp = reinterpret_cast<bf16*>(shadow->data_ptr());
   }
   const int64_t n = p.numel();
-  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n / 4 + 255) / 256, 4096));
-  hipLaunchKernelGGL(adam_flat_kernel, dim3(grid), dim3(256), 0, at::hip::getCurrentHIPStream(), p.data_ptr<float>(),
+  const char* ge = std::getenv("PENROZ_ADAM_GRID");
+  // one float4 per thread, non-temporal loads and stores by default: 1.36x (GPT-2 124M flat size)
+  // and 1.17x (Gemma-3 1B) over a 4096-workgroup grid-stride loop (profiles/ew_ab_r4.log)
+  const int64_t gmax = ge && *ge ? std::max(1, std::atoi(ge)) : (int64_t)1 << 30;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n / 4 + 255) / 256, gmax));
+  const char* ne = std::getenv("PENROZ_ADAM_NT");
+  const int nt = ne && *ne ? std::atoi(ne) : 1;
+  auto kern = nt == 1 ? adam_flat_kernel<1> : (nt == 2 ? adam_flat_kernel<2> : adam_flat_kernel<0>);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, at::hip::getCurrentHIPStream(), p.data_ptr<float>(),
                      g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), sp, n, h);
 }
 

@@ -3,13 +3,14 @@
 // quantisation, and on-device tensor statistics (moments, min/max, density histogram).
 //
 // All streams use 16-B per-lane vectors (8 bf16 or 4 fp32), grid-stride loops capped at
-// ~2048 workgroups (CDNA HIP guide, Guideline 11/13). Column-sum fusions keep each thread's
+// 8192 workgroups for the large passes (2048 elsewhere; CDNA HIP guide, Guideline 11/13). Column-sum fusions keep each thread's
 // 8 columns fixed while it walks rows, so the partial sums live in registers; a workgroup
 // reduces its 4 waves in LDS and writes one partial row, finished by a tiny reduction.
 #include "common.h"
 #include "deferred.h"
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
+#include <cstdlib>
 
 namespace penroz {
 
@@ -21,34 +22,34 @@ __device__ __forceinline__ float act_grad_f(float x, int kind) {
   return gelu_grad_f(x, kind);
 }
 
-template <typename T>
+template <typename T, bool NT = false>
 __global__ void __launch_bounds__(256) gelu_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t n8,
                                                        int approx) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
     float v[8];
-    Vec8<T>::load(x + 8 * i, v);
+    load8<NT>(x + 8 * i, v);
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = gelu_f(v[k], approx);
-    Vec8<T>::store(y + 8 * i, v);
+    store8<NT>(y + 8 * i, v);
   }
 }
 
-template <typename T>
+template <typename T, bool NT = false>
 __global__ void __launch_bounds__(256) gelu_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                        T* __restrict__ dx, int64_t n8, int approx) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
     float g[8], v[8];
-    Vec8<T>::load(dy + 8 * i, g);
-    Vec8<T>::load(x + 8 * i, v);
+    load8<NT>(dy + 8 * i, g);
+    load8<NT>(x + 8 * i, v);
 #pragma unroll
     for (int k = 0; k < 8; ++k) g[k] *= gelu_grad_f(v[k], approx);
-    Vec8<T>::store(dx + 8 * i, g);
+    store8<NT>(dx + 8 * i, g);
   }
 }
 
 // MODE 0: colsum of x.  MODE 1: dx = dy*gelu'(x) written to out, colsum of dx.
 // grid = (F/512 column tiles, R row splits); block 256 = 4 waves; lane -> 8 columns.
-template <int MODE, typename T>
+template <int MODE, typename T, bool NT = false>
 __global__ void __launch_bounds__(256) rows_colsum_kernel(const T* __restrict__ a, const T* __restrict__ x,
                                                           T* __restrict__ out, float* __restrict__ part, int N, int F,
                                                           int approx) {
@@ -64,14 +65,14 @@ __global__ void __launch_bounds__(256) rows_colsum_kernel(const T* __restrict__ 
     for (int r = r0 + wid; r < r1; r += 4) {
       const size_t off = (size_t)r * F + col;
       float v[8];
-      Vec8<T>::load(a + off, v);
+      load8<NT>(a + off, v);
       if constexpr (MODE == 1) {
         float xv[8];
-        Vec8<T>::load(x + off, xv);
+        load8<NT>(x + off, xv);
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] = to_f(from_f<T>(v[k] * gelu_grad_f(xv[k], approx)));
         // v now holds the *rounded* values: dbias matches the bf16 gradient the GEMMs see
-        Vec8<T>::store(out + off, v);
+        store8<NT>(out + off, v);
       }
 #pragma unroll
       for (int k = 0; k < 8; ++k) acc[k] += v[k];
@@ -87,72 +88,72 @@ __global__ void __launch_bounds__(256) rows_colsum_kernel(const T* __restrict__ 
 }
 
 // ------------------------------------------------------------------------------ gated MLP act
-template <typename T>
+template <typename T, bool NT = false>
 __global__ void __launch_bounds__(256) gated_fwd_kernel(const T* __restrict__ g, const T* __restrict__ u,
                                                         T* __restrict__ y, int64_t n8, int kind) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
     float gv[8], uv[8];
-    Vec8<T>::load(g + 8 * i, gv);
-    Vec8<T>::load(u + 8 * i, uv);
+    load8<NT>(g + 8 * i, gv);
+    load8<NT>(u + 8 * i, uv);
 #pragma unroll
     for (int k = 0; k < 8; ++k) gv[k] = act_f(gv[k], kind) * uv[k];
-    Vec8<T>::store(y + 8 * i, gv);
+    store8<NT>(y + 8 * i, gv);
   }
 }
 
 // decode: gate and up halves of one fused [N, 2I] projection -> act(gate) * up [N, I]
-template <typename T>
+template <typename T, bool NT = false>
 __global__ void __launch_bounds__(256) gated_packed_kernel(const T* __restrict__ gu, T* __restrict__ y, int64_t n8,
                                                            int I8, int kind) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = i / I8, c = i - r * I8;
     float gv[8], uv[8];
-    Vec8<T>::load(gu + 8 * (r * 2 * I8 + c), gv);
-    Vec8<T>::load(gu + 8 * (r * 2 * I8 + I8 + c), uv);
+    load8<NT>(gu + 8 * (r * 2 * I8 + c), gv);
+    load8<NT>(gu + 8 * (r * 2 * I8 + I8 + c), uv);
 #pragma unroll
     for (int k = 0; k < 8; ++k) gv[k] = act_f(gv[k], kind) * uv[k];
-    Vec8<T>::store(y + 8 * i, gv);
+    store8<NT>(y + 8 * i, gv);
   }
 }
 
-template <typename T>
+template <typename T, bool NT = false>
 __global__ void __launch_bounds__(256) gated_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ g,
                                                         const T* __restrict__ u, T* __restrict__ dg,
                                                         T* __restrict__ du, int64_t n8, int kind) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
     float d[8], gv[8], uv[8], o1[8], o2[8];
-    Vec8<T>::load(dy + 8 * i, d);
-    Vec8<T>::load(g + 8 * i, gv);
-    Vec8<T>::load(u + 8 * i, uv);
+    load8<NT>(dy + 8 * i, d);
+    load8<NT>(g + 8 * i, gv);
+    load8<NT>(u + 8 * i, uv);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       o1[k] = d[k] * uv[k] * act_grad_f(gv[k], kind);
       o2[k] = d[k] * act_f(gv[k], kind);
     }
-    Vec8<T>::store(dg + 8 * i, o1);
-    Vec8<T>::store(du + 8 * i, o2);
+    store8<NT>(dg + 8 * i, o1);
+    store8<NT>(du + 8 * i, o2);
   }
 }
 
 // packed form of the backward: gu = [gate | up] per row (I8 chunks of 8 each), dgu likewise —
 // the layout one GEMM over the concatenated [gate; up] weight consumes (fused Gemma executor)
-template <typename T>
+template <typename T, bool NT = false>
 __global__ void __launch_bounds__(256) gated_bwd_packed_kernel(const T* __restrict__ dy, const T* __restrict__ gu,
                                                                T* __restrict__ dgu, int64_t n8, int I8, int kind) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = i / I8, c = i - r * I8;
     const int64_t go = 8 * (r * 2 * I8 + c), uo = go + 8 * (int64_t)I8;
     float d[8], gv[8], uv[8], o1[8], o2[8];
-    Vec8<T>::load(dy + 8 * i, d);
-    Vec8<T>::load(gu + go, gv);
-    Vec8<T>::load(gu + uo, uv);
+    load8<NT>(dy + 8 * i, d);
+    load8<NT>(gu + go, gv);
+    load8<NT>(gu + uo, uv);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       o1[k] = d[k] * uv[k] * act_grad_f(gv[k], kind);
       o2[k] = d[k] * act_f(gv[k], kind);
     }
-    Vec8<T>::store(dgu + go, o1);
-    Vec8<T>::store(dgu + uo, o2);
+    store8<NT>(dgu + go, o1);
+    store8<NT>(dgu + uo, o2);
   }
 }
 
@@ -429,6 +430,20 @@ using namespace penroz;
   else if ((t) == torch::kFloat16) { using NAME = __half; __VA_ARGS__; }            \
   else TORCH_CHECK(false, "unsupported dtype");
 
+// PENROZ_EW_NT (non-temporal loads / stores, default on) and PENROZ_EW_GRID (workgroup cap of the
+// grid-stride launches, default 8192) for the large streaming passes: GELU, gated activation,
+// GELU backward + bias columns. Against the old plain / 2048 setting (profiles/ew_ab_r4.log):
+// gelu_fwd 180-198 -> 146-152 us, GELU backward + columns 292 -> 246 us (GPT-2 shapes), gated
+// forward 68 -> 58 us, gated backward 129 -> 109 us (Gemma-3 1B shapes).
+static bool ew_nt() {
+  const char* e = std::getenv("PENROZ_EW_NT");
+  return e && *e ? std::atoi(e) != 0 : true;
+}
+static int ew_cap() {
+  const char* e = std::getenv("PENROZ_EW_GRID");
+  return e && *e ? std::max(1, std::atoi(e)) : 8192;
+}
+
 static inline int grid_for(int64_t work, int block = 256, int cap = 2048) {
   int64_t g = (work + block - 1) / block;
   return (int)std::max<int64_t>(1, std::min<int64_t>(g, cap));
@@ -447,7 +462,7 @@ void gelu_fwd(torch::Tensor x, int64_t approx, torch::Tensor y) {
   const int64_t n8 = x.numel() / 8;
   auto stream = at::hip::getCurrentHIPStream();
   FOR_FLOAT_TYPES(x.scalar_type(), T,
-    hipLaunchKernelGGL(gelu_fwd_kernel<T>, dim3(grid_for(n8)), dim3(256), 0, stream,
+    hipLaunchKernelGGL((ew_nt() ? gelu_fwd_kernel<T, true> : gelu_fwd_kernel<T, false>), dim3(grid_for(n8, 256, ew_cap())), dim3(256), 0, stream,
                        reinterpret_cast<const T*>(x.data_ptr()), reinterpret_cast<T*>(y.data_ptr()), n8, (int)approx))
 }
 
@@ -458,7 +473,8 @@ static void colsum_impl(const torch::Tensor& a, const torch::Tensor* x, torch::T
   TORCH_CHECK(dst.scalar_type() == torch::kFloat32 && dst.numel() == F && dst.is_contiguous());
   if (N == 0) return;
   const int ctiles = (F + 511) / 512;
-  int R = std::max(1, std::min(N / 16, 2048 / ctiles));
+  int R = std::max(1, std::min(N / 16, ew_cap() / ctiles));
+  const bool nt = ew_nt();
   auto part = torch::empty({R, F}, a.options().dtype(torch::kFloat32));
   auto stream = at::hip::getCurrentHIPStream();
   FOR_FLOAT_TYPES(a.scalar_type(), T, {
@@ -466,10 +482,10 @@ static void colsum_impl(const torch::Tensor& a, const torch::Tensor* x, torch::T
     const T* xp = x ? reinterpret_cast<const T*>(x->data_ptr()) : nullptr;
     T* op = out ? reinterpret_cast<T*>(out->data_ptr()) : nullptr;
     if (mode == 0)
-      hipLaunchKernelGGL((rows_colsum_kernel<0, T>), dim3(ctiles, R), dim3(256), 0, stream, ap, xp, op,
+      hipLaunchKernelGGL((nt ? rows_colsum_kernel<0, T, true> : rows_colsum_kernel<0, T, false>), dim3(ctiles, R), dim3(256), 0, stream, ap, xp, op,
                          part.data_ptr<float>(), N, F, approx);
     else
-      hipLaunchKernelGGL((rows_colsum_kernel<1, T>), dim3(ctiles, R), dim3(256), 0, stream, ap, xp, op,
+      hipLaunchKernelGGL((nt ? rows_colsum_kernel<1, T, true> : rows_colsum_kernel<1, T, false>), dim3(ctiles, R), dim3(256), 0, stream, ap, xp, op,
                          part.data_ptr<float>(), N, F, approx);
   })
   float* outs[1] = {dst.data_ptr<float>()};
@@ -491,7 +507,7 @@ void gelu_bwd(torch::Tensor dy, torch::Tensor x, int64_t approx, c10::optional<t
   }
   const int64_t n8 = x.numel() / 8;
   FOR_FLOAT_TYPES(x.scalar_type(), T,
-    hipLaunchKernelGGL(gelu_bwd_kernel<T>, dim3(grid_for(n8)), dim3(256), 0, stream,
+    hipLaunchKernelGGL((ew_nt() ? gelu_bwd_kernel<T, true> : gelu_bwd_kernel<T, false>), dim3(grid_for(n8, 256, ew_cap())), dim3(256), 0, stream,
                        reinterpret_cast<const T*>(dy.data_ptr()), reinterpret_cast<const T*>(x.data_ptr()),
                        reinterpret_cast<T*>(out.data_ptr()), n8, (int)approx))
 }
@@ -508,7 +524,7 @@ torch::Tensor gated_act_fwd(torch::Tensor g, torch::Tensor u, int64_t kind) {
   const int64_t n8 = g.numel() / 8;
   auto stream = at::hip::getCurrentHIPStream();
   FOR_FLOAT_TYPES(g.scalar_type(), T,
-    hipLaunchKernelGGL(gated_fwd_kernel<T>, dim3(grid_for(n8)), dim3(256), 0, stream,
+    hipLaunchKernelGGL((ew_nt() ? gated_fwd_kernel<T, true> : gated_fwd_kernel<T, false>), dim3(grid_for(n8, 256, ew_cap())), dim3(256), 0, stream,
                        reinterpret_cast<const T*>(g.data_ptr()), reinterpret_cast<const T*>(u.data_ptr()),
                        reinterpret_cast<T*>(y.data_ptr()), n8, (int)kind))
   return y;
@@ -531,7 +547,7 @@ torch::Tensor gated_act_packed(torch::Tensor gu, int64_t kind, c10::optional<tor
   if (n8 == 0) return y;
   auto stream = at::hip::getCurrentHIPStream();
   FOR_FLOAT_TYPES(gu.scalar_type(), T,
-    hipLaunchKernelGGL(gated_packed_kernel<T>, dim3(grid_for(n8)), dim3(256), 0, stream,
+    hipLaunchKernelGGL((ew_nt() ? gated_packed_kernel<T, true> : gated_packed_kernel<T, false>), dim3(grid_for(n8, 256, ew_cap())), dim3(256), 0, stream,
                        reinterpret_cast<const T*>(gu.data_ptr()), reinterpret_cast<T*>(y.data_ptr()), n8, (int)(I / 8),
                        (int)kind))
   return y;
@@ -545,7 +561,7 @@ std::vector<torch::Tensor> gated_act_bwd(torch::Tensor dy, torch::Tensor g, torc
   const int64_t n8 = g.numel() / 8;
   auto stream = at::hip::getCurrentHIPStream();
   FOR_FLOAT_TYPES(g.scalar_type(), T,
-    hipLaunchKernelGGL(gated_bwd_kernel<T>, dim3(grid_for(n8)), dim3(256), 0, stream,
+    hipLaunchKernelGGL((ew_nt() ? gated_bwd_kernel<T, true> : gated_bwd_kernel<T, false>), dim3(grid_for(n8, 256, ew_cap())), dim3(256), 0, stream,
                        reinterpret_cast<const T*>(dy.data_ptr()), reinterpret_cast<const T*>(g.data_ptr()),
                        reinterpret_cast<const T*>(u.data_ptr()), reinterpret_cast<T*>(dg.data_ptr()),
                        reinterpret_cast<T*>(du.data_ptr()), n8, (int)kind))
@@ -564,7 +580,7 @@ void gated_act_bwd_packed(torch::Tensor dy, torch::Tensor gu, torch::Tensor dgu,
   const int64_t I = dy.size(1), n8 = dy.numel() / 8;
   auto stream = at::hip::getCurrentHIPStream();
   FOR_FLOAT_TYPES(gu.scalar_type(), T,
-    hipLaunchKernelGGL(gated_bwd_packed_kernel<T>, dim3(grid_for(n8)), dim3(256), 0, stream,
+    hipLaunchKernelGGL((ew_nt() ? gated_bwd_packed_kernel<T, true> : gated_bwd_packed_kernel<T, false>), dim3(grid_for(n8, 256, ew_cap())), dim3(256), 0, stream,
                        reinterpret_cast<const T*>(dy.data_ptr()), reinterpret_cast<const T*>(gu.data_ptr()),
                        reinterpret_cast<T*>(dgu.data_ptr()), n8, (int)(I / 8), (int)kind))
 }
