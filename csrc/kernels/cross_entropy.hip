@@ -16,6 +16,7 @@
 #include <type_traits>
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
+#include <cstdlib>
 
 namespace penroz {
 
@@ -32,7 +33,8 @@ __device__ __forceinline__ float block_reduce(float v, float* sh, bool is_max) {
   return r;
 }
 
-template <int CPT, typename T>
+// NT: non-temporal row loads and gradient stores (PENROZ_CE_NT, see cross_entropy_fwd_bwd)
+template <int CPT, typename T, bool NT = false>
 __global__ void __launch_bounds__(kCEThreads) ce_kernel(T* __restrict__ logits, const int64_t* __restrict__ targets,
                                                         float* __restrict__ loss, int V, int ld, float scale,
                                                         int64_t ignore_index, T* __restrict__ gout) {
@@ -56,7 +58,12 @@ __global__ void __launch_bounds__(kCEThreads) ce_kernel(T* __restrict__ logits, 
       const int c = 8 * (t + kCEThreads * k);
       u[k] = uint4{0xff80ff80u, 0xff80ff80u, 0xff80ff80u, 0xff80ff80u};  // bf16 -inf pairs
       if (c < V) {
-        u[k] = *reinterpret_cast<const uint4*>(rp + c);
+        if constexpr (NT) {
+          const u32x4_t r = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(rp + c));
+          u[k] = uint4{r.x, r.y, r.z, r.w};
+        } else {
+          u[k] = *reinterpret_cast<const uint4*>(rp + c);
+        }
         if (c + 8 > V) {  // the row's last, partial chunk: elements past V become -inf
           uint32_t w[4] = {u[k].x, u[k].y, u[k].z, u[k].w};
 #pragma unroll
@@ -105,7 +112,7 @@ __global__ void __launch_bounds__(kCEThreads) ce_kernel(T* __restrict__ logits, 
           g[2 * q] = fmaf(__expf(__uint_as_float(w[q] << 16) - m), ps, c + 2 * q == tgt ? -sc : 0.f);
           g[2 * q + 1] = fmaf(__expf(__uint_as_float(w[q] & 0xffff0000u) - m), ps, c + 2 * q + 1 == tgt ? -sc : 0.f);
         }
-        Vec8<T>::store(gp + c, g);
+        store8<NT>(gp + c, g);
       }
     }
     return;
@@ -116,7 +123,7 @@ __global__ void __launch_bounds__(kCEThreads) ce_kernel(T* __restrict__ logits, 
   for (int k = 0; k < CPT; ++k) {
     const int c = 8 * (t + kCEThreads * k);
     if (c < V) {
-      Vec8<T>::load(rp + c, v[k]);
+      load8<NT>(rp + c, v[k]);
       if (c + 8 > V) {  // the row's last, partial chunk
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[k][j] = c + j < V ? v[k][j] : -INFINITY;
@@ -155,13 +162,13 @@ __global__ void __launch_bounds__(kCEThreads) ce_kernel(T* __restrict__ logits, 
       float g[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) g[j] = fmaf(v[k][j], ps, c + j == tgt ? -sc : 0.f);
-      Vec8<T>::store(gp + c, g);
+      store8<NT>(gp + c, g);
     }
   }
 }
 
 // Wide-V fallback (more than 8 chunks per thread): three streamed passes through L2.
-template <typename T>
+template <typename T, bool NT = false>
 __global__ void __launch_bounds__(kCEThreads) ce_loop_kernel(T* __restrict__ logits,
                                                              const int64_t* __restrict__ targets,
                                                              float* __restrict__ loss, int V, int ld, float scale,
@@ -203,7 +210,7 @@ __global__ void __launch_bounds__(kCEThreads) ce_loop_kernel(T* __restrict__ log
     Vec8<T>::load(rp + c, v);
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = c + j < V ? (__expf(v[j] - lse) - (c + j == tgt ? 1.f : 0.f)) * sc : 0.f;
-    Vec8<T>::store(gp + c, v);
+    store8<NT>(gp + c, v);  // (the first pass keeps plain loads: the second reads the row again)
   }
 }
 
@@ -240,6 +247,8 @@ torch::Tensor cross_entropy_fwd_bwd(torch::Tensor logits, torch::Tensor targets,
   }
   auto stream = at::hip::getCurrentHIPStream();
   const int chunks = ((V + 7) / 8 + kCEThreads - 1) / kCEThreads;
+  const char* ne = std::getenv("PENROZ_CE_NT");
+  const bool nt = ne && *ne ? std::atoi(ne) != 0 : true;  // default on: GPT-2 64.52 / 64.82 -> 64.44 / 64.51 ms, Gemma neutral (profiles/ew_ab_r4.log)
   auto launch = [&](auto tag) {
     using T = decltype(tag);
     T* lp = reinterpret_cast<T*>(logits.data_ptr());
@@ -247,17 +256,18 @@ torch::Tensor cross_entropy_fwd_bwd(torch::Tensor logits, torch::Tensor targets,
     float* op = loss.data_ptr<float>();
     const float sc = (float)scale;
     T* gp = reinterpret_cast<T*>(gptr);
-    switch (chunks) {
-      case 1: hipLaunchKernelGGL((ce_kernel<1, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index, gp); break;
-      case 2: hipLaunchKernelGGL((ce_kernel<2, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index, gp); break;
-      case 3: hipLaunchKernelGGL((ce_kernel<3, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index, gp); break;
-      case 4: hipLaunchKernelGGL((ce_kernel<4, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index, gp); break;
-      case 5: hipLaunchKernelGGL((ce_kernel<5, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index, gp); break;
-      case 6: hipLaunchKernelGGL((ce_kernel<6, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index, gp); break;
-      case 7: hipLaunchKernelGGL((ce_kernel<7, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index, gp); break;
-      case 8: hipLaunchKernelGGL((ce_kernel<8, T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index, gp); break;
-      default: hipLaunchKernelGGL((ce_loop_kernel<T>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index, gp);
-    }
+    auto go = [&](auto nt_tag) {
+      constexpr bool NT = decltype(nt_tag)::value;
+      switch (chunks) {
+#define PZ_CE_CASE(K) \
+        case K: hipLaunchKernelGGL((ce_kernel<K, T, NT>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index, gp); break;
+        PZ_CE_CASE(1) PZ_CE_CASE(2) PZ_CE_CASE(3) PZ_CE_CASE(4) PZ_CE_CASE(5) PZ_CE_CASE(6) PZ_CE_CASE(7) PZ_CE_CASE(8)
+#undef PZ_CE_CASE
+        default: hipLaunchKernelGGL((ce_loop_kernel<T, NT>), dim3(N), dim3(kCEThreads), 0, stream, lp, tp, op, V, ld, sc, ignore_index, gp);
+      }
+    };
+    if (nt) go(std::true_type{});
+    else go(std::false_type{});
   };
   if (logits.scalar_type() == torch::kBFloat16) launch(bf16{});
   else if (logits.scalar_type() == torch::kFloat32) launch(float{});

@@ -28,6 +28,7 @@
 #include "deferred.h"
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
+#include <cstdlib>
 
 namespace penroz {
 
@@ -38,13 +39,26 @@ struct RowF {  // one row's fp32 values owned by a lane: columns 4(lane + 64j) .
   float v[NCH][4];
 };
 
-template <int NCH>
+// NT: non-temporal row loads / stores (rows are streamed once; the weight loads stay plain)
+typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+template <bool NT, typename V>
+__device__ __forceinline__ V ldv(const V* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <bool NT, typename V>
+__device__ __forceinline__ void stv(V* p, V x) {
+  if constexpr (NT) __builtin_nontemporal_store(x, p);
+  else *p = x;
+}
+
+template <int NCH, bool NT = false>
 __device__ __forceinline__ void ld_f32(RowF<NCH>& r, const float* p, int lane, int C) {
 #pragma unroll
   for (int j = 0; j < NCH; ++j) {
     const int c = 4 * (lane + 64 * j);
     if (c < C) {
-      const float4_t t = *reinterpret_cast<const float4_t*>(p + c);
+      const float4_t t = ldv<NT>(reinterpret_cast<const float4_t*>(p + c));
       r.v[j][0] = t[0]; r.v[j][1] = t[1]; r.v[j][2] = t[2]; r.v[j][3] = t[3];
     } else {
       r.v[j][0] = r.v[j][1] = r.v[j][2] = r.v[j][3] = 0.f;
@@ -52,13 +66,13 @@ __device__ __forceinline__ void ld_f32(RowF<NCH>& r, const float* p, int lane, i
   }
 }
 
-template <int NCH>
+template <int NCH, bool NT = false>
 __device__ __forceinline__ void ld_bf16(RowF<NCH>& r, const bf16* p, int lane, int C) {
 #pragma unroll
   for (int j = 0; j < NCH; ++j) {
     const int c = 4 * (lane + 64 * j);
     if (c < C) {
-      const uint2 u = *reinterpret_cast<const uint2*>(p + c);
+      const u32x2_t u = ldv<NT>(reinterpret_cast<const u32x2_t*>(p + c));
       r.v[j][0] = __uint_as_float(u.x << 16); r.v[j][1] = __uint_as_float(u.x & 0xffff0000u);
       r.v[j][2] = __uint_as_float(u.y << 16); r.v[j][3] = __uint_as_float(u.y & 0xffff0000u);
     } else {
@@ -67,22 +81,23 @@ __device__ __forceinline__ void ld_bf16(RowF<NCH>& r, const bf16* p, int lane, i
   }
 }
 
-template <int NCH>
+template <int NCH, bool NT = false>
 __device__ __forceinline__ void st_f32(float* p, const RowF<NCH>& r, int lane, int C) {
 #pragma unroll
   for (int j = 0; j < NCH; ++j) {
     const int c = 4 * (lane + 64 * j);
-    if (c < C) *reinterpret_cast<float4_t*>(p + c) = float4_t{r.v[j][0], r.v[j][1], r.v[j][2], r.v[j][3]};
+    if (c < C) stv<NT>(reinterpret_cast<float4_t*>(p + c), float4_t{r.v[j][0], r.v[j][1], r.v[j][2], r.v[j][3]});
   }
 }
 
-template <int NCH>
+template <int NCH, bool NT = false>
 __device__ __forceinline__ void st_bf16(bf16* p, const RowF<NCH>& r, int lane, int C) {
 #pragma unroll
   for (int j = 0; j < NCH; ++j) {
     const int c = 4 * (lane + 64 * j);
     if (c < C)
-      *reinterpret_cast<uint2*>(p + c) = uint2{pack_bf16x2(r.v[j][0], r.v[j][1]), pack_bf16x2(r.v[j][2], r.v[j][3])};
+      stv<NT>(reinterpret_cast<u32x2_t*>(p + c),
+              u32x2_t{pack_bf16x2(r.v[j][0], r.v[j][1]), pack_bf16x2(r.v[j][2], r.v[j][3])});
   }
 }
 
@@ -104,7 +119,7 @@ __device__ __forceinline__ void ld_w(RowF<NCH>& r, const float* w, int lane, int
 
 }  // namespace
 
-template <int NCH>
+template <int NCH, bool NT = false>
 __global__ void __launch_bounds__(256) gm_combine_fwd_kernel(int mode, const float* __restrict__ x,
                                                              const bf16* __restrict__ a, const float* __restrict__ w1,
                                                              const float* __restrict__ w2, float eps1, float eps2,
@@ -116,10 +131,10 @@ __global__ void __launch_bounds__(256) gm_combine_fwd_kernel(int mode, const flo
   for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < N; row += gridDim.x * 4) {
     const size_t base = (size_t)row * C;
     RowF<NCH> h;
-    ld_f32<NCH>(h, x + base, lane, C);
+    ld_f32<NCH, NT>(h, x + base, lane, C);
     if (mode != 3) {
       RowF<NCH> av, wv;
-      ld_bf16<NCH>(av, a + base, lane, C);
+      ld_bf16<NCH, NT>(av, a + base, lane, C);
       if (mode == 1) {  // h = x + RMS(a)·w1
         ld_w<NCH>(wv, w1, lane, C);
         const float r1 = rsqrtf(sumsq<NCH>(av) * inv_c + eps1);
@@ -134,7 +149,7 @@ __global__ void __launch_bounds__(256) gm_combine_fwd_kernel(int mode, const flo
 #pragma unroll
           for (int k = 0; k < 4; ++k) h.v[j][k] += av.v[j][k];
         if (mode == 0) {  // s = x + a (kept for the backward); h = RMS(s)·w1
-          st_f32<NCH>(s_save + base, h, lane, C);
+          st_f32<NCH, NT>(s_save + base, h, lane, C);
           ld_w<NCH>(wv, w1, lane, C);
           const float r1 = rsqrtf(sumsq<NCH>(h) * inv_c + eps1);
           if (lane == 0) r1_out[row] = r1;
@@ -144,7 +159,7 @@ __global__ void __launch_bounds__(256) gm_combine_fwd_kernel(int mode, const flo
             for (int k = 0; k < 4; ++k) h.v[j][k] *= r1 * wv.v[j][k];
         }
       }
-      st_f32<NCH>(h_out + base, h, lane, C);
+      st_f32<NCH, NT>(h_out + base, h, lane, C);
     }
     RowF<NCH> wv2;
     ld_w<NCH>(wv2, w2, lane, C);
@@ -154,12 +169,12 @@ __global__ void __launch_bounds__(256) gm_combine_fwd_kernel(int mode, const flo
     for (int j = 0; j < NCH; ++j)
 #pragma unroll
       for (int k = 0; k < 4; ++k) h.v[j][k] *= r2 * wv2.v[j][k];
-    st_bf16<NCH>(y_out + base, h, lane, C);
+    st_bf16<NCH, NT>(y_out + base, h, lane, C);
   }
 }
 
 // part: fp32 [2][gridDim.x][C] — this workgroup's dw1 (row block 0) and dw2 (row block 1) sums
-template <int NCH>
+template <int NCH, bool NT = false>
 __global__ void __launch_bounds__(256) gm_combine_bwd_kernel(int mode, const bf16* __restrict__ dy,
                                                              const float* __restrict__ dh_in,
                                                              const float* __restrict__ h_save,
@@ -182,8 +197,8 @@ __global__ void __launch_bounds__(256) gm_combine_bwd_kernel(int mode, const bf1
   for (int row = gw; row < N; row += nw) {
     const size_t base = (size_t)row * C;
     RowF<NCH> g, hv, wv;
-    ld_bf16<NCH>(g, dy + base, lane, C);
-    ld_f32<NCH>(hv, h_save + base, lane, C);
+    ld_bf16<NCH, NT>(g, dy + base, lane, C);
+    ld_f32<NCH, NT>(hv, h_save + base, lane, C);
     ld_w<NCH>(wv, w2, lane, C);
     const float r2 = r2_in[row];
     float dot = 0.f;
@@ -198,7 +213,7 @@ __global__ void __launch_bounds__(256) gm_combine_bwd_kernel(int mode, const bf1
       }
     const float c2 = wave_sum(dot) * inv_c * r2 * r2 * r2;
     RowF<NCH> dh;
-    if (dh_in != nullptr) ld_f32<NCH>(dh, dh_in + base, lane, C);
+    if (dh_in != nullptr) ld_f32<NCH, NT>(dh, dh_in + base, lane, C);
     else {
 #pragma unroll
       for (int j = 0; j < NCH; ++j)
@@ -209,11 +224,11 @@ __global__ void __launch_bounds__(256) gm_combine_bwd_kernel(int mode, const bf1
     for (int j = 0; j < NCH; ++j)
 #pragma unroll
       for (int k = 0; k < 4; ++k) dh.v[j][k] += r2 * g.v[j][k] - hv.v[j][k] * c2;
-    if (dh_save != nullptr) st_f32<NCH>(dh_save + base, dh, lane, C);  // diagnostics: dL/dh
+    if (dh_save != nullptr) st_f32<NCH, NT>(dh_save + base, dh, lane, C);  // diagnostics: dL/dh
     if (mode == 0 || mode == 1) {
       RowF<NCH> sv;  // the post-norm's input: s (mode 0) or a (mode 1)
-      if (mode == 0) ld_f32<NCH>(sv, s_save + base, lane, C);
-      else ld_bf16<NCH>(sv, a_save + base, lane, C);
+      if (mode == 0) ld_f32<NCH, NT>(sv, s_save + base, lane, C);
+      else ld_bf16<NCH, NT>(sv, a_save + base, lane, C);
       ld_w<NCH>(wv, w1, lane, C);
       const float r1 = r1_in[row];
       float dot1 = 0.f;
@@ -231,15 +246,15 @@ __global__ void __launch_bounds__(256) gm_combine_bwd_kernel(int mode, const bf1
 #pragma unroll
         for (int k = 0; k < 4; ++k) dn.v[j][k] = r1 * wv.v[j][k] * dh.v[j][k] - sv.v[j][k] * c1;
       if (mode == 0) {
-        st_f32<NCH>(dx + base, dn, lane, C);
-        st_bf16<NCH>(da + base, dn, lane, C);
+        st_f32<NCH, NT>(dx + base, dn, lane, C);
+        st_bf16<NCH, NT>(da + base, dn, lane, C);
       } else {
-        st_f32<NCH>(dx + base, dh, lane, C);
-        st_bf16<NCH>(da + base, dn, lane, C);
+        st_f32<NCH, NT>(dx + base, dh, lane, C);
+        st_bf16<NCH, NT>(da + base, dn, lane, C);
       }
     } else {
-      st_f32<NCH>(dx + base, dh, lane, C);
-      if (mode == 2) st_bf16<NCH>(da + base, dh, lane, C);
+      st_f32<NCH, NT>(dx + base, dh, lane, C);
+      if (mode == 2) st_bf16<NCH, NT>(da + base, dh, lane, C);
     }
   }
   // the workgroup's 4 wave partials summed through LDS in wave order (deterministic): one partial
@@ -287,7 +302,18 @@ static void gm_check_vec(const c10::optional<torch::Tensor>& t, int64_t n, const
 
 // 4 rows in flight per workgroup, up to 4 workgroups per CU: enough waves to overlap each row's
 // memory latency (a one-workgroup-per-CU grid ran the backward 2.4x off its HBM roofline)
-static int gm_grid(int64_t N) { return (int)std::min<int64_t>((N + 3) / 4, 1024); }
+static int gm_grid(int64_t N) {
+  const char* e = std::getenv("PENROZ_GM_GRID");
+  const int64_t cap = e && *e ? std::max(1, std::atoi(e)) : 1024;
+  return (int)std::min<int64_t>((N + 3) / 4, cap);
+}
+
+// PENROZ_GM_NT: non-temporal row loads / stores in the combine kernels (default on: Gemma-3 1B B=8
+// 68.65 / 68.57 -> 68.24 / 68.33 ms; a 2048-workgroup cap was slower either way, ew_ab_r4.log)
+static bool gm_nt() {
+  const char* e = std::getenv("PENROZ_GM_NT");
+  return e && *e ? std::atoi(e) != 0 : true;
+}
 
 // see the file header; x fp32 [N, C]; a bf16 [N, C] (modes 0-2); h_out fp32 (modes 0-2);
 // y_out bf16; s_save fp32 (mode 0); r1 fp32 [N] (modes 0, 1); r2 fp32 [N]
@@ -313,7 +339,7 @@ void gemma_combine_fwd(int64_t mode, torch::Tensor x, c10::optional<torch::Tenso
   if (mode == 0) gm_check_rows(*s_save, N, C, torch::kFloat32, "s_save");
   if (N == 0) return;
   auto stream = at::hip::getCurrentHIPStream();
-  PENROZ_GM_NCH(C, hipLaunchKernelGGL((gm_combine_fwd_kernel<NCH>), dim3(gm_grid(N)), dim3(256), 0, stream, (int)mode,
+  PENROZ_GM_NCH(C, hipLaunchKernelGGL((gm_nt() ? gm_combine_fwd_kernel<NCH, true> : gm_combine_fwd_kernel<NCH, false>), dim3(gm_grid(N)), dim3(256), 0, stream, (int)mode,
                                       x.data_ptr<float>(),
                                       mode != 3 ? reinterpret_cast<const bf16*>(a->data_ptr()) : nullptr,
                                       (mode == 0 || mode == 1) ? w1->data_ptr<float>() : nullptr, w2.data_ptr<float>(),
@@ -367,7 +393,7 @@ void gemma_combine_bwd(int64_t mode, torch::Tensor dy, c10::optional<torch::Tens
   const int grid = gm_grid(N), G = grid;
   auto part = torch::empty({2, G, C}, h.options());
   auto stream = at::hip::getCurrentHIPStream();
-  PENROZ_GM_NCH(C, hipLaunchKernelGGL((gm_combine_bwd_kernel<NCH>), dim3(grid), dim3(256), 4 * C * sizeof(float),
+  PENROZ_GM_NCH(C, hipLaunchKernelGGL((gm_nt() ? gm_combine_bwd_kernel<NCH, true> : gm_combine_bwd_kernel<NCH, false>), dim3(grid), dim3(256), 4 * C * sizeof(float),
                                       stream, (int)mode,
                                       reinterpret_cast<const bf16*>(dy.data_ptr()), dhp, h.data_ptr<float>(),
                                       mode == 0 ? s_save->data_ptr<float>() : nullptr,
