@@ -73,6 +73,8 @@ int64_t skinny_gemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tenso
                     torch::Tensor ws, torch::Tensor cnt, int64_t splitk);
 void skinny_gated(torch::Tensor x, torch::Tensor gu, torch::Tensor out, int64_t kind);
 std::vector<int64_t> skinny_qkv_rope_plan(int64_t M, int64_t N, int64_t K);
+std::vector<int64_t> attn_work_plan(int64_t nblk, int64_t nvh, int64_t slots, int64_t BM, int64_t BN, int64_t T,
+                                    int64_t D, double tile_us);
 int64_t skinny_qkv_rope(torch::Tensor x, torch::Tensor w, torch::Tensor cosv, torch::Tensor sinv, int64_t D,
                         int64_t nrot, torch::Tensor out, torch::Tensor ws, torch::Tensor cnt, int64_t splitk);
 void decode_ln_linear(torch::Tensor rin, c10::optional<torch::Tensor> delta, c10::optional<torch::Tensor> dbias,
@@ -163,6 +165,9 @@ PYBIND11_MODULE(penroz_kernels, m) {
   m.def("skinny_gated", &skinny_gated, pybind11::arg("x"), pybind11::arg("gu"), pybind11::arg("out"),
         pybind11::arg("kind"),
         "decode gated MLP projection: out[M<=64, I] = act(x·gu[:I]ᵀ)·(x·gu[I:]ᵀ), bf16, one launch");
+  m.def("attn_work_plan", &attn_work_plan, pybind11::arg("nblk"), pybind11::arg("nvh"), pybind11::arg("slots"),
+        pybind11::arg("BM"), pybind11::arg("BN"), pybind11::arg("T"), pybind11::arg("D"), pybind11::arg("tile_us"),
+        "causal attention work list (flash_attn_gen.hip attn_plan): [items, split0, block | part << 16 ...]");
   m.def("skinny_qkv_rope_plan", &skinny_qkv_rope_plan, pybind11::arg("M"), pybind11::arg("N"), pybind11::arg("K"),
         "(split-K, fp32 workspace floats, counters) skinny_qkv_rope uses at this shape (host only)");
   m.def("skinny_qkv_rope", &skinny_qkv_rope, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("cos"),

@@ -74,10 +74,11 @@ __device__ __forceinline__ void dma_rows(const bf16* base, size_t RS, int r0, in
 // D = 256 runs 4 waves per workgroup (128 query rows): its LDS (K/V double buffer + the Q image,
 // 128 KB) admits one workgroup per CU, and 4 waves then occupy all four SIMDs.
 template <int D> constexpr int fwd_waves() { return D >= 256 ? 4 : 2; }
-// column parts of the backward kernels (grid z): dK / dV and dQ accumulators per part
+// column parts of the backward kernels (folded into the 1-D grid as virtual heads, see
+// item_head): dK / dV and dQ accumulators per part
 template <int D> constexpr int kv_parts() { return D >= 512 ? 4 : (D >= 256 ? 2 : 1); }
 template <int D> constexpr int dq_parts() { return D >= 512 ? 2 : 1; }
-// forward: Oᵀ column halves per workgroup at D = 512 (grid z; S recomputed by both halves) —
+// forward: Oᵀ column halves per workgroup at D = 512 (virtual heads; S recomputed by both halves) —
 // Q (128 VGPRs) beside a full Oᵀ (256 accumulators) spilled 2 KB per lane
 template <int D> constexpr int fwd_parts() { return D >= 512 ? 2 : 1; }
 
@@ -839,6 +840,16 @@ void launch_combine(bool fwd, const float* ws, bf16* dst, float* lse, int nbh, i
 }
 
 }  // namespace
+
+// the causal work list attn_plan builds (host only, for tests): {items, split0, entries...}
+std::vector<int64_t> attn_work_plan(int64_t nblk, int64_t nvh, int64_t slots, int64_t BM, int64_t BN, int64_t T,
+                                    int64_t D, double tile_us) {
+  const WorkList wl = attn_plan((int)nblk, (int)nvh, (int)slots, (int)BM, (int)BN, (int)T, (int)D, tile_us);
+  std::vector<int64_t> r{wl.n, wl.split0};
+  if (wl.split0 < nblk)
+    for (int i = 0; i < wl.n; ++i) r.push_back(wl.it[i]);
+  return r;
+}
 
 void flash_attn_gen_fwd(torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int64_t H, int64_t Hkv, int64_t D,
                         double scale, double p_drop, int64_t seed) {
