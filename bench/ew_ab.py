@@ -34,14 +34,22 @@ gu = torch.randn(8192, 13824, **bf)
 g = torch.empty(8192, 6912, **bf)
 dg = torch.randn(8192, 6912, **bf)
 dgu = torch.empty_like(gu)
+qkv = torch.randn(8, 1024, 1536, **bf)
+qkv_out = torch.empty_like(qkv)
+cosv = torch.randn(1024, 128, device="cuda")
+sinv = torch.randn(1024, 128, device="cuda")
 cases = {
+    "rope_qkv_gemma": (lambda: k.rope_qkv(qkv, cosv, sinv, 4, 1, 256, False, qkv_out), 2 * qkv.numel() * 2),
     "gelu_fwd": (lambda: k.gelu_fwd(x, 0, y), 2 * x.numel() * 2),
     "gelu_bwd_colsum": (lambda: k.gelu_bwd(dy, x, 0, db, y), 3 * x.numel() * 2),
     "gated_packed": (lambda: k.gated_act_packed(gu, 1, g), (gu.numel() + g.numel()) * 2),
     "gated_bwd_packed": (lambda: k.gated_act_bwd_packed(dg, gu, dgu, 1), (dg.numel() + 2 * gu.numel()) * 2),
 }
+only = sys.argv[1:]
 for rep in range(2):
     for name, (fn, nbytes) in cases.items():
+        if only and name not in only:
+            continue
         for nt in ("0", "1"):
             for cap in ("2048", "8192", "1073741824"):
                 os.environ["PENROZ_EW_NT"], os.environ["PENROZ_EW_GRID"] = nt, cap
