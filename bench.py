@@ -30,11 +30,13 @@ Extra fields (outside the timed region):
     (``penroz.parallel.commtune``): ``devices`` (every rank's PCI id; duplicate devices abort
     the run), ``sweep`` (bare all-reduce ms / busbw over bucket sizes 16-256 MB x fp32/bf16 wire x
     c10d/native transport x native channel count 0 (RCCL's)/8/16/32 x forced protocol (RCCL's /
-    Simple / LL128 at RCCL's channel count), each result checked for the exact average), ``plan``
-    (``commtune.plan``: transport + channel count + protocol, bucket size and wire
+    Simple / LL128) x forced algorithm (RCCL's / Ring / Tree) at RCCL's channel count, each result
+    checked for the exact average), ``plan`` (``commtune.plan``: transport + channel count +
+    protocol + algorithm, bucket size and wire
     the gradient reducer then uses — each transport judged at its own bucket size, the bf16 wire
     only when the predicted fp32 all-reduce exceeds the estimated backward; user-set
-    ``PENROZ_COMM`` / ``PENROZ_RCCL_CHANNELS`` / ``PENROZ_RCCL_PROTO`` / ``PENROZ_BUCKET_MB`` /
+    ``PENROZ_COMM`` / ``PENROZ_RCCL_CHANNELS`` / ``PENROZ_RCCL_PROTO`` / ``PENROZ_RCCL_ALGO`` /
+    ``PENROZ_BUCKET_MB`` /
     ``PENROZ_GRAD_WIRE`` win) and ``rccl.coll_channels`` (parsed from RCCL's INIT log). The process group has an explicit timeout
     (``PENROZ_DIST_TIMEOUT``, 300 s), so a stuck rank fails the run instead of hanging it;
   * ``vs_reference_eager_same_gpu``: the same config through the ``reference`` engine (stock
@@ -288,8 +290,9 @@ def _first_contact(args, device, world: int, rccl_log) -> dict:
         sizes = commtune.SWEEP_SIZES_MB if device.type == "cuda" else (1, 4)
         channels = commtune.SWEEP_CHANNELS if device.type == "cuda" else (0,)
         protos = commtune.SWEEP_PROTOS if device.type == "cuda" else ("",)
+        algos = commtune.SWEEP_ALGOS if device.type == "cuda" else ("",)
         rows = commtune.sweep(device, sizes_mb=sizes, iters=args.comm_probe_iters or 3, channels=channels,
-                              protos=protos)
+                              protos=protos, algos=algos)
         out["sweep"] = rows
         grad_bytes, bwd_ms = _grad_plan_inputs(args)
         if device.type != "cuda":
@@ -303,6 +306,8 @@ def _first_contact(args, device, world: int, rccl_log) -> dict:
             applied["PENROZ_RCCL_CHANNELS"] = str(pl["channels"])
         if pl["transport"] == "native" and pl.get("proto"):
             applied["PENROZ_RCCL_PROTO"] = pl["proto"]
+        if pl["transport"] == "native" and pl.get("algo"):
+            applied["PENROZ_RCCL_ALGO"] = pl["algo"]
         if device.type == "cuda":
             if pl.get("bucket_mb") is not None:
                 applied["PENROZ_BUCKET_MB"] = str(pl["bucket_mb"])
@@ -317,7 +322,8 @@ def _first_contact(args, device, world: int, rccl_log) -> dict:
             from penroz.parallel import rccl
             native = os.environ["PENROZ_COMM"] == "native"
             keep = int(os.environ.get("PENROZ_RCCL_CHANNELS", "0") or 0) if native else -1
-            rccl.NativeComm.release(keep=keep, keep_proto=os.environ.get("PENROZ_RCCL_PROTO", "") if native else "")
+            rccl.NativeComm.release(keep=keep, keep_proto=os.environ.get("PENROZ_RCCL_PROTO", "") if native else "",
+                                    keep_algo=os.environ.get("PENROZ_RCCL_ALGO", "") if native else "")
     out["rccl"] = commtune.rccl_channels(rccl_log)
     return out
 

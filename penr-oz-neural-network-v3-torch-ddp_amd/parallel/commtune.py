@@ -37,6 +37,9 @@ SWEEP_CHANNELS = (0, 8, 16, 32)
 # protocols forced on a native communicator at RCCL's own channel count ("" = RCCL's per-size
 # choice): Simple (bandwidth) vs LL128 (latency / mid sizes); LL is for small messages, not buckets
 SWEEP_PROTOS = ("", "Simple", "LL128")
+# algorithms forced likewise (the per-communicator NCCL_ALGO): Ring (bandwidth-optimal over the
+# point-to-point xGMI rings) vs Tree (fewer steps for latency-bound sizes)
+SWEEP_ALGOS = ("", "Ring", "Tree")
 _LOG_DIR = "/tmp"
 
 
@@ -91,9 +94,10 @@ def _sync(device):
         torch.cuda.synchronize(device)
 
 
-def _native_or_none(device, channels: int = 0, proto: str = ""):
-    """The C++ communicator (``channels`` > 0: built with exactly that many RCCL channels; ``proto``:
-    with that RCCL protocol forced) on every rank, or None on every rank (agreed over the c10d group).
+def _native_or_none(device, channels: int = 0, proto: str = "", algo: str = ""):
+    """The C++ communicator (``channels`` > 0: built with exactly that many RCCL channels; ``proto`` /
+    ``algo``: with that RCCL protocol / algorithm forced) on every rank, or None on every rank
+    (agreed over the c10d group).
 
     A rank that refuses right away (module missing, duplicate device, init error) makes every
     rank fall back. A rank that BLOCKS inside ncclCommInitRank while another refused cannot be
@@ -128,11 +132,11 @@ def _native_or_none(device, channels: int = 0, proto: str = ""):
         guard.start()
         built = torch.zeros(1, device=device)
         try:
-            native = rccl.NativeComm.get(channels=channels, proto=proto)
+            native = rccl.NativeComm.get(channels=channels, proto=proto, algo=algo)
             built += 1
         except RuntimeError as e:  # refused right away on this rank: everybody falls back to c10d
             log.warning(f"native RCCL communicator ({channels or 'default'} channels, protocol "
-                        f"{proto or 'default'}) unavailable: {e}")
+                        f"{proto or 'default'}, algorithm {algo or 'default'}) unavailable: {e}")
         finally:
             guard.cancel()
         dist.all_reduce(built, op=dist.ReduceOp.MIN)
@@ -142,14 +146,15 @@ def _native_or_none(device, channels: int = 0, proto: str = ""):
 
 
 def sweep(device: torch.device, sizes_mb=SWEEP_SIZES_MB, wires=("fp32", "bf16"), transports=("c10d", "native"),
-          iters: int = 3, warmup: int = 1, channels=(0,), protos=("",)) -> list[dict]:
+          iters: int = 3, warmup: int = 1, channels=(0,), protos=("",), algos=("",)) -> list[dict]:
     """Time every (transport, wire, bucket size); max over ranks; correctness-checked.
 
     ``channels``: the native communicator is swept once per channel count (0 = RCCL's own
     choice; others build a communicator with exactly that many channels — the per-communicator
     form of ``NCCL_MIN/MAX_NCHANNELS``); ``protos``: at the first channel count, once more per
-    forced protocol (the per-communicator form of ``NCCL_PROTO``). The extra arms are swept at
-    fp32 only. Every row says which (``channels`` / ``proto``: None for c10d, "" = RCCL's).
+    forced protocol (the per-communicator form of ``NCCL_PROTO``) and per forced algorithm
+    (``NCCL_ALGO``). The extra arms are swept at fp32 only. Every row says which (``channels`` /
+    ``proto`` / ``algo``: None for c10d, "" = RCCL's).
 
     The input on rank r is r + 1 everywhere, so the average is (n + 1) / 2 exactly in fp32 and
     bf16 (n ≤ 255); ``ok`` records whether the result matched on every rank."""
@@ -157,13 +162,15 @@ def sweep(device: torch.device, sizes_mb=SWEEP_SIZES_MB, wires=("fp32", "bf16"),
     gloo = dist.get_backend() != "nccl"
     natives = {}
     if "native" in transports:
-        native_arms = [(ch, protos[0]) for ch in channels] + [(channels[0], pr) for pr in protos[1:]]
-        for ch, pr in native_arms:
-            c = _native_or_none(device, ch, pr)
-            if c is None and (ch, pr) == native_arms[0]:
+        native_arms = ([(ch, protos[0], algos[0]) for ch in channels]
+                       + [(channels[0], pr, algos[0]) for pr in protos[1:]]
+                       + [(channels[0], protos[0], al) for al in algos[1:]])
+        for arm in native_arms:
+            c = _native_or_none(device, *arm)
+            if c is None and arm == native_arms[0]:
                 break  # the communicator cannot be built at all
             if c is not None:
-                natives[(ch, pr)] = c
+                natives[arm] = c
     expect = (world + 1) / 2.0
     arms = [(tr, None) for tr in transports if tr != "native"] + [("native", k) for k in natives]
     rows = []
@@ -173,10 +180,10 @@ def sweep(device: torch.device, sizes_mb=SWEEP_SIZES_MB, wires=("fp32", "bf16"),
             n = int(mb * 2**20) // 4  # elements of an fp32 gradient bucket of that size
             buf = torch.empty(n, device=device, dtype=dt)
             for tr, key in arms:
-                if tr == "native" and wire != "fp32" and key != (channels[0], protos[0]):
+                if tr == "native" and wire != "fp32" and key != (channels[0], protos[0], algos[0]):
                     continue
                 native = natives.get(key)
-                ch, pr = key if key is not None else (None, None)
+                ch, pr, al = key if key is not None else (None, None, None)
 
                 def one():
                     if tr == "native":
@@ -207,7 +214,7 @@ def sweep(device: torch.device, sizes_mb=SWEEP_SIZES_MB, wires=("fp32", "bf16"),
                 sec = float(t.item())
                 nbytes = buf.numel() * buf.element_size()
                 alg = nbytes / sec / 1e9
-                rows.append({"transport": tr, "channels": ch, "proto": pr, "wire": wire, "bucket_mb": mb,
+                rows.append({"transport": tr, "channels": ch, "proto": pr, "algo": al, "wire": wire, "bucket_mb": mb,
                              "ms": round(sec * 1e3, 4),
                              "algbw_GBps": round(alg, 2), "busbw_GBps": round(alg * 2 * (world - 1) / world, 2),
                              "ok": bool(good.item() > 0)})
@@ -215,9 +222,14 @@ def sweep(device: torch.device, sizes_mb=SWEEP_SIZES_MB, wires=("fp32", "bf16"),
     return rows
 
 
-def _arm_rows(rows, transport, channels, wire="fp32", proto=""):
+def _arm_key(r) -> tuple:
+    """A native row's arm: (channel count, protocol, algorithm); "" = RCCL's own choice."""
+    return (r.get("channels", 0), r.get("proto") or "", r.get("algo") or "")
+
+
+def _arm_rows(rows, transport, channels, wire="fp32", proto="", algo=""):
     return [r for r in rows if r["transport"] == transport and r["wire"] == wire and r["ok"]
-            and (transport != "native" or (r.get("channels", 0) == channels and (r.get("proto") or "") == proto))]
+            and (transport != "native" or _arm_key(r) == (channels, proto, algo))]
 
 
 def plan(rows: list[dict], grad_bytes: int, backward_ms: float | None = None, margin: float = 1.03,
@@ -233,43 +245,44 @@ def plan(rows: list[dict], grad_bytes: int, backward_ms: float | None = None, ma
        hide behind the backward — and the bf16 wire of the same transport, correct at that size,
        is ≥ ``bf16_gain`` × faster for the whole gradient.
 
-    The native arms are (channel count, protocol) pairs; the winning arm brings both.
+    The native arms are (channel count, protocol, algorithm) triples; the winning arm brings all three.
 
-    Returns {"transport", "channels", "proto", "bucket_mb", "wire", "predicted_fp32_ms", ...,"reason"}."""
-    out = {"transport": "c10d", "channels": None, "proto": None, "bucket_mb": None, "wire": "fp32"}
+    Returns {"transport", "channels", "proto", "algo", "bucket_mb", "wire", "predicted_fp32_ms", ...,
+    "reason"}."""
+    out = {"transport": "c10d", "channels": None, "proto": None, "algo": None, "bucket_mb": None, "wire": "fp32"}
     c_rows = _arm_rows(rows, "c10d", None)
     if not c_rows:
         out["reason"] = "no correct c10d rows"
         return out
-    arms = {("c10d", None, None): c_rows}
-    for ch, pr in sorted({(r.get("channels", 0), r.get("proto") or "") for r in rows if r["transport"] == "native"}):
-        nr = _arm_rows(rows, "native", ch, proto=pr)
+    arms = {("c10d", None, None, None): c_rows}
+    for ch, pr, al in sorted({_arm_key(r) for r in rows if r["transport"] == "native"}):
+        nr = _arm_rows(rows, "native", ch, proto=pr, algo=al)
         if nr:
-            arms[("native", ch, pr)] = nr
+            arms[("native", ch, pr, al)] = nr
     picked = {}
     for key, ar in arms.items():
         best = max(r["busbw_GBps"] for r in ar)
         pick = min((r for r in ar if r["busbw_GBps"] >= 0.9 * best), key=lambda r: r["bucket_mb"])
         picked[key] = pick
-    c = picked[("c10d", None, None)]
+    c = picked[("c10d", None, None, None)]
     nat = [(k, r) for k, r in picked.items() if k[0] == "native"]
-    choice_key, choice = ("c10d", None, None), c
+    choice_key, choice = ("c10d", None, None, None), c
     if nat:
         nk, nr = max(nat, key=lambda kv: kv[1]["busbw_GBps"])
         if nr["busbw_GBps"] >= margin * c["busbw_GBps"]:
             choice_key, choice = nk, nr
-        out["reason"] = (f"native ({nk[1] or 'default'} channels, protocol {nk[2] or 'default'}) {nr['busbw_GBps']} "
-                         f"GB/s at {nr['bucket_mb']} MB vs c10d {c['busbw_GBps']} GB/s at {c['bucket_mb']} MB")
+        out["reason"] = (f"native ({nk[1] or 'default'} channels, protocol {nk[2] or 'default'}, algorithm "
+                         f"{nk[3] or 'default'}) {nr['busbw_GBps']} GB/s at {nr['bucket_mb']} MB vs c10d "
+                         f"{c['busbw_GBps']} GB/s at {c['bucket_mb']} MB")
     else:
         out["reason"] = "no correct native arm"
-    out.update(transport=choice_key[0], channels=choice_key[1], proto=choice_key[2], bucket_mb=choice["bucket_mb"],
-               busbw_GBps=choice["busbw_GBps"])
+    out.update(transport=choice_key[0], channels=choice_key[1], proto=choice_key[2], algo=choice_key[3],
+               bucket_mb=choice["bucket_mb"], busbw_GBps=choice["busbw_GBps"])
     fp32_ms = grad_bytes / (choice["algbw_GBps"] * 1e9) * 1e3
     out["predicted_fp32_ms"] = round(fp32_ms, 3)
     bf = [r for r in rows if r["transport"] == choice_key[0] and r["wire"] == "bf16" and r["ok"]
           and r["bucket_mb"] == choice["bucket_mb"]
-          and (choice_key[0] != "native" or (r.get("channels", 0) == choice_key[1]
-                                             and (r.get("proto") or "") == choice_key[2]))]
+          and (choice_key[0] != "native" or _arm_key(r) == choice_key[1:])]
     if bf:
         bf16_ms = (grad_bytes / 2) / (bf[0]["algbw_GBps"] * 1e9) * 1e3
         out["predicted_bf16_ms"] = round(bf16_ms, 3)

@@ -26,29 +26,29 @@ def load_module():
 class NativeComm:
     _instances: dict = {}
 
-    def __init__(self, group=None, key: str = "penroz_rccl_uid", channels: int = 0, proto: str = ""):
+    def __init__(self, group=None, key: str = "penroz_rccl_uid", channels: int = 0, proto: str = "", algo: str = ""):
         mod = load_module()
         rank, world = dist.get_rank(group), dist.get_world_size(group)
         store = dist.distributed_c10d._get_default_store()
-        key = f"{key}_c{channels}_p{proto or 'default'}"  # one unique id per communicator
+        key = f"{key}_c{channels}_p{proto or 'default'}_a{algo or 'default'}"  # one unique id per communicator
         if rank == 0:
             store.set(key, mod.RcclComm.unique_id())
         uid = store.get(key)
-        # the protocol (Simple / LL / LL128) is fixed per communicator: RCCL reads NCCL_PROTO while
-        # tuning a communicator at init, so it is set for this init only (a user's own NCCL_PROTO
-        # is left alone when no protocol is asked for)
-        prev = os.environ.get("NCCL_PROTO")
-        if proto:
-            os.environ["NCCL_PROTO"] = proto
+        # the protocol (Simple / LL / LL128) and algorithm (Ring / Tree) are fixed per communicator:
+        # RCCL reads NCCL_PROTO / NCCL_ALGO while tuning a communicator at init, so they are set for
+        # this init only (a user's own setting is left alone when nothing is asked for)
+        forced = {k: v for k, v in (("NCCL_PROTO", proto), ("NCCL_ALGO", algo)) if v}
+        prev = {k: os.environ.get(k) for k in forced}
+        os.environ.update(forced)
         try:
             self.comm = mod.RcclComm(bytes(uid), rank, world, torch.cuda.current_device(), channels)
         finally:
-            if proto:
-                if prev is None:
-                    os.environ.pop("NCCL_PROTO", None)
+            for k, v in prev.items():
+                if v is None:
+                    os.environ.pop(k, None)
                 else:
-                    os.environ["NCCL_PROTO"] = prev
-        self.rank, self.world, self.channels, self.proto = rank, world, channels, proto
+                    os.environ[k] = v
+        self.rank, self.world, self.channels, self.proto, self.algo = rank, world, channels, proto, algo
 
     @staticmethod
     def default_channels() -> int:
@@ -62,20 +62,29 @@ class NativeComm:
         first-contact sweep when a forced protocol beat RCCL's per-size choice), else "" = RCCL's."""
         return os.environ.get("PENROZ_RCCL_PROTO", "")
 
+    @staticmethod
+    def default_algo() -> str:
+        """Algorithm for :meth:`get` without an explicit one: ``PENROZ_RCCL_ALGO`` (set by the
+        first-contact sweep when a forced algorithm beat RCCL's per-size choice), else "" = RCCL's."""
+        return os.environ.get("PENROZ_RCCL_ALGO", "")
+
     @classmethod
-    def get(cls, group=None, channels: int | None = None, proto: str | None = None) -> "NativeComm":
+    def get(cls, group=None, channels: int | None = None, proto: str | None = None,
+            algo: str | None = None) -> "NativeComm":
         ch = cls.default_channels() if channels is None else channels
         pr = cls.default_proto() if proto is None else proto
-        k = (id(group), ch, pr)
+        al = cls.default_algo() if algo is None else algo
+        k = (id(group), ch, pr, al)
         if k not in cls._instances:
-            cls._instances[k] = NativeComm(group, channels=ch, proto=pr)
+            cls._instances[k] = NativeComm(group, channels=ch, proto=pr, algo=al)
         return cls._instances[k]
 
     @classmethod
-    def release(cls, group=None, keep: int | None = None, keep_proto: str = ""):
-        """Destroy this group's communicators except the one with ``keep`` channels and protocol
-        ``keep_proto`` (the sweep builds one per arm; only the chosen one stays alive)."""
-        for k in [k for k in cls._instances if k[0] == id(group) and (k[1], k[2]) != (keep, keep_proto)]:
+    def release(cls, group=None, keep: int | None = None, keep_proto: str = "", keep_algo: str = ""):
+        """Destroy this group's communicators except the one with ``keep`` channels, protocol
+        ``keep_proto`` and algorithm ``keep_algo`` (the sweep builds one per arm; only the chosen
+        one stays alive)."""
+        for k in [k for k in cls._instances if k[0] == id(group) and k[1:] != (keep, keep_proto, keep_algo)]:
             del cls._instances[k]
 
     def all_reduce_avg_async(self, t: torch.Tensor) -> int:

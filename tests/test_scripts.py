@@ -108,9 +108,10 @@ def test_bench_self_launches_ranks_cpu_gloo():
     sweep = d["comm"]["sweep"]
     assert {r["bucket_mb"] for r in sweep} == {1, 4} and {r["wire"] for r in sweep} == {"fp32", "bf16"}
     assert all(r["ok"] and r["busbw_GBps"] > 0 and r["transport"] == "c10d" for r in sweep)
-    assert all(r["channels"] is None and r["proto"] is None for r in sweep)  # arm keys of every row
+    assert all(r["channels"] is None and r["proto"] is None and r["algo"] is None for r in sweep)  # arm keys
     pl = d["comm"]["plan"]
     assert pl["transport"] == "c10d" and pl["wire"] == "fp32" and pl["channels"] is None and pl["proto"] is None
+    assert pl["algo"] is None
     assert pl["grad_bytes"] > 0 and pl["backward_ms_estimate"] is None and "predicted_fp32_ms" in pl
     assert set(d["comm"]["rccl"]) == {"coll_channels", "log"}
 
@@ -136,10 +137,11 @@ def test_comm_choice_rules():
     assert choose(rows, 100)["transport"] == "native" and choose(rows, 40)["transport"] == "c10d"
 
 
-def _prow(tr, mb, bw, ok=True, wire="fp32", ch=None, proto=""):
+def _prow(tr, mb, bw, ok=True, wire="fp32", ch=None, proto="", algo=""):
     # busbw at world 8 = algbw * 2 * 7 / 8
     return {"transport": tr, "channels": ch if tr == "native" else None, "proto": proto if tr == "native" else None,
-            "wire": wire, "bucket_mb": mb, "busbw_GBps": bw, "algbw_GBps": bw * 8 / 14, "ok": ok}
+            "algo": algo if tr == "native" else None, "wire": wire, "bucket_mb": mb, "busbw_GBps": bw,
+            "algbw_GBps": bw * 8 / 14, "ok": ok}
 
 
 def test_comm_plan_judges_each_transport_at_its_own_bucket():
@@ -181,6 +183,23 @@ def test_comm_plan_picks_protocol():
     # RCCL's own protocol choice wins when nothing forced beats it
     rows = [_prow("c10d", 64, 100), _prow("native", 64, 160, ch=0), _prow("native", 64, 150, ch=0, proto="LL128")]
     assert plan(rows, grad_bytes=1)["proto"] == ""
+
+
+def test_comm_plan_picks_algorithm():
+    """A forced algorithm (the per-communicator NCCL_ALGO) comes with the winning native arm, never
+    mixed with another arm's protocol; wrong sums never win; RCCL's own choice wins ties."""
+    from penroz.parallel.commtune import plan
+    rows = [_prow("c10d", 64, 100), _prow("native", 64, 120, ch=0), _prow("native", 64, 130, ch=0, proto="Simple"),
+            _prow("native", 64, 155, ch=0, algo="Ring"), _prow("native", 64, 200, ch=0, algo="Tree", ok=False)]
+    p = plan(rows, grad_bytes=652 * 2**20)
+    assert p["transport"] == "native" and p["algo"] == "Ring" and p["proto"] == "" and p["busbw_GBps"] == 155
+    assert "algorithm Ring" in p["reason"]
+    rows = [_prow("c10d", 64, 100), _prow("native", 64, 160, ch=0), _prow("native", 64, 150, ch=0, algo="Tree")]
+    assert plan(rows, grad_bytes=1)["algo"] == ""
+    # the bf16 wire is looked up on the winning (channels, protocol, algorithm) arm only
+    rows = [_prow("c10d", 64, 100), _prow("native", 64, 155, ch=0, algo="Ring"),
+            _prow("native", 64, 150, ch=0, wire="bf16")]
+    assert plan(rows, 6550 * 2**20, backward_ms=1.0)["wire"] == "fp32"
 
 
 def test_comm_plan_bf16_wire_only_when_exposed():
