@@ -144,7 +144,22 @@ def test_native_rccl_world_size_one():
         c.reset_handles()
         assert c.all_reduce_avg_async(bufs[0]) == 0
         c.wait_all()
+        # first-contact arms: communicators with a forced channel count / protocol / algorithm
+        # (NCCL_* set for their init only) build, reduce exactly and leave the environment alone
+        before = {k: os.environ.get(k) for k in ("NCCL_PROTO", "NCCL_ALGO")}
+        for kw in ({"channels": 8}, {"proto": "Simple"}, {"proto": "LL128"}, {"algo": "Ring"}, {"algo": "Tree"}):
+            arm = NativeComm.get(**kw)
+            assert arm is not c
+            u = torch.full((1 << 16,), 3.0, device="cuda")
+            arm.all_reduce_avg_async(u)
+            arm.wait_all()
+            torch.cuda.synchronize()
+            assert torch.all(u == 3.0), kw
+        assert {k: os.environ.get(k) for k in before} == before
+        NativeComm.release(keep=0)
+        assert NativeComm.get() is c
     finally:
+        NativeComm._instances.clear()
         dist.destroy_process_group()
 
 
