@@ -135,17 +135,20 @@ __device__ __forceinline__ void store4(bf16* p, float a, float b, float c, float
 
 // XCD-aware block mapping. Workgroups are dealt to the 8 XCDs round-robin in dispatch order
 // (x fastest), so the plain grid would scatter one head's blocks over all eight L2s. Remap so
-// the gridDim.x blocks of a head share an XCD (its L2 then serves the head's K/V or Q/dO
-// re-reads) with heads dealt to XCDs round-robin; block index order (heaviest first) is kept
-// per XCD. Bijective; a tail of heads that is not a multiple of 8 keeps the plain order.
+// the gridDim.x blocks of a head share an XCD with heads dealt to XCDs round-robin, and within
+// an XCD dispatch block-major: block 0 (the heaviest) of every head, then block 1, ... — a
+// head-major order ended every launch on the last heads' whole block sequences (GPT-2 B=64:
+// forward -3.5 %, backward -5.5 %, headline -0.6 ms vs head-major, profiles/attn_ab_pmc_r4.log).
+// A head's K/V (256 KB at D = 64) then stay in the 256 MB infinity cache rather than in one L2.
+// Bijective; a tail of heads that is not a multiple of 8 keeps the plain order.
 __device__ __forceinline__ void xcd_head_block(int& blk, int& head) {
   const int nblk = gridDim.x, nheads = gridDim.y;
   const int id = blockIdx.x + nblk * blockIdx.y;
-  const int full = (nheads >> 3) * nblk;  // slots per XCD in the full head groups
+  const int hp = nheads >> 3, full = hp * nblk;  // slots per XCD in the full head groups
   const int xcd = id & 7, slot = id >> 3;
-  if (slot < full) {
-    head = (slot / nblk) * 8 + xcd;
-    blk = slot - (slot / nblk) * nblk;
+  if (slot < full) {  // block-major within the XCD: every head's heaviest block first
+    blk = slot / hp;
+    head = (slot - blk * hp) * 8 + xcd;
   } else {
     const int r = id - 8 * full;
     head = (nheads & ~7) + r / nblk;
