@@ -50,8 +50,8 @@ for rep in range(2):
     for name, (fn, nbytes) in cases.items():
         if only and name not in only:
             continue
-        for nt in ("0", "1"):
-            for cap in ("2048", "8192", "1073741824"):
+        for nt in os.environ.get("EW_NTS", "0 1").split():
+            for cap in os.environ.get("EW_CAPS", "2048 8192 1073741824").split():
                 os.environ["PENROZ_EW_NT"], os.environ["PENROZ_EW_GRID"] = nt, cap
                 t = timeit(fn)
                 print(json.dumps({"kernel": name, "rep": rep, "nt": nt, "cap": cap, "us": round(t * 1e6, 1),
