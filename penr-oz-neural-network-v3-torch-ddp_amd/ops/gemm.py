@@ -20,8 +20,19 @@ from penroz.ops._ext import use_kernels, kernels
 # "auto"/"1": the native kernel (faster than hipBLASLt on every measured GPT-2 shape);
 # "0": hipBLASLt (A/B switch for benchmarking).
 NATIVE_WGRAD = os.environ.get("PENROZ_NATIVE_WGRAD", "auto")
-# pipeline variant of the 256-tile kernel (csrc/kernels/gemm_wgrad.hip): 8 (default), 6, 4 — A/B knob
-WGRAD_VARIANT = int(os.environ.get("PENROZ_WGRAD_VARIANT", "8"))
+# pipeline variant of the 256-tile kernel (csrc/kernels/gemm_wgrad.hip): 8 (fragment prefetch), 6,
+# 4 — A/B knob. Unset: 8 for long token dimensions (GPT-2 B=64: K = 65 536), 6 for K <= 16 384,
+# where the prefetch's extra prologue does not pay (Gemma-3 1B B=8, K = 8192: 67.05 / 67.11 ->
+# 66.62 / 66.66 ms; GPT-2: 8 beats 6, 61.28 / 61.35 vs 61.49 / 61.43 ms; profiles/knobs_ab_r4.log)
+_WGRAD_VARIANT_ENV = os.environ.get("PENROZ_WGRAD_VARIANT")
+WGRAD_VARIANT = int(_WGRAD_VARIANT_ENV) if _WGRAD_VARIANT_ENV else 0  # 0: by K
+WGRAD_SHORT_K = 16384
+
+
+def _wgrad_variant(k: int) -> int:
+    if WGRAD_VARIANT:
+        return WGRAD_VARIANT
+    return 6 if k <= WGRAD_SHORT_K else 8
 
 
 def _native_ok(m: int, n: int, lda: int | None = None) -> bool:
@@ -41,7 +52,7 @@ def wgrad(dy: Tensor, x: Tensor, grad: Tensor, accumulate: bool = True) -> None:
     step whose zero_grad skipped this range)."""
     if (use_kernels(dy) and _native_ok(dy.shape[1], x.shape[1], dy.stride(0)) and dy.dtype == torch.bfloat16
             and x.dtype == torch.bfloat16 and dy.stride(0) % 8 == 0 and x.stride(0) % 8 == 0):
-        kernels().wgrad_gemm(dy, x, grad, 256, WGRAD_VARIANT, accumulate)
+        kernels().wgrad_gemm(dy, x, grad, 256, _wgrad_variant(dy.shape[0]), accumulate)
     elif dy.is_cuda:
         prod = torch.mm(dy.t(), x, out_dtype=torch.float32)
         grad.add_(prod) if accumulate else grad.copy_(prod)
