@@ -29,15 +29,19 @@ Extra fields (outside the timed region):
   * ``comm`` at N > 1 also holds the first-contact record made before the model is built
     (``penroz.parallel.commtune``): ``devices`` (every rank's PCI id; duplicate devices abort
     the run), ``sweep`` (bare all-reduce ms / busbw over bucket sizes 16-256 MB x fp32/bf16 wire x
-    c10d/native transport x native channel count 0 (RCCL's)/8/16/32 x forced protocol (RCCL's /
-    Simple / LL128) x forced algorithm (RCCL's / Ring / Tree) at RCCL's channel count, each result
-    checked for the exact average), ``plan`` (``commtune.plan``: transport + channel count +
-    protocol + algorithm, bucket size and wire
-    the gradient reducer then uses — each transport judged at its own bucket size, the bf16 wire
-    only when the predicted fp32 all-reduce exceeds the estimated backward; user-set
+    c10d/native transport, each result checked for the exact average; with
+    ``PENROZ_COMM_SWEEP_ARMS=full`` also native channel count 8/16/32, forced protocol Simple /
+    LL128 and forced algorithm Ring / Tree), ``plan`` (``commtune.plan``: transport + channel count +
+    protocol + algorithm and bucket size the gradient reducer then uses — each transport judged at
+    its own bucket size — and ``wire_recommendation``, bf16 when the predicted fp32 all-reduce
+    exceeds the estimated backward; the wire itself stays fp32 unless the user sets it; user-set
     ``PENROZ_COMM`` / ``PENROZ_RCCL_CHANNELS`` / ``PENROZ_RCCL_PROTO`` / ``PENROZ_RCCL_ALGO`` /
     ``PENROZ_BUCKET_MB`` /
-    ``PENROZ_GRAD_WIRE`` win) and ``rccl.coll_channels`` (parsed from RCCL's INIT log). The process group has an explicit timeout
+    ``PENROZ_GRAD_WIRE`` win) and ``rccl.coll_channels`` / ``rccl.nranks`` (parsed from RCCL's INIT
+    log: what RCCL itself built for c10d's communicator). ``rccl_nranks`` is ``ncclCommCount`` of the
+    native communicator when the gradients go through it. ``sweep_stats`` holds the sweep's wall time
+    and the arms run / skipped (``commtune.SWEEP_BUDGET_S``) / failed. The forced channel / protocol /
+    algorithm arms run only with ``PENROZ_COMM_SWEEP_ARMS=full``. The process group has an explicit timeout
     (``PENROZ_DIST_TIMEOUT``, 300 s), so a stuck rank fails the run instead of hanging it;
   * ``vs_reference_eager_same_gpu``: the same config through the ``reference`` engine (stock
     PyTorch eager + autocast + foreach AdamW, the reference's semantics) measured in this same
@@ -99,7 +103,7 @@ MODELS = {
     # google/gemma-3-1b-pt text shapes through Mapper.from_hf_config (RMSNorm, RoPE, GQA 4:1,
     # head_dim 256, gated GELU MLP, 262k vocab; random init, no checkpoint): the generic engine
     # (autograd over the HIP layers: flash attention D=256, RMSNorm, gated activation)
-    "gemma3-1b": dict(V=262144, C=1152, L=26, H=4, P=32768, gemma=True),
+    "gemma3-1b": dict(V=262144, C=1152, L=26, H=4, P=32768, gemma=True, Hkv=1, D=256, F=6912),
 }
 
 
@@ -228,6 +232,10 @@ def _comm_info(runner, world: int) -> dict:
     elif getattr(runner, "reducer", None) is not None:
         red = runner.reducer.reducer
     info = {"nranks": dist.get_world_size() if dist.is_initialized() else 1}
+    native = getattr(red, "_native", None) if red is not None else None
+    if native is not None:  # what RCCL itself reports for the communicator the gradients go through
+        info["rccl_nranks"] = {"native": native.nranks, "native_rank": native.comm_rank,
+                               "native_device": native.comm_device}
     try:
         v = torch.cuda.nccl.version()
         info["rccl_version"] = ".".join(map(str, v)) if isinstance(v, tuple) else str(v)
@@ -264,8 +272,9 @@ def _grad_plan_inputs(args) -> tuple[int, float]:
     Gemma: the layer list's linears), backward ≈ 2/3 of 6·params·tokens at a planning 1.0 PF/s."""
     cfg = MODELS[args.model]
     C, L, V = cfg["C"], cfg["L"], cfg["V"]
-    if cfg.get("gemma"):
-        n = L * (C * (cfg["H"] * 256 * 2 + 256 * 2) + 3 * C * 6912) + V * C
+    if cfg.get("gemma"):  # q, o: H·D·C each; k, v: Hkv·D·C each; gate, up, down: C·F each; tied embedding
+        D, Hkv, F = cfg["D"], cfg["Hkv"], cfg["F"]
+        n = L * (C * (2 * cfg["H"] * D + 2 * Hkv * D) + 3 * C * F) + V * C
     else:
         n = L * (12 * C * C + 13 * C) + 2 * V * C + cfg["P"] * C + 2 * C
     tokens = args.batch * args.seq
@@ -288,16 +297,19 @@ def _first_contact(args, device, world: int, rccl_log) -> dict:
     out = {"devices": [d.get("pci", d.get("host")) for d in devices]}
     if args.comm_sweep:
         sizes = commtune.SWEEP_SIZES_MB if device.type == "cuda" else (1, 4)
-        channels = commtune.SWEEP_CHANNELS if device.type == "cuda" else (0,)
-        protos = commtune.SWEEP_PROTOS if device.type == "cuda" else ("",)
-        algos = commtune.SWEEP_ALGOS if device.type == "cuda" else ("",)
+        channels, protos, algos = commtune.sweep_arms() if device.type == "cuda" else ((0,), ("",), ("",))
+        stats = {}
+        transports = ("c10d", "native") if device.type == "cuda" else ("c10d",)  # native = RCCL only
         rows = commtune.sweep(device, sizes_mb=sizes, iters=args.comm_probe_iters or 3, channels=channels,
-                              protos=protos, algos=algos)
+                              protos=protos, algos=algos, transports=transports, stats=stats)
         out["sweep"] = rows
+        out["sweep_stats"] = stats
         grad_bytes, bwd_ms = _grad_plan_inputs(args)
         if device.type != "cuda":
             bwd_ms = None  # the 1 PF/s planning rate means nothing for the CPU plumbing config
-        pl = commtune.plan(rows, grad_bytes, bwd_ms)
+        # the wire stays fp32 (the reference DDP's numerics); the plan only RECORDS whether a bf16
+        # wire would pay (wire_recommendation) — PENROZ_GRAD_WIRE=bf16 is the user's opt-in
+        pl = commtune.plan(rows, grad_bytes, bwd_ms, auto_bf16=False)
         pl["grad_bytes"], pl["backward_ms_estimate"] = grad_bytes, None if bwd_ms is None else round(bwd_ms, 4)
         # the gloo plumbing config keeps the reference DDP's 25 MB buckets and fp32 wire: the sweep's
         # sizes do not model its TCP transfers
@@ -311,12 +323,19 @@ def _first_contact(args, device, world: int, rccl_log) -> dict:
         if device.type == "cuda":
             if pl.get("bucket_mb") is not None:
                 applied["PENROZ_BUCKET_MB"] = str(pl["bucket_mb"])
-            applied["PENROZ_GRAD_WIRE"] = pl["wire"]
         for k, v in applied.items():
             if k in os.environ:
                 pl.setdefault("user_set", {})[k] = os.environ[k]
             else:
                 os.environ[k] = v
+        # every rank must run the same reducer plan (bucket boundaries, transport): the sweep rows are
+        # MAX/MIN-reduced so the plan is a pure function of identical inputs — checked, not assumed
+        env = {k: os.environ.get(k) for k in sorted(applied)}
+        seen = [None] * world
+        dist.all_gather_object(seen, env)
+        if any(e != env for e in seen):
+            raise SystemExit(f"bench.py: ranks disagree on the gradient-sync plan: {seen}")
+        pl["applied_env"], pl["agreed_ranks"] = env, world
         out["plan"] = pl
         if device.type == "cuda":
             from penroz.parallel import rccl

@@ -129,6 +129,23 @@ class RcclComm {
   int rank() const { return rank_; }
   int world() const { return world_; }
   int channels() const { return channels_; }
+  // what RCCL itself says about the communicator (not what the caller passed in): the rank count
+  // of the clique, this member's rank and the device it is bound to
+  int nranks() const {
+    int n = 0;
+    NCCL_OK(ncclCommCount(comm_, &n));
+    return n;
+  }
+  int comm_rank() const {
+    int r = -1;
+    NCCL_OK(ncclCommUserRank(comm_, &r));
+    return r;
+  }
+  int comm_device() const {
+    int d = -1;
+    NCCL_OK(ncclCommCuDevice(comm_, &d));
+    return d;
+  }
 
  private:
   void fence_from_current() {
@@ -185,7 +202,10 @@ PYBIND11_MODULE(penroz_comm, m) {
       .def("synchronize", &RcclComm::synchronize)
       .def_property_readonly("rank", &RcclComm::rank)
       .def_property_readonly("world", &RcclComm::world)
-      .def_property_readonly("channels", &RcclComm::channels);
+      .def_property_readonly("channels", &RcclComm::channels)
+      .def_property_readonly("nranks", &RcclComm::nranks)
+      .def_property_readonly("comm_rank", &RcclComm::comm_rank)
+      .def_property_readonly("comm_device", &RcclComm::comm_device);
   m.def("version", [] {
     int v = 0;
     ncclGetVersion(&v);

@@ -8,8 +8,8 @@ per-module autograd it runs an explicit forward and backward:
 forward, per layer (N = B·T tokens, fp32 residual stream — the reference's autocast numerics)
   LN1 (HIP, → bf16) → QKV GEMM+bias (hipBLASLt) → flash attention (HIP, reads the fused QKV
   tensor, writes head-merged O + LSE) → proj GEMM+bias → residual-add+LN2 (one HIP pass)
-  → fc GEMM+bias+GELU (HIP deferred-epilogue GEMM writing pre-activation and activation) → fc2
-  GEMM+bias → (residual-add fused into the next LN)
+  → fc GEMM+bias (hipBLASLt) → GELU (HIP elementwise kernel writing the activation; the
+  pre-activation is kept for the backward) → fc2 GEMM+bias → (residual-add fused into the next LN)
 head: final LN → lm_head GEMM → cross-entropy (HIP: one LDS-resident pass per row, writes
   the logits gradient in place, no fp32 logits). The head can run in token chunks
   (``_head_chunk_rows``: automatic above 8 GiB of logits, or ``PENROZ_HEAD_CHUNK`` rows):
@@ -421,7 +421,9 @@ class GPTExecutor:
             dp, ds = self._drop(training, dropout_seed, l, 0)
             norm_ops.add_ln_fwd(self.resid[l], self.tmp_c, self.resid_mid[l], f(b.ln2.weight), f(b.ln2.bias),
                                 b.ln2.eps, y=self.ln2[l], mean=mean2, rstd=rstd2, dropout_p=dp, dropout_seed=ds)
-            # fc + GELU: one kernel writing pre-activation and activation (ops/gemm.py linear_gelu)
+            # fc: library GEMM + bias into the pre-activation, then the HIP GELU kernel writes the
+            # activation (ops/gemm.py linear_gelu); the backward's dgrad_gelu is a library GEMM
+            # followed by one GELU-backward + fc-bias column-sum kernel
             gemm_ops.linear_gelu(self.ln2[l], self.bf16(b.fc.weight), self.bf16(b.fc.bias), self.fcpre[l],
                                  self.fcact[l], s.gelu_approx)
             self._linear(self.fcact[l], b.fc2, out=self.tmp_c)
@@ -491,10 +493,10 @@ class GPTExecutor:
                 self._zero_views = [self.flat_grad[a:b] for a, b in gaps]
                 self._zero_views_of = self.flat_grad
             torch._foreach_zero_(self._zero_views)
-            self._fresh = set(self._wgrad_ranges)
+            self._stale = {k: [r] for k, r in self._wgrad_ranges.items()}
         else:
             self.flat_grad.zero_()
-            self._fresh = set()
+            self._stale = {}
         self._captured = None
 
     def _learn_wgrad_ranges(self):
@@ -584,7 +586,14 @@ class GPTExecutor:
 
     def _wgrad_into(self, key: int, dy: Tensor, x: Tensor, g: Tensor):
         """g (+)= dyᵀ·x on the side stream: the first write of a range that zero_grad left alone
-        overwrites it; the ranges are recorded during the first backward (see zero_grad)."""
+        overwrites it; the ranges are recorded during the first backward (see zero_grad).
+
+        ``_stale[key]`` holds the parts of the key's learned range that zero_grad skipped and no
+        write of this step has touched yet. A write covering exactly the whole stale learned range
+        overwrites it; any other write (e.g. a chunked wgrad writing sub-ranges under one key)
+        first clears the stale parts it overlaps and accumulates; parts still stale at the end of
+        the backward are cleared by :meth:`_finish_wgrad_bookkeeping`. A range pattern that differs
+        from the learned one also makes zero_grad clear everything from the next step on."""
         rec = getattr(self, "_wgrad_ranges", None)
         if rec is None:
             rec = self._wgrad_ranges = {}
@@ -595,38 +604,47 @@ class GPTExecutor:
                 self._wgrad_ranges_invalid = True
             rec[key] = rng
         elif rec.get(key) != rng:
-            # a range zero_grad did not learn (e.g. a chunked wgrad writing sub-ranges under one
-            # key): zero_grad clears everything from the next step on; in this step the learned
-            # range, which zero_grad skipped, is cleared before the first write, then accumulated
             self._wgrad_ranges_invalid = True
             self._zero_gaps = None
-            fresh = getattr(self, "_fresh", None)
-            if fresh and key in fresh:
-                fresh.discard(key)
-                s_, e_ = rec[key]
-                stale = self.flat_grad[s_:e_]
-                self._side_call(dy, lambda: stale.zero_())
-            self._side_call(dy, lambda: gemm_ops.wgrad(dy, x, g, True))
+        stale = getattr(self, "_stale", None) or {}
+        parts = stale.get(key)
+        if parts and parts == [rng]:  # the whole learned range, untouched this step: overwrite
+            del stale[key]
+            self._side_call(dy, lambda: gemm_ops.wgrad(dy, x, g, False))
             return
-        fresh = getattr(self, "_fresh", None)
-        acc = not (fresh and key in fresh)
-        if not acc:
-            fresh.discard(key)
-        self._side_call(dy, lambda: gemm_ops.wgrad(dy, x, g, acc))
+        if parts:
+            keep = []
+            for s_, e_ in parts:
+                a, b = max(s_, rng[0]), min(e_, rng[1])
+                if a >= b:
+                    keep.append((s_, e_))
+                    continue
+                view = self.flat_grad[a:b]
+                self._side_call(dy, lambda v=view: v.zero_())
+                if s_ < a:
+                    keep.append((s_, a))
+                if b < e_:
+                    keep.append((b, e_))
+            if keep:
+                stale[key] = keep
+            else:
+                del stale[key]
+        self._side_call(dy, lambda: gemm_ops.wgrad(dy, x, g, True))
 
     def _finish_wgrad_bookkeeping(self):
-        """End of a backward: learn the ranges once; clear any range zero_grad skipped that no GEMM
-        wrote (not expected: every backward writes every linear weight's gradient)."""
+        """End of a backward: learn the ranges once; clear any part of a range zero_grad skipped
+        that no GEMM wrote (not expected: every backward writes every linear weight's gradient)."""
         if not getattr(self, "_ranges_learned", False):
             self._ranges_learned = True
             self._learn_wgrad_ranges()
-        fresh = getattr(self, "_fresh", None)
-        if fresh:
-            log.warning(f"weight-gradient ranges not written by this backward: {len(fresh)}; clearing them")
-            for key in list(fresh):
-                s_, e_ = self._wgrad_ranges[key]
-                self.flat_grad[s_:e_].zero_()
-            fresh.clear()
+        stale = getattr(self, "_stale", None)
+        if stale:
+            log.warning(f"weight-gradient ranges not written by this backward: {len(stale)}; clearing them")
+            self._join_side()
+            for parts in stale.values():
+                for s_, e_ in parts:
+                    self.flat_grad[s_:e_].zero_()
+            stale.clear()
 
     def _defer_reductions(self, on: bool):
         """LayerNorm / bias column-reduction finishing kernels go to the side stream (on) or not."""

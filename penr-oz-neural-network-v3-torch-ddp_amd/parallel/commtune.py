@@ -31,15 +31,32 @@ import torch.distributed as dist
 log = logging.getLogger(__name__)
 
 SWEEP_SIZES_MB = (16, 32, 64, 128, 256)
-# native communicator channel counts tried on first contact (0 = RCCL's own choice); an MI355X
-# node has 7 xGMI links per GPU, so the useful counts are multiples of the rings RCCL lays over them
+# native communicator arms. The default first contact builds ONE native communicator (RCCL's own
+# channel count, protocol and algorithm). The forced arms below are opt-in
+# (``PENROZ_COMM_SWEEP_ARMS=full``): a forced protocol / algorithm that RCCL cannot serve fails only
+# at enqueue time, and no run with more than one GPU has exercised them yet.
+# channel counts: an MI355X node has 7 xGMI links per GPU, so the useful counts are multiples of the
+# rings RCCL lays over them (0 = RCCL's own choice)
 SWEEP_CHANNELS = (0, 8, 16, 32)
-# protocols forced on a native communicator at RCCL's own channel count ("" = RCCL's per-size
-# choice): Simple (bandwidth) vs LL128 (latency / mid sizes); LL is for small messages, not buckets
+# protocols forced at RCCL's own channel count ("" = RCCL's per-size choice): Simple (bandwidth) vs
+# LL128 (latency / mid sizes); LL is for small messages, not buckets
 SWEEP_PROTOS = ("", "Simple", "LL128")
 # algorithms forced likewise (the per-communicator NCCL_ALGO): Ring (bandwidth-optimal over the
 # point-to-point xGMI rings) vs Tree (fewer steps for latency-bound sizes)
 SWEEP_ALGOS = ("", "Ring", "Tree")
+# wall-clock budget of the whole first-contact sweep; arms not yet started when it is spent are
+# skipped (agreed over the group, so every rank skips the same ones)
+SWEEP_BUDGET_S = 90.0
+
+
+def sweep_arms() -> tuple[tuple, tuple, tuple]:
+    """(channels, protos, algos) the first contact sweeps: RCCL's defaults only, or every forced arm
+    with ``PENROZ_COMM_SWEEP_ARMS=full``."""
+    if os.environ.get("PENROZ_COMM_SWEEP_ARMS", "default") == "full":
+        return SWEEP_CHANNELS, SWEEP_PROTOS, SWEEP_ALGOS
+    return (0,), ("",), ("",)
+
+
 _LOG_DIR = "/tmp"
 
 
@@ -58,27 +75,41 @@ def enable_rccl_init_log(rank: int) -> str | None:
 
 
 _CHAN_RE = [re.compile(r"(\d+) coll channels"), re.compile(r"Channel \d+/(\d+)")]
+# RCCL's "Init COMPLETE" / "comm ... rank r nranks n" lines: the clique size RCCL itself built
+_NRANKS_RE = re.compile(r"\bn[Rr]anks[ =](\d+)")
+
+
+def parse_rccl_log(text: str) -> dict:
+    """{'coll_channels', 'nranks'} from RCCL INIT/GRAPH log text (None where absent). ``nranks`` is
+    the largest clique size any communicator of the process reported."""
+    n = None
+    for rx in _CHAN_RE:
+        vals = [int(v) for v in rx.findall(text)]
+        if vals:
+            n = max(vals)
+            break
+    ranks = [int(v) for v in _NRANKS_RE.findall(text)]
+    return {"coll_channels": n, "nranks": max(ranks) if ranks else None}
 
 
 def rccl_channels(pattern: str | None) -> dict:
-    """{'coll_channels': n | None, 'log': path} from the INIT log written under ``pattern``."""
+    """{'coll_channels': n | None, 'nranks': n | None, 'log': path} from the INIT log written under
+    ``pattern`` (``nranks``: what RCCL itself reported for its communicators, c10d's included)."""
     if not pattern:
-        return {"coll_channels": None, "log": None}
+        return {"coll_channels": None, "nranks": None, "log": None}
     files = sorted(glob.glob(pattern + "*")) or ([pattern] if os.path.exists(pattern) else [])
-    n = None
+    out = {"coll_channels": None, "nranks": None}
     for f in files:
         try:
             text = open(f, errors="replace").read()
         except OSError:
             continue
-        for rx in _CHAN_RE:
-            vals = [int(v) for v in rx.findall(text)]
-            if vals:
-                n = max(vals)
-                break
-        if n is not None:
-            break
-    return {"coll_channels": n, "log": files[0] if files else None}
+        got = parse_rccl_log(text)
+        for k, v in got.items():
+            if v is not None and out[k] is None:
+                out[k] = v
+    out["log"] = files[0] if files else None
+    return out
 
 
 def gather_identities(device: torch.device) -> list[dict]:
@@ -142,11 +173,37 @@ def _native_or_none(device, channels: int = 0, proto: str = "", algo: str = ""):
         dist.all_reduce(built, op=dist.ReduceOp.MIN)
         if built.item() == 0:
             native = None
+        else:
+            native = _probe_native(device, native, channels, proto, algo)
     return native
 
 
+def _probe_native(device, native, channels, proto, algo):
+    """One small AVG all-reduce on a freshly built communicator before any timing: a forced
+    protocol / algorithm that RCCL cannot serve fails at ENQUEUE time, not at init. Every rank must
+    agree (MIN over the c10d group) or the arm is dropped on every rank."""
+    ok = torch.zeros(1, device=device)
+    try:
+        t = torch.full((4096,), float(dist.get_rank() + 1), device=device)
+        native.all_reduce_avg_async(t)
+        native.wait_all()
+        _sync(device)
+        if bool((t == (dist.get_world_size() + 1) / 2.0).all()):
+            ok += 1
+    except RuntimeError as e:
+        log.warning(f"native RCCL arm ({channels or 'default'} channels, protocol {proto or 'default'}, "
+                    f"algorithm {algo or 'default'}) failed its probe all-reduce: {e}")
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if ok.item() > 0:
+        return native
+    from penroz.parallel import rccl
+    rccl.NativeComm.drop(channels=channels, proto=proto, algo=algo)
+    return None
+
+
 def sweep(device: torch.device, sizes_mb=SWEEP_SIZES_MB, wires=("fp32", "bf16"), transports=("c10d", "native"),
-          iters: int = 3, warmup: int = 1, channels=(0,), protos=("",), algos=("",)) -> list[dict]:
+          iters: int = 3, warmup: int = 1, channels=(0,), protos=("",), algos=("",),
+          budget_s: float | None = None, stats: dict | None = None) -> list[dict]:
     """Time every (transport, wire, bucket size); max over ranks; correctness-checked.
 
     ``channels``: the native communicator is swept once per channel count (0 = RCCL's own
@@ -156,34 +213,54 @@ def sweep(device: torch.device, sizes_mb=SWEEP_SIZES_MB, wires=("fp32", "bf16"),
     (``NCCL_ALGO``). The extra arms are swept at fp32 only. Every row says which (``channels`` /
     ``proto`` / ``algo``: None for c10d, "" = RCCL's).
 
+    Arms run one after another: each native arm is built, probed (:func:`_probe_native`), timed at
+    every size and — unless it is the first (RCCL-default) arm — destroyed right away, so at most
+    two native communicators are alive at once. ``budget_s`` (default ``SWEEP_BUDGET_S``) caps the
+    sweep's wall time: an arm that would start after it is spent is skipped on every rank (the
+    elapsed time is MAX-agreed). ``stats`` (a dict) receives ``wall_s``, ``arms_run``,
+    ``arms_skipped`` and ``arms_failed``.
+
     The input on rank r is r + 1 everywhere, so the average is (n + 1) / 2 exactly in fp32 and
     bf16 (n ≤ 255); ``ok`` records whether the result matched on every rank."""
     world, rank = dist.get_world_size(), dist.get_rank()
     gloo = dist.get_backend() != "nccl"
-    natives = {}
-    if "native" in transports:
-        native_arms = ([(ch, protos[0], algos[0]) for ch in channels]
-                       + [(channels[0], pr, algos[0]) for pr in protos[1:]]
-                       + [(channels[0], protos[0], al) for al in algos[1:]])
-        for arm in native_arms:
-            c = _native_or_none(device, *arm)
-            if c is None and arm == native_arms[0]:
-                break  # the communicator cannot be built at all
-            if c is not None:
-                natives[arm] = c
+    budget = SWEEP_BUDGET_S if budget_s is None else budget_s
+    t_start = time.perf_counter()
+    st = stats if stats is not None else {}
+    st.update(arms_run=[], arms_skipped=[], arms_failed=[])
     expect = (world + 1) / 2.0
-    arms = [(tr, None) for tr in transports if tr != "native"] + [("native", k) for k in natives]
+    arms = [(tr, None) for tr in transports if tr != "native"]
+    if "native" in transports:
+        arms += [("native", (ch, protos[0], algos[0])) for ch in channels]
+        arms += [("native", (channels[0], pr, algos[0])) for pr in protos[1:]]
+        arms += [("native", (channels[0], protos[0], al)) for al in algos[1:]]
+    default_arm = (channels[0], protos[0], algos[0])
     rows = []
-    for wire in wires:
-        dt = {"fp32": torch.float32, "bf16": torch.bfloat16}[wire]
-        for mb in sizes_mb:
-            n = int(mb * 2**20) // 4  # elements of an fp32 gradient bucket of that size
-            buf = torch.empty(n, device=device, dtype=dt)
-            for tr, key in arms:
-                if tr == "native" and wire != "fp32" and key != (channels[0], protos[0], algos[0]):
-                    continue
-                native = natives.get(key)
-                ch, pr, al = key if key is not None else (None, None, None)
+    native_dead = False
+    for tr, key in arms:
+        label = tr if key is None else f"native:{key[0] or 'default'}/{key[1] or 'default'}/{key[2] or 'default'}"
+        spent = torch.tensor([time.perf_counter() - t_start], dtype=torch.float64, device=device)
+        dist.all_reduce(spent, op=dist.ReduceOp.MAX)
+        if spent.item() > budget or (tr == "native" and native_dead):
+            st["arms_skipped"].append(label)
+            continue
+        native = None
+        if tr == "native":
+            native = _native_or_none(device, *key)
+            if native is None:
+                st["arms_failed"].append(label)
+                if key == default_arm:
+                    native_dead = True  # the communicator cannot be built at all
+                continue
+        st["arms_run"].append(label)
+        ch, pr, al = key if key is not None else (None, None, None)
+        for wire in wires:
+            if tr == "native" and wire != "fp32" and key != default_arm:
+                continue
+            dt = {"fp32": torch.float32, "bf16": torch.bfloat16}[wire]
+            for mb in sizes_mb:
+                n = int(mb * 2**20) // 4  # elements of an fp32 gradient bucket of that size
+                buf = torch.empty(n, device=device, dtype=dt)
 
                 def one():
                     if tr == "native":
@@ -218,7 +295,13 @@ def sweep(device: torch.device, sizes_mb=SWEEP_SIZES_MB, wires=("fp32", "bf16"),
                              "ms": round(sec * 1e3, 4),
                              "algbw_GBps": round(alg, 2), "busbw_GBps": round(alg * 2 * (world - 1) / world, 2),
                              "ok": bool(good.item() > 0)})
-            del buf
+                del buf
+        if tr == "native" and key != default_arm:
+            from penroz.parallel import rccl
+            del native
+            rccl.NativeComm.drop(channels=key[0], proto=key[1], algo=key[2])
+    st["wall_s"] = round(time.perf_counter() - t_start, 3)
+    st["budget_s"] = budget
     return rows
 
 
@@ -233,17 +316,19 @@ def _arm_rows(rows, transport, channels, wire="fp32", proto="", algo=""):
 
 
 def plan(rows: list[dict], grad_bytes: int, backward_ms: float | None = None, margin: float = 1.03,
-         bf16_gain: float = 1.2) -> dict:
+         bf16_gain: float = 1.2, auto_bf16: bool = False) -> dict:
     """The whole gradient-sync configuration from one sweep, each transport judged at ITS OWN size:
 
     1. every correct (transport, channel count) arm gets its bucket size from :func:`choose_bucket`'s
        rule (the smallest size within 90 % of that arm's best bus bandwidth);
     2. the native communicator wins only if its best arm's bus bandwidth, at that arm's size, is
        ≥ ``margin`` × c10d's at c10d's size (the channel count comes with the arm);
-    3. the wire: fp32 (the reference DDP's) unless the predicted fp32 all-reduce of the whole
+    3. the wire: always fp32 (the reference DDP's numerics) unless ``auto_bf16``. The bf16 wire is
+       RECOMMENDED (``wire_recommendation``) when the predicted fp32 all-reduce of the whole
        gradient (``grad_bytes`` / algbw at the chosen size) exceeds ``backward_ms`` — it could not
        hide behind the backward — and the bf16 wire of the same transport, correct at that size,
-       is ≥ ``bf16_gain`` × faster for the whole gradient.
+       is ≥ ``bf16_gain`` × faster for the whole gradient; only ``auto_bf16`` applies it (the user
+       opts in with ``PENROZ_GRAD_WIRE=bf16``; a bf16 wire changes gradient numerics).
 
     The native arms are (channel count, protocol, algorithm) triples; the winning arm brings all three.
 
@@ -287,9 +372,12 @@ def plan(rows: list[dict], grad_bytes: int, backward_ms: float | None = None, ma
         bf16_ms = (grad_bytes / 2) / (bf[0]["algbw_GBps"] * 1e9) * 1e3
         out["predicted_bf16_ms"] = round(bf16_ms, 3)
         if backward_ms is not None and fp32_ms > backward_ms and fp32_ms >= bf16_gain * bf16_ms:
-            out["wire"] = "bf16"
+            out["wire_recommendation"] = "bf16"
+            if auto_bf16:
+                out["wire"] = "bf16"
             out["wire_reason"] = (f"fp32 all-reduce {fp32_ms:.1f} ms > backward {backward_ms:.1f} ms; "
                                   f"bf16 {bf16_ms:.1f} ms")
+    out.setdefault("wire_recommendation", "fp32")
     if "wire_reason" not in out:
         out["wire_reason"] = ("no backward estimate" if backward_ms is None else
                               f"fp32 all-reduce {fp32_ms:.1f} ms vs backward {backward_ms:.1f} ms")

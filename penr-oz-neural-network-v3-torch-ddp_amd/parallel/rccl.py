@@ -87,6 +87,27 @@ class NativeComm:
         for k in [k for k in cls._instances if k[0] == id(group) and k[1:] != (keep, keep_proto, keep_algo)]:
             del cls._instances[k]
 
+    @classmethod
+    def drop(cls, group=None, channels: int = 0, proto: str = "", algo: str = ""):
+        """Destroy the one communicator of this group with that (channels, protocol, algorithm)."""
+        cls._instances.pop((id(group), channels, proto, algo), None)
+
+    @property
+    def nranks(self) -> int:
+        """The clique size RCCL reports for this communicator (``ncclCommCount``), not the world
+        size the caller passed in."""
+        return int(self.comm.nranks)
+
+    @property
+    def comm_rank(self) -> int:
+        """This member's rank as RCCL reports it (``ncclCommUserRank``)."""
+        return int(self.comm.comm_rank)
+
+    @property
+    def comm_device(self) -> int:
+        """The HIP device RCCL bound this communicator to (``ncclCommCuDevice``)."""
+        return int(self.comm.comm_device)
+
     def all_reduce_avg_async(self, t: torch.Tensor) -> int:
         """Launch; returns the handle :meth:`wait` takes."""
         return self.comm.all_reduce_avg_async(t)

@@ -99,3 +99,77 @@ def test_gemma_executor_matches_heterogeneous_gemma4_layer_list():
     wide = SimpleNamespace(**{**vars(cfg), "hidden_size": 5376, "num_hidden_layers": 1, "layer_types": None,
                               "intermediate_size": 64, "vocab_size": 16})
     assert GemmaExecutor.match(NeuralNetworkModel("w", Mapper(Mapper.from_hf_config(wide), {"adamw": {}}))) is not None
+
+
+def _range_exec(monkeypatch):
+    """A bare executor with only the weight-gradient bookkeeping live: flat fp32 buffer, wgrad
+    done eagerly on the CPU (g = dyᵀ·x or g += dyᵀ·x), no side stream."""
+    import types
+    import torch
+    from penroz.models import executor as E
+    ex = object.__new__(GPTExecutor)
+    ex.flat_grad = torch.zeros(64)
+    ex.device = types.SimpleNamespace(type="cuda", index=0)  # range learning is a GPU-path feature
+    ex._side = None
+    ex.wait_gradients = lambda: None
+
+    def wgrad(dy, x, g, acc):
+        r = dy.t() @ x
+        if acc:
+            g.add_(r)
+        else:
+            g.copy_(r)
+    monkeypatch.setattr(E.gemm_ops, "wgrad", wgrad)
+    return ex
+
+
+def test_wgrad_ranges_chunked_after_learning(monkeypatch):
+    """after the ranges are learned, a key that writes sub-ranges (chunked wgrad) must
+    never accumulate onto last step's data — whether its first chunk is a sub-range, the whole
+    learned range, or some parts are never written."""
+    import torch
+    ex = _range_exec(monkeypatch)
+    torch.manual_seed(0)
+    A = ex.flat_grad[0:32].view(8, 4)    # weight A's gradient
+    Bg = ex.flat_grad[40:56].view(4, 4)  # weight B's gradient; [32:40) and [56:64) are other grads
+    dyA, xA = torch.randn(5, 8), torch.randn(5, 4)
+    dyB, xB = torch.randn(5, 4), torch.randn(5, 4)
+    # learning step: whole-range writes
+    ex.zero_grad()
+    ex._wgrad_into(1, dyA, xA, A)
+    ex._wgrad_into(2, dyB, xB, Bg)
+    ex._finish_wgrad_bookkeeping()
+    assert ex._zero_gaps == [(0 + 32, 40), (56, 64)]
+    assert torch.allclose(A, dyA.t() @ xA)
+
+    def step(writes_a, learned_ranges_skipped=False):
+        ex.flat_grad.fill_(123.0)  # last step's values everywhere
+        ex.zero_grad()
+        assert torch.all(ex.flat_grad[32:40] == 0)
+        if learned_ranges_skipped:
+            assert torch.all(ex.flat_grad[40:56] == 123.0) and torch.all(ex.flat_grad[0:32] == 123.0)
+        for r0, r1, dy, x in writes_a:
+            ex._wgrad_into(1, dy[:, r0:r1], x, A[r0:r1])
+        ex._wgrad_into(2, dyB, xB, Bg)
+        ex._finish_wgrad_bookkeeping()
+        assert torch.allclose(Bg, dyB.t() @ xB)
+
+    d1, d2 = torch.randn(5, 8), torch.randn(5, 8)
+    # sub-ranges first, one range accumulated twice (two token chunks), the rest once
+    step([(0, 4, d1, xA), (0, 4, d2, xA), (4, 8, d1, xA)], learned_ranges_skipped=True)
+    want = torch.cat([(d1[:, :4] + d2[:, :4]).t() @ xA, d1[:, 4:].t() @ xA])
+    assert torch.allclose(A, want, atol=1e-5)
+    # the whole learned range first (overwrite), then a sub-range accumulates onto it; with the
+    # pattern changed zero_grad now clears everything, so re-arm the skip to test the stale path
+    assert ex._zero_gaps is None
+    ex._zero_gaps = [(32, 40), (56, 64)]
+    step([(0, 8, d1, xA), (2, 6, d2, xA)], learned_ranges_skipped=True)
+    want = d1.t() @ xA
+    want[2:6] += d2[:, 2:6].t() @ xA
+    assert torch.allclose(A, want, atol=1e-5)
+    # a part never written this step ends up zero, not stale
+    ex._zero_gaps = [(32, 40), (56, 64)]
+    step([(0, 3, d1, xA)], learned_ranges_skipped=True)
+    assert torch.allclose(A[0:3], d1[:, :3].t() @ xA, atol=1e-5) and torch.all(A[3:] == 0)
+    # the changed pattern makes zero_grad clear everything from now on
+    assert ex._wgrad_ranges_invalid and ex._zero_gaps is None

@@ -10,7 +10,7 @@ from fastapi.testclient import TestClient
 
 from penroz.utils import checkpoint as ckpt
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")]
 
 
 def test_import_then_generate_on_gpu_matches_hf_greedy(workdir, monkeypatch):

@@ -103,7 +103,7 @@ def test_gelu(approx):
     out = dy.clone()
     Ac.gelu_bwd(out, x, approx, dbias, out=out)  # in place + fused column sum
     _close(out, ref, 0.05, 0.01)
-    _close(dbias, out.float().sum(0), 0.05, 1e-3)
+    _close(dbias, ref.sum(0), 0.05, 2e-3, "dbias vs fp32 reference")  # independent fp32 column sum
 
 
 @pytest.mark.parametrize("rows", [8192, 8191])
@@ -120,7 +120,7 @@ def test_gelu_wide_grid_stride_and_row_pairs(rows):
     out = dy.clone()
     Ac.gelu_bwd(out, x, "none", dbias, out=out)
     _close(out, ref, 0.05, 0.01)
-    _close(dbias, out.float().sum(0), 0.05, 1e-3)
+    _close(dbias, ref.sum(0), 0.25, 2e-3, "dbias vs fp32 reference")  # independent fp32 column sum
 
 
 @pytest.mark.parametrize("N,V", [(64, 50304), (37, 262144), (5, 1000)])

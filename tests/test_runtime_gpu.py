@@ -126,6 +126,8 @@ def test_native_rccl_world_size_one():
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"))
     try:
         c = NativeComm.get()
+        # what RCCL itself reports (ncclCommCount / UserRank / CuDevice), not the caller's world size
+        assert (c.nranks, c.comm_rank, c.comm_device) == (1, 0, torch.cuda.current_device())
         t = torch.arange(1024, device="cuda", dtype=torch.float32)
         c.all_reduce_avg_async(t)
         c.wait_all()
@@ -158,6 +160,12 @@ def test_native_rccl_world_size_one():
         assert {k: os.environ.get(k) for k in before} == before
         NativeComm.release(keep=0)
         assert NativeComm.get() is c
+        # the sweep's per-arm probe and drop: a probed arm survives, a dropped one is rebuilt anew
+        from penroz.parallel import commtune
+        arm = commtune._native_or_none(torch.device("cuda:0"), 8)
+        assert arm is not None and arm.nranks == 1
+        NativeComm.drop(channels=8)
+        assert NativeComm.get(channels=8) is not arm
     finally:
         NativeComm._instances.clear()
         dist.destroy_process_group()

@@ -113,7 +113,11 @@ def test_bench_self_launches_ranks_cpu_gloo():
     assert pl["transport"] == "c10d" and pl["wire"] == "fp32" and pl["channels"] is None and pl["proto"] is None
     assert pl["algo"] is None
     assert pl["grad_bytes"] > 0 and pl["backward_ms_estimate"] is None and "predicted_fp32_ms" in pl
-    assert set(d["comm"]["rccl"]) == {"coll_channels", "log"}
+    assert set(d["comm"]["rccl"]) == {"coll_channels", "nranks", "log"}
+    assert pl["agreed_ranks"] == 2 and pl["applied_env"] == {"PENROZ_COMM": "c10d"}
+    st = d["comm"]["sweep_stats"]
+    assert st["arms_run"] == ["c10d"] and not st["arms_skipped"] and not st["arms_failed"]
+    assert 0 < st["wall_s"] <= st["budget_s"]
 
 
 def test_bench_refuses_more_gpus_than_visible():
@@ -179,7 +183,7 @@ def test_comm_plan_picks_protocol():
     assert "protocol Simple" in p["reason"]
     rows.append(_prow("native", 64, 150, ch=0, proto="Simple", wire="bf16"))
     g = 6550 * 2**20
-    assert plan(rows, g, backward_ms=1.0)["wire"] == "bf16"
+    assert plan(rows, g, backward_ms=1.0, auto_bf16=True)["wire"] == "bf16"
     # RCCL's own protocol choice wins when nothing forced beats it
     rows = [_prow("c10d", 64, 100), _prow("native", 64, 160, ch=0), _prow("native", 64, 150, ch=0, proto="LL128")]
     assert plan(rows, grad_bytes=1)["proto"] == ""
@@ -199,25 +203,66 @@ def test_comm_plan_picks_algorithm():
     # the bf16 wire is looked up on the winning (channels, protocol, algorithm) arm only
     rows = [_prow("c10d", 64, 100), _prow("native", 64, 155, ch=0, algo="Ring"),
             _prow("native", 64, 150, ch=0, wire="bf16")]
-    assert plan(rows, 6550 * 2**20, backward_ms=1.0)["wire"] == "fp32"
+    assert plan(rows, 6550 * 2**20, backward_ms=1.0, auto_bf16=True)["wire"] == "fp32"
 
 
 def test_comm_plan_bf16_wire_only_when_exposed():
-    """bf16 wire only when the predicted fp32 all-reduce of the whole gradient exceeds the backward
-    and the bf16 arm is correct and clearly faster."""
+    """bf16 wire recommended only when the predicted fp32 all-reduce of the whole gradient exceeds
+    the backward and the bf16 arm is correct and clearly faster; APPLIED only with auto_bf16 (ADVICE
+    r4: the default wire stays the reference DDP's fp32)."""
     from penroz.parallel.commtune import plan
     rows = [_prow("c10d", 64, 100), _prow("c10d", 64, 100, wire="bf16")]
     g = 6550 * 2**20  # GPT-2 XL fp32 gradients
     fp32_ms = g / (100 * 8 / 14 * 1e9) * 1e3
-    assert plan(rows, g, backward_ms=fp32_ms * 2)["wire"] == "fp32"     # hidden behind the backward
-    p = plan(rows, g, backward_ms=fp32_ms / 2)
+    P = lambda r, **kw: plan(r, g, auto_bf16=True, **kw)
+    assert P(rows, backward_ms=fp32_ms * 2)["wire"] == "fp32"     # hidden behind the backward
+    p = P(rows, backward_ms=fp32_ms / 2)
     assert p["wire"] == "bf16" and abs(p["predicted_bf16_ms"] * 2 - p["predicted_fp32_ms"]) < 0.01
-    assert plan(rows, g, backward_ms=None)["wire"] == "fp32"            # no estimate, no change
+    assert P(rows, backward_ms=None)["wire"] == "fp32"            # no estimate, no change
     bad = [_prow("c10d", 64, 100), _prow("c10d", 64, 100, wire="bf16", ok=False)]
-    assert plan(bad, g, backward_ms=1.0)["wire"] == "fp32"              # wrong bf16 sums
+    assert P(bad, backward_ms=1.0)["wire"] == "fp32"              # wrong bf16 sums
     slow = [_prow("c10d", 64, 100), _prow("c10d", 64, 40, wire="bf16")]
-    assert plan(slow, g, backward_ms=1.0)["wire"] == "fp32"             # bf16 not faster overall
+    assert P(slow, backward_ms=1.0)["wire"] == "fp32"             # bf16 not faster overall
     assert plan([], g)["transport"] == "c10d"
+    # default: recorded, never applied
+    q = plan(rows, g, backward_ms=fp32_ms / 2)
+    assert q["wire"] == "fp32" and q["wire_recommendation"] == "bf16"
+    assert plan(rows, g, backward_ms=fp32_ms * 2)["wire_recommendation"] == "fp32"
+
+
+def test_parse_rccl_log_nranks_and_channels():
+    """rccl.nranks / coll_channels come from what RCCL itself logged at init."""
+    from penroz.parallel.commtune import parse_rccl_log
+    text = ("host:1:1 [0] NCCL INFO Channel 00/16 :    0   1   2   3   4   5   6   7\n"
+            "host:1:1 [0] NCCL INFO 16 coll channels, 16 collnet channels, 0 nvls channels\n"
+            "host:1:1 [0] NCCL INFO comm 0x5581 rank 0 nranks 8 cudaDev 0 busId 5000 - Init COMPLETE\n")
+    assert parse_rccl_log(text) == {"coll_channels": 16, "nranks": 8}
+    assert parse_rccl_log("nothing here") == {"coll_channels": None, "nranks": None}
+    assert parse_rccl_log("ncclCommInitRank comm 0x1 rank 3 nRanks 4 nNodes 1")["nranks"] == 4
+
+
+def test_sweep_arms_default_is_rccl_only(monkeypatch):
+    """the forced channel / protocol / algorithm arms are opt-in."""
+    from penroz.parallel import commtune
+    monkeypatch.delenv("PENROZ_COMM_SWEEP_ARMS", raising=False)
+    assert commtune.sweep_arms() == ((0,), ("",), ("",))
+    monkeypatch.setenv("PENROZ_COMM_SWEEP_ARMS", "full")
+    assert commtune.sweep_arms() == (commtune.SWEEP_CHANNELS, commtune.SWEEP_PROTOS, commtune.SWEEP_ALGOS)
+
+
+def test_comm_plan_identical_for_identical_rows():
+    """The plan is a pure function of the (MAX/MIN-reduced, hence identical) sweep rows: shuffled row
+    order on another rank gives the same plan."""
+    import random
+    from penroz.parallel.commtune import plan
+    rows = [_prow("c10d", mb, 90 + mb / 8) for mb in (16, 32, 64, 128)] + \
+           [_prow("native", mb, 80 + mb / 4, ch=0) for mb in (16, 32, 64, 128)] + \
+           [_prow("c10d", 64, 120, wire="bf16"), _prow("native", 64, 130, ch=0, wire="bf16")]
+    ref = plan(rows, 652 * 2**20, backward_ms=3.0)
+    for seed in range(5):
+        r = list(rows)
+        random.Random(seed).shuffle(r)
+        assert plan(r, 652 * 2**20, backward_ms=3.0) == ref
 
 
 def test_comm_bucket_choice_rule(monkeypatch):
