@@ -4,6 +4,7 @@
 #   bash bench/gpu.sh tests [-k EXPR]        GPU tests only (optionally a subset)
 #   bash bench/gpu.sh bench [bench.py args]  headline bench (default 20 timed / 5 warmup steps)
 #   bash bench/gpu.sh ab "VAR=a" "VAR=b"     same-box A/B of the headline bench, two passes
+#                                            (any arms x workloads: python bench/ab.py --help)
 #   bash bench/gpu.sh prof [tag] [-- cmd]    rocprofv3 kernel trace + per-step summary (default cmd:
 #                                            the headline bench, 3 warmup + 5 timed steps)
 #   bash bench/gpu.sh pmc tag KERNELS -- cmd  the standard PMC passes (timing/LDS, instruction mix,
@@ -45,13 +46,9 @@ case $cmd in
   tests) tests "$@" ;;
   bench) bench "$@" ;;
   ab)
-    for i in 1 2; do
-      for e in "$@"; do
-        env $e timeout -k 10 200 python bench.py --steps 20 --warmup 5 --ref-steps 0 > gpurun_out/ab.log 2>&1 \
-          || { tail -20 gpurun_out/ab.log; exit 1; }
-        echo "$e $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/ab.log)"
-      done
-    done ;;
+    args=(); i=0
+    for e in "$@"; do args+=(--arm "arm$i:$e"); i=$((i+1)); done
+    timeout -k 10 1000 python bench/ab.py "${args[@]}" --work headline --log gpurun_out/ab.jsonl || exit 1 ;;
   prof)
     tag=${1:-prof}; shift || true
     steps=8

@@ -2,6 +2,7 @@
 import json
 import os
 import stat
+import sys
 
 import pytest
 
@@ -328,3 +329,19 @@ def test_bench_rank_failure_stops_group():
     r = _run_bench(["--gpus", "2", "--device", "cpu", "--model", "tiny", "--steps", "1", "--warmup", "0",
                     "--seq", "4096"], timeout=120)
     assert r.returncode != 0
+
+
+def test_ab_tool_arms_and_workloads():
+    """bench/ab.py: arm specs parse to env dicts; every workload kind maps to a bounded command."""
+    sys.path.insert(0, os.path.join(ROOT, "bench"))
+    import ab
+    assert ab.parse_arm("base:PENROZ_EXT_DIR=build_ab X=1") == ("base", {"PENROZ_EXT_DIR": "build_ab", "X": "1"})
+    assert ab.parse_arm("new:") == ("new", {})
+    with pytest.raises(SystemExit):
+        ab.parse_arm("bad:NOVALUE")
+    cmd, lim = ab.work_cmd("headline", 20, 5)
+    assert cmd[1:] == ["bench.py", "--steps", "20", "--warmup", "5", "--ref-steps", "0"] and lim > 0
+    assert ab.work_cmd("gemma3-1b:8", 20, 5)[0][-2:] == ["--batch", "8"]
+    assert ab.work_cmd("decode:gpt2:1", 20, 5)[0][-4:] == ["--model", "gpt2", "--batch", "1"]
+    assert "--D" in ab.work_cmd("attn:--B 4 --D 64", 20, 5)[0]
+    assert ab.headline_number('noise\n{"ms_per_step": 61.2, "value": 1.0, "x": 3}\n') == {"ms_per_step": 61.2, "value": 1.0}
