@@ -104,6 +104,13 @@ MODELS = {
     # head_dim 256, gated GELU MLP, 262k vocab; random init, no checkpoint): the generic engine
     # (autograd over the HIP layers: flash attention D=256, RMSNorm, gated activation)
     "gemma3-1b": dict(V=262144, C=1152, L=26, H=4, P=32768, gemma=True, Hkv=1, D=256, F=6912),
+    # a Gemma-4-class layer list through the reference's heterogeneous-layer mapping
+    # (mappers.py:206-233; the E2B-sized text stack is not published offline, so the shape is
+    # synthetic): sliding (head_dim 256) and full-attention (global_head_dim 512, one global KV
+    # head) layers alternating, the last 8 layers KV-shared with double-wide gated MLPs,
+    # 262k vocab, tied embedding. Exercises the D = 512 flash kernels in the fused executor.
+    "gemma4-e2b": dict(V=262144, C=1536, L=20, H=8, P=32768, gemma=True, gemma4=True, Hkv=1, D=256, F=6144,
+                       Dg=512, Hkv_g=1, shared=8),
 }
 
 
@@ -115,6 +122,28 @@ def gemma3_1b_layers(L: int = 26) -> list[dict]:
         num_attention_heads=4, num_key_value_heads=1, head_dim=256, rms_norm_eps=1e-6, rope_theta=1e6,
         rope_local_base_freq=10000.0, attention_dropout=0.0, hidden_activation="gelu_pytorch_tanh",
         query_pre_attn_scalar=256, sliding_window=512))
+
+
+def gemma4_config(cfg: dict):
+    """The HF-style text config of a ``gemma4=True`` MODELS entry (Mapper.from_hf_config input)."""
+    from types import SimpleNamespace
+    return SimpleNamespace(
+        model_type="gemma4_text", vocab_size=cfg["V"], hidden_size=cfg["C"], intermediate_size=cfg["F"],
+        num_hidden_layers=cfg["L"], num_attention_heads=cfg["H"], num_key_value_heads=cfg["Hkv"],
+        head_dim=cfg["D"], global_head_dim=cfg["Dg"], num_global_key_value_heads=cfg["Hkv_g"],
+        layer_types=["sliding_attention", "full_attention"] * (cfg["L"] // 2) + ["sliding_attention"] * (cfg["L"] % 2),
+        num_kv_shared_layers=cfg["shared"], use_double_wide_mlp=True, rms_norm_eps=1e-6, rope_theta=1e6,
+        attention_dropout=0.0, hidden_activation="gelu_pytorch_tanh", query_pre_attn_scalar=cfg["D"])
+
+
+def gemma_layer_shapes(cfg: dict) -> list[tuple[int, int, int]]:
+    """Per layer (head_dim, KV heads, MLP width) of a gemma MODELS entry."""
+    if not cfg.get("gemma4"):
+        return [(cfg["D"], cfg["Hkv"], cfg["F"])] * cfg["L"]
+    g = gemma4_config(cfg)
+    first_shared = cfg["L"] - cfg["shared"]
+    return [((cfg["Dg"], cfg["Hkv_g"]) if t == "full_attention" else (cfg["D"], cfg["Hkv"]))
+            + ((2 * cfg["F"]) if i >= first_shared else cfg["F"],) for i, t in enumerate(g.layer_types)]
 
 
 def hf_gpt2_layers(V, C, L, H, P, pdrop=0.1):
@@ -272,9 +301,10 @@ def _grad_plan_inputs(args) -> tuple[int, float]:
     Gemma: the layer list's linears), backward ≈ 2/3 of 6·params·tokens at a planning 1.0 PF/s."""
     cfg = MODELS[args.model]
     C, L, V = cfg["C"], cfg["L"], cfg["V"]
-    if cfg.get("gemma"):  # q, o: H·D·C each; k, v: Hkv·D·C each; gate, up, down: C·F each; tied embedding
-        D, Hkv, F = cfg["D"], cfg["Hkv"], cfg["F"]
-        n = L * (C * (2 * cfg["H"] * D + 2 * Hkv * D) + 3 * C * F) + V * C
+    if cfg.get("gemma"):  # q, o: H·D·C each; k, v: Hkv·D·C each; gate, up, down: C·F each; 4 RMSNorms per
+        # layer + the final one; embedding + lm_head
+        n = sum(C * (2 * cfg["H"] * D + 2 * Hkv * D) + 3 * C * F + 4 * C for D, Hkv, F in gemma_layer_shapes(cfg))
+        n += 2 * V * C + C
     else:
         n = L * (12 * C * C + 13 * C) + 2 * V * C + cfg["P"] * C + 2 * C
     tokens = args.batch * args.seq
@@ -372,7 +402,10 @@ def _build(args, cfg, device, engine, world):
     os.environ["PENROZ_ENGINE"] = engine
     torch.manual_seed(1234)
     dims = {k: cfg[k] for k in ("V", "C", "L", "H", "P")}
-    if cfg.get("gemma"):
+    if cfg.get("gemma4"):
+        from penroz.models.mapper import Mapper
+        layers = Mapper.from_hf_config(gemma4_config(cfg))
+    elif cfg.get("gemma"):
         layers = gemma3_1b_layers(cfg["L"])
     else:
         layers = hf_gpt2_layers(**dims) if cfg.get("hf") else gpt2_layers(**dims)
@@ -555,7 +588,7 @@ def run_rank(args):
 
     if rank == 0:
         if cfg.get("gemma"):  # matmul weights (tied lm_head counted as the Linear it is) + attention
-            flops_per_tok = 6 * n_linear + 12 * cfg["L"] * cfg["H"] * 256 * T
+            flops_per_tok = 6 * n_linear + sum(12 * cfg["H"] * D * T for D, _, _ in gemma_layer_shapes(cfg))
         else:
             flops_per_tok = 6 * (n_params - cfg["V"] * cfg["C"] - cfg["P"] * cfg["C"]) + 12 * cfg["L"] * cfg["C"] * T
         print(json.dumps({

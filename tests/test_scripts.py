@@ -345,3 +345,24 @@ def test_ab_tool_arms_and_workloads():
     assert ab.work_cmd("decode:gpt2:1", 20, 5)[0][-4:] == ["--model", "gpt2", "--batch", "1"]
     assert "--D" in ab.work_cmd("attn:--B 4 --D 64", 20, 5)[0]
     assert ab.headline_number('noise\n{"ms_per_step": 61.2, "value": 1.0, "x": 3}\n') == {"ms_per_step": 61.2, "value": 1.0}
+
+
+def test_bench_gemma4_config_shapes():
+    """The Gemma-4-class bench config: alternating D = 256 sliding / D = 512 full-attention layers,
+    double-wide MLPs on the KV-shared tail; it lowers to the fused Gemma executor and the gradient
+    plan counts its parameters."""
+    import torch
+    import bench
+    from penroz.models.gemma_executor import GemmaExecutor
+    from penroz.models.mapper import Mapper
+    from penroz.models.model import NeuralNetworkModel
+    cfg = bench.MODELS["gemma4-e2b"]
+    shapes = bench.gemma_layer_shapes(cfg)
+    assert shapes[0] == (256, 1, 6144) and shapes[1] == (512, 1, 6144) and shapes[-1] == (512, 1, 12288)
+    with torch.device("meta"):
+        m = NeuralNetworkModel("g4", Mapper(Mapper.from_hf_config(bench.gemma4_config(cfg)), {"adamw": {}}))
+    spec = GemmaExecutor.match(m)
+    assert spec is not None and [(b.D, b.Hkv, b.F) for b in spec.blocks] == shapes
+    args = bench.parse_args(["--model", "gemma4-e2b", "--batch", "8"])
+    grad_bytes, _ = bench._grad_plan_inputs(args)
+    assert grad_bytes == 4 * sum(p.numel() for p in m.parameters())
