@@ -176,6 +176,9 @@ def parse_args(argv=None):
     ap.add_argument("--no-comm-sweep", dest="comm_sweep", action="store_false",
                     help="world > 1: skip the first-contact all-reduce sweep (bucket size x wire x transport) "
                          "that picks the gradient transport before the timed run")
+    ap.add_argument("--no-gemm-table-guard", dest="gemm_table_guard", action="store_false",
+                    help="skip the pre-timing check that keeps the shipped GEMM solution table only if it is not "
+                         "slower than hipBLASLt's heuristic on this step (reported as gemm_table)")
     ap.add_argument("--via-runtime", action="store_true",
                     help="also time the same config through NeuralNetworkModel.train_model (Loader over synthetic "
                          "shards, per-epoch diagnostics, checkpoints) and report its tokensPerSec progress figure")
@@ -538,6 +541,11 @@ def run_rank(args):
 
     for i in range(args.warmup):
         step(i)
+    gemm_table = {}
+    if device.type == "cuda" and args.gemm_table_guard:  # before the timed region, never inside it
+        from penroz.ops import gemm as gemm_ops
+        # _timed MAX-reduces over ranks, so every rank keeps or drops the table together
+        gemm_table = gemm_ops.guard_tuned_gemms(lambda n: _timed(step, n, world, device)[0])
     dt, loss = _timed(step, args.steps, world, device)
     ms = dt / args.steps * 1e3
     tok_s = world * B * T * args.steps / dt
@@ -602,6 +610,7 @@ def run_rank(args):
             "dtype": "bf16" if device.type == "cuda" else "fp32",
             "data": "synthetic uniform tokens, random-init weights",
             "comm": comm,
+            **({"gemm_table": gemm_table} if gemm_table else {}),
             **({"via_runtime": runtime} if runtime is not None else {}),
             "config": {"model": args.model, "global_batch": world * B, "seq_len": T, "micro_batch_per_gpu": B,
                        "tokens_per_step": world * B * T, "parallelism": f"dp{world}"},

@@ -91,6 +91,7 @@ void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad, int64_t t
 void flash_attn_fwd(torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int64_t H, int64_t Hkv, int64_t D,
                     double scale, double p_drop, int64_t seed);
 int64_t flash_fwd_variant(int64_t v);
+void flash_bwd_stamps(c10::optional<torch::Tensor> buf);
 void flash_attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, torch::Tensor dqkv,
                     int64_t H, int64_t Hkv, int64_t D, double scale, double p_drop, int64_t seed,
                     c10::optional<torch::Tensor> dbias);
@@ -195,6 +196,8 @@ PYBIND11_MODULE(penroz_kernels, m) {
         pybind11::arg("lse"), pybind11::arg("dqkv"), pybind11::arg("H"), pybind11::arg("Hkv"), pybind11::arg("D"),
         pybind11::arg("scale"), pybind11::arg("p_drop"), pybind11::arg("seed"), pybind11::arg("dbias") = pybind11::none(),
         "causal flash-attention backward (head_dim 64) into dqkv; dbias += column sums of dqkv when given");
+  m.def("flash_bwd_stamps", &flash_bwd_stamps, pybind11::arg("buf") = pybind11::none(),
+        "diagnostic: s_memtime phase sums of the dK/dV kernel into an int64 [6] GPU tensor (None: off)");
   m.def("flash_attn_gen_fwd", &flash_attn_gen_fwd, "causal flash attention forward, head_dim 128 / 256");
   m.def("flash_attn_gen_bwd", &flash_attn_gen_bwd, "causal flash attention backward, head_dim 128 / 256");
 }

@@ -156,7 +156,6 @@ __device__ __forceinline__ void xcd_head_block(int& blk, int& head) {
   }
 }
 
-
 // Bias-gradient partial of one wave's 32 rows (on lanes lane&31) of a 64-column head slice held in
 // MFMA accumulators: acc[dh][i] is column 32·dh + 8·(i>>2) + 4·(lane>>5) + (i&3). Each value is
 // scaled by `mul` and rounded to bf16 exactly as the kernel stores it (so the sums equal the

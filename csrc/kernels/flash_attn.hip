@@ -513,13 +513,37 @@ __device__ __forceinline__ void ring_tail(F&& f, int base, int total, std::integ
 
 // GC: the query-group size H/Hkv when known at compile time (1: multi-head attention — the
 // slice counter then maps to (head, slice) without the per-iteration division), 0 = any
-template <bool DROPOUT, int NST, int GC>
+// x as two bf16 (hi = bf16(x), lo = bf16(x − hi)) packed in the low / high halves of a word: the
+// k = 0 / 1 elements of a fold operand — an MFMA against a "ones" operand adds hi + lo = x to within
+// 2^-16 relative, exactly in its fp32 accumulator
+__device__ __forceinline__ uint32_t bf16_hilo(float x) {
+  const float hi = __bfloat162float(__float2bfloat16(x));
+  return pack_bf16x2(hi, x - hi);
+}
+
+// STAMP (diagnostic build only, flash_bwd_stamps): s_memtime brackets around the phases of every
+// ring iteration, summed per wave and added into stamps[0..5] (DMA issue, S/dP MFMA issue, softmax-
+// gradient + dV/dK, DMA wait, barrier, iterations); sched_barrier(0) pins each bracket, so the
+// instrumented schedule differs slightly from the production one
+template <bool DROPOUT, int NST, int GC, bool STAMP = false>
 __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv3_kernel(const bf16* __restrict__ qkv,
                                                               const bf16* __restrict__ dout,
                                                               const float* __restrict__ lse,
                                                               const float* __restrict__ delta,
                                                               bf16* __restrict__ dqkv, float* __restrict__ cpart, int T, int H, int Hkv,
-                                                              float scale, float p_drop, uint64_t seed) {
+                                                              float scale, float p_drop, uint64_t seed,
+                                                              unsigned long long* __restrict__ stamps = nullptr,
+                                                              int diag = 0) {
+  unsigned long long st_acc[5] = {0, 0, 0, 0, 0}, st_n = 0, st_t = 0;
+  auto stamp = [&](int seg) {
+    if constexpr (STAMP) {
+      __builtin_amdgcn_sched_barrier(0);
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      if (seg >= 0) st_acc[seg] += now - st_t;
+      st_t = now;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
   constexpr int BK = 128, QS = 64;
   constexpr int TILE = QS * 128;              // one 64-row slice, 128-B rows
   constexpr int STAGE = 2 * TILE + 512;       // Q | dO | LSE[64] | δ[64]
@@ -558,6 +582,10 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv3_kernel(const bf16* __rest
   for (int dh = 0; dh < 2; ++dh)
 #pragma unroll
     for (int i = 0; i < 16; ++i) dk[dh][i] = dv[dh][i] = 0.f;
+  // fold operands (k = 0 / 1 live in the first half-wave's lanes only): ones = 1.0 at k = 0 and 1
+  const uint32_t lo_lane = hh == 0 ? 0xFFFFFFFFu : 0u;
+  const uint4 onesf = uint4{0x3F803F80u & lo_lane, 0u, 0u, 0u};
+  const f32x16 zacc = {};
 
   // per-lane LDS byte offsets: row reads (row lane&31, chunk 2s+hh) and transposed reads (rows
   // 4hh+q and 8+4hh+q, columns 32dh + 16((lane>>4)&1) + 4p); tile_off(r0 + x, ch) = 128·r0 +
@@ -596,7 +624,10 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv3_kernel(const bf16* __rest
     voff[par] = (unsigned)(lane >> 3) * rsb + 16u * ch;
   }
   auto dma = [&](int it) {
-    const int itc = min(it, total - 1);  // beyond the end: refetch the last slice (uniform counts)
+    // (STAMP diagnostics, wrong results: diag 2 = no DMA at all, diag 1 = every DMA refetches the
+    // first slice — cache-hot sources)
+    if (STAMP && diag == 2) return;
+    const int itc = (STAMP && diag == 1) ? 0 : min(it, total - 1);  // beyond the end: refetch the last slice
     const int hq = GC == 1 ? hk : hk * G + itc / per_head;
     const int qs0 = (s_first + (GC == 1 ? itc : itc % per_head)) * QS;
     const unsigned st = __builtin_amdgcn_readfirstlane(lds_addr_of(smem + (it % NST) * STAGE));
@@ -629,7 +660,6 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv3_kernel(const bf16* __rest
     else
       RingWait<NST>::template wait<4>();
   };
-
   if (total > 0) {
 #pragma unroll
     for (int i = 0; i < NST - 1; ++i) dma(i);
@@ -638,7 +668,9 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv3_kernel(const bf16* __rest
   __syncthreads();
   auto iter = [&](int it, auto stage_tag) {
     constexpr int ST = decltype(stage_tag)::value;
+    stamp(-1);
     dma(it + NST - 1);  // into the stage consumed at it-1 (freed by its barrier)
+    stamp(0);
     const char* stg = smem + ST * STAGE;
     const float* lse_s = reinterpret_cast<const float*>(stg + 2 * TILE);
     const float* del_s = lse_s + QS;
@@ -653,23 +685,26 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv3_kernel(const bf16* __rest
       if (act[half]) {
         const char* Qt = stg + half * 32 * 128;
         const char* Dt = stg + TILE + half * 32 * 128;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const float4_t dl = *reinterpret_cast<const float4_t*>(&del_s[32 * half + 8 * g + 4 * hh]);
-          const float4_t l2 = *reinterpret_cast<const float4_t*>(&lse_s[32 * half + 8 * g + 4 * hh]) * kLog2e;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            sp[half][4 * g + k] = -l2[k];  // S accumulates onto −LSE·log2(e): P = exp2(S)
-            dp[half][4 * g + k] = DROPOUT ? 0.f : -dl[k];
-          }
-        }
-        // all 8 operand fragments requested first, then the 8 MFMAs: one LDS latency per half
+        // all 8 operand fragments requested first, then the MFMAs: one LDS latency per half
         // instead of one per MFMA pair
         uint4 qa[4], da[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           qa[s] = rowf(Qt, s);
           da[s] = rowf(Dt, s);
+        }
+        // row constants folded into the chains: S starts at −LSE·log2(e) (P = exp2(S)) and dP at −δ
+        // of each query row — one MFMA each against the ones operand (this lane's row = lane&31
+        // supplies k = 0 / 1 as a bf16 hi + lo pair) instead of 32 per-register moves
+        const int r = 32 * half + (lane & 31);
+        const uint4 lfold = uint4{bf16_hilo(-lse_s[r] * kLog2e) & lo_lane, 0u, 0u, 0u};
+        sp[half] = mfma32(lfold, onesf, zacc);
+        if constexpr (DROPOUT) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) dp[half][i] = 0.f;
+        } else {
+          const uint4 dfold = uint4{bf16_hilo(-del_s[r]) & lo_lane, 0u, 0u, 0u};
+          dp[half] = mfma32(dfold, onesf, zacc);
         }
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
@@ -678,6 +713,7 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv3_kernel(const bf16* __rest
         }
       }
     }
+    stamp(1);
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
       const int qh0 = qs0 + 32 * half;
@@ -688,8 +724,9 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv3_kernel(const bf16* __rest
         const uint32_t drow0 = DROPOUT ? (uint32_t)((b * H + hq) * T + qh0 + 4 * hh) * kDropRowMul : 0u;
         // the dV / dK operand fragments (transposed reads) go out before the softmax-gradient VALU
         // (not with dropout: its hash registers leave no room — 42 spilled — so it reads at use)
+        constexpr bool HOIST = !DROPOUT;
         uint4 tdo[2][2], tqq[2][2];
-        if constexpr (!DROPOUT) {
+        if constexpr (HOIST) {
 #pragma unroll
           for (int ss = 0; ss < 2; ++ss)
 #pragma unroll
@@ -731,19 +768,30 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dkdv3_kernel(const bf16* __rest
           const uint4 pf = acc_frag(sp[half], ss), sf = acc_frag(dp[half], ss);
 #pragma unroll
           for (int dh = 0; dh < 2; ++dh) {
-            dv[dh] = mfma32(DROPOUT ? trf(Dt + 16 * ss * 128, dh) : tdo[ss][dh], pf, dv[dh]);
-            dk[dh] = mfma32(DROPOUT ? trf(Qt + 16 * ss * 128, dh) : tqq[ss][dh], sf, dk[dh]);
+            dv[dh] = mfma32(HOIST ? tdo[ss][dh] : trf(Dt + 16 * ss * 128, dh), pf, dv[dh]);
+            dk[dh] = mfma32(HOIST ? tqq[ss][dh] : trf(Qt + 16 * ss * 128, dh), sf, dk[dh]);
           }
         }
       }
     }
+    stamp(2);
     wait_next();
+    stamp(3);
     __syncthreads();
+    stamp(4);
+    if constexpr (STAMP) ++st_n;
   };
   int it = 0;
   for (; it + NST <= total; it += NST) ring_unroll(iter, it, std::make_integer_sequence<int, NST>{});
   ring_tail(iter, it, total, std::make_integer_sequence<int, NST - 1>{});
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (STAMP) {
+    if (lane == 0) {
+#pragma unroll
+      for (int i = 0; i < 5; ++i) atomicAdd(stamps + i, st_acc[i]);
+      atomicAdd(stamps + 5, st_n);
+    }
+  }
   if (cpart != nullptr) {  // qkv-bias gradient: this wave's dK / dV column sums (one partial row)
     float* prow = cpart + (((size_t)b * gridDim.x + kb) * 4 + w) * RS;
     colsum32_wave(dk, scale, key < T, prow + (size_t)(H + hk) * kD);
@@ -838,6 +886,14 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dq4_kernel(const bf16* __restri
     launder(dof[s]);
   }
   asm volatile("" : "+v"(l2), "+v"(dl));
+  // the S / dP accumulator starts (−LSE·log2 e and −δ of this lane's query row) as loop-invariant
+  // register blocks: each chain's first MFMA reads its C operand from them, so no per-tile moves
+  f32x16 s_init, dp_init;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    s_init[i] = -l2;
+    dp_init[i] = DROPOUT ? 0.f : -dl;
+  }
 
   // LDS-DMA ring (3 stages, two tiles ahead): waves 0-1 fetch the K tile, waves 2-3 the V
   // tile, 4 pieces (8 keys x 128 B each) per wave, tile_off image
@@ -911,19 +967,17 @@ __global__ void __launch_bounds__(256, 2) fa_bwd_dq4_kernel(const bf16* __restri
       f32x16 s[2], dp[2];
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          s[kh][i] = -l2;  // S accumulates onto −LSE·log2(e) of this lane's query row: P = exp2(S)
-          dp[kh][i] = DROPOUT ? 0.f : -dl;
-        }
         uint4 ka[4], va[4];  // fragments first, then the MFMAs (one LDS latency per 32 keys)
 #pragma unroll
         for (int st = 0; st < 4; ++st) {
           ka[st] = rowf(Kt + 32 * kh * 128, st);
           va[st] = rowf(Vt + 32 * kh * 128, st);
         }
+        // S accumulates onto −LSE·log2(e) of this lane's query row (P = exp2(S)), dP onto −δ
+        s[kh] = mfma32(ka[0], qf[0], s_init);
+        dp[kh] = mfma32(va[0], dof[0], dp_init);
 #pragma unroll
-        for (int st = 0; st < 4; ++st) {
+        for (int st = 1; st < 4; ++st) {
           s[kh] = mfma32(ka[st], qf[st], s[kh]);
           dp[kh] = mfma32(va[st], dof[st], dp[kh]);
         }
@@ -1036,6 +1090,17 @@ int64_t flash_fwd_variant(int64_t v) {
 // dbias (optional, fp32 [(H + 2·Hkv)·D]): += the column sums of dqkv over all B·T rows (the fused
 // QKV projection's bias gradient), produced in the dK/dV and dQ epilogues (one fp32 partial row
 // per 32-row wave slice, finished by the deferred reduction).
+// diagnostic: when set (uint64 [6] on the GPU), the MHA no-dropout dK/dV launch runs the STAMP build
+static unsigned long long* g_fa_stamps = nullptr;
+void flash_bwd_stamps(c10::optional<torch::Tensor> buf) {
+  if (buf.has_value() && buf->defined()) {
+    TORCH_CHECK(buf->is_cuda() && buf->scalar_type() == torch::kInt64 && buf->numel() >= 6 && buf->is_contiguous());
+    g_fa_stamps = reinterpret_cast<unsigned long long*>(buf->data_ptr());
+  } else {
+    g_fa_stamps = nullptr;
+  }
+}
+
 void flash_attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, torch::Tensor dqkv,
                     int64_t H, int64_t Hkv, int64_t D, double scale, double p_drop, int64_t seed,
                     c10::optional<torch::Tensor> dbias) {
@@ -1064,18 +1129,25 @@ void flash_attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, to
   bf16* g = reinterpret_cast<bf16*>(dqkv.data_ptr());
   dim3 gkv((T + 127) / 128, B * Hkv), gq((T + 127) / 128, B * H);
   using BwdKernel = void (*)(const bf16*, const bf16*, const float*, const float*, bf16*, float*, int, int, int, float, float,
-                            uint64_t);
+                            uint64_t, unsigned long long*, int);
   using DqKernel = void (*)(const bf16*, const bf16*, const float*, float*, bf16*, float*, int, int, int, float, float,
                             uint64_t, const bf16*);
   const bool drop = p_drop > 0.0;
   BwdKernel kv;
   DqKernel dq;
-  if (H == Hkv)
+  if (H == Hkv && !drop && g_fa_stamps)
+    kv = fa_bwd_dkdv3_kernel<false, 3, 1, true>;
+  else if (H == Hkv)
     kv = drop ? fa_bwd_dkdv3_kernel<true, 3, 1> : fa_bwd_dkdv3_kernel<false, 3, 1>;
   else
     kv = drop ? fa_bwd_dkdv3_kernel<true, 3, 0> : fa_bwd_dkdv3_kernel<false, 3, 0>;
   dq = drop ? fa_bwd_dq4_kernel<true, 3> : fa_bwd_dq4_kernel<false, 3>;
   const float pd = drop ? (float)p_drop : 0.f;
+  // (STAMP diagnostics only: PENROZ_FA_STAMP_DIAG=1 cache-hot DMA sources, 2 no DMA)
+  static const int kv_diag = [] {
+    const char* e = std::getenv("PENROZ_FA_STAMP_DIAG");
+    return e ? std::atoi(e) : 0;
+  }();
   const bool want_bias = dbias.has_value() && dbias->defined();
   const int W = (int)((H + 2 * Hkv) * D), nblk = (T + 127) / 128;
   if (want_bias)
@@ -1088,7 +1160,7 @@ void flash_attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, to
                      (int)H, (int)Hkv, (float)scale, pd, (uint64_t)seed,
                      prepass ? nullptr : reinterpret_cast<const bf16*>(out.data_ptr()));
   hipLaunchKernelGGL(kv, gkv, dim3(256), 0, stream, q, d, lse.data_ptr<float>(), delta.data_ptr<float>(), g, pp, T,
-                     (int)H, (int)Hkv, (float)scale, pd, (uint64_t)seed);
+                     (int)H, (int)Hkv, (float)scale, pd, (uint64_t)seed, g_fa_stamps, kv_diag);
   if (want_bias) {
     float* outs[1] = {dbias->data_ptr<float>()};
     reduce_partials_auto(part, 1, B * nblk * 4, W, outs, stream);

@@ -91,6 +91,40 @@ def load_tuned_gemms() -> bool:
     return ok
 
 
+def set_tuned_gemms(on: bool) -> bool:
+    """Switch the loaded table's solutions on or off at run time (off: hipBLASLt's own heuristic
+    for every shape). Returns whether the table is now in use."""
+    if not _tuned_state.get("loaded"):
+        return False
+    import torch.cuda.tunable as tunable
+    tunable.enable(bool(on))
+    _tuned_state["active"] = bool(on)
+    return bool(on)
+
+
+def guard_tuned_gemms(run_steps, steps: int = 3, rounds: int = 2, margin: float = 1.0, agree=None) -> dict:
+    """The shipped table must never cost time (it once drifted to 1 ms/step SLOWER than
+    hipBLASLt's heuristic and nothing noticed). Times ``run_steps(steps)`` (returns seconds) with the
+    table off and on, ``rounds`` interleaved times each, keeps the table only if its best time is
+    <= ``margin`` × the heuristic's best, and leaves that choice switched on. ``agree`` (optional)
+    maps a local time to the group's (MAX over ranks) so every rank decides the same.
+    {} when no table is loaded."""
+    if not _tuned_state.get("loaded"):
+        return {}
+    best = {False: float("inf"), True: float("inf")}
+    for _ in range(rounds):
+        for on in (False, True):
+            set_tuned_gemms(on)
+            dt = run_steps(steps)
+            if agree is not None:
+                dt = agree(dt)
+            best[on] = min(best[on], dt / steps)
+    keep = best[True] <= margin * best[False]
+    set_tuned_gemms(keep)
+    return {"table": os.path.basename(TUNED_GEMM_FILE), "with_table_ms": round(best[True] * 1e3, 3),
+            "heuristic_ms": round(best[False] * 1e3, 3), "table_kept": keep}
+
+
 # ---- linear + GELU / GELU backward (library GEMM + the HIP GELU kernels) -------------------
 # Two native fused designs were built and measured against this pair (round 3-4): an 8-phase
 # persistent MFMA GEMM with a bias/GELU epilogue and a 4-wave deferred-epilogue GEMM whose

@@ -324,6 +324,64 @@ def test_flash_fwd(B, T, H, Hkv, variant):
     _close(lse, rl, 2e-3, 1e-4, "lse")
 
 
+@pytest.mark.parametrize("variant", [1, 3])
+@pytest.mark.parametrize("profile", ["grow", "shrink", "spike"])
+def test_flash_fwd_running_max_paths(profile, variant):
+    """The running-max paths on data built to take them (random data almost never does):
+    'grow' — key magnitudes rise along the sequence, so most tiles raise m (fwd4: the tile sum
+    exceeds 2^8 and the rare path recomputes the tile); 'shrink' — the first tile holds the
+    maximum and later tiles' p underflow towards 0; 'spike' — one very large key per 200 in an
+    otherwise flat row (a single p far above the running max). Exercises the deferred-rescale
+    branch (kRescaleThr) of both forward kernels."""
+    torch.manual_seed(1)
+    B, T, H = 2, 640, 3
+    qkv = torch.randn(B, T, 3 * H * 64, device=DEV)
+    t = torch.arange(T, device=DEV, dtype=torch.float32)
+    if profile == "grow":
+        f = 0.2 + 3.0 * t / T
+    elif profile == "shrink":
+        f = 3.2 - 3.0 * t / T
+    else:
+        f = torch.full((T,), 0.3, device=DEV)
+        f[::200] = 6.0
+    qkv[:, :, H * 64:2 * H * 64] *= f.view(1, T, 1)
+    qkv[:, :, :H * 64] *= 2.0
+    qkv = qkv.to(torch.bfloat16)
+    k = _ext.kernels()
+    prev = k.flash_fwd_variant(variant)
+    try:
+        out, lse = A.flash_fwd(qkv, H, H, 64)
+    finally:
+        k.flash_fwd_variant(prev)
+    ro, rl = A.reference_attention_lse(qkv, H, H, 64)
+    _close(out, ro, 0.03, 0.01, "out")
+    _close(lse, rl, 0.02, 1e-3, "lse")
+
+
+def test_flash_bwd_stamps_diagnostic_is_transparent():
+    """The s_memtime phase build of the dK/dV kernel (bench/attn_stamps.py) counts every ring
+    iteration and returns the same gradients as the production build."""
+    torch.manual_seed(0)
+    B, T, H = 2, 384, 4
+    qkv = _qkv(B, T, H, H)
+    out, lse = A.flash_fwd(qkv, H, H, 64)
+    dout = torch.randn_like(out)
+    ref = A.flash_bwd(dout, qkv, out, lse, H, H, 64)
+    k = _ext.kernels()
+    buf = torch.zeros(6, dtype=torch.int64, device=DEV)
+    k.flash_bwd_stamps(buf)
+    try:
+        got = A.flash_bwd(dout, qkv, out, lse, H, H, 64)
+    finally:
+        k.flash_bwd_stamps(None)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+    v = buf.tolist()
+    nblk = T // 128
+    assert v[5] == B * H * 4 * sum(T // 64 - 2 * kb for kb in range(nblk))  # wave iterations
+    assert all(x > 0 for x in v[:5])
+
+
 @pytest.mark.parametrize("B,T,H,Hkv", [(2, 512, 4, 4), (1, 200, 3, 3), (2, 130, 4, 2), (1, 7, 2, 1), (1, 1024, 2, 2),
                                        (1, 320, 4, 1)])
 def test_flash_bwd(B, T, H, Hkv):

@@ -366,3 +366,21 @@ def test_bench_gemma4_config_shapes():
     args = bench.parse_args(["--model", "gemma4-e2b", "--batch", "8"])
     grad_bytes, _ = bench._grad_plan_inputs(args)
     assert grad_bytes == 4 * sum(p.numel() for p in m.parameters())
+
+
+def test_gemm_table_guard_keeps_only_a_faster_table(monkeypatch):
+    """the shipped GEMM table is timed against hipBLASLt's heuristic before the
+    timed region and dropped when slower; the choice is left switched on."""
+    import torch.cuda.tunable as tunable
+    from penroz.ops import gemm as G
+    state = {}
+    monkeypatch.setattr(tunable, "enable", lambda on=True: state.__setitem__("on", on))
+    monkeypatch.setattr(G, "_tuned_state", {"loaded": True})
+    times = {True: 0.060, False: 0.063}
+    r = G.guard_tuned_gemms(lambda n: times[state["on"]] * n, steps=3)
+    assert r["table_kept"] and state["on"] is True and r["with_table_ms"] == 60.0 and r["heuristic_ms"] == 63.0
+    times = {True: 0.0645, False: 0.0635}
+    r = G.guard_tuned_gemms(lambda n: times[state["on"]] * n, steps=3)
+    assert not r["table_kept"] and state["on"] is False
+    monkeypatch.setattr(G, "_tuned_state", {})
+    assert G.guard_tuned_gemms(lambda n: 1.0) == {}
