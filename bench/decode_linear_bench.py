@@ -43,6 +43,28 @@ def main():
     k = kernels()
     M, C = a.rows, 768
     dev = "cuda"
+    if M <= 4:  # the batch-1..4 decode GEMV (decode_gemv), per GPT-2 shape and rows per wave
+        resid = torch.randn(M, C, device=dev)
+        gamma, beta = torch.ones(C, device=dev), torch.zeros(C, device=dev)
+        for name, N, K, ln in (("qkv", 3 * C, C, True), ("fc", 4 * C, C, True), ("proj", C, C, False),
+                               ("fc2", C, 4 * C, False), ("lm_head", 50304, C, True)):
+            nl = 1 if name == "lm_head" else L
+            ws = [torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.02 for _ in range(nl)]
+            x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+            out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            row = {"kernel": "decode_gemv", "shape": name, "M": M, "N": N, "K": K, "ln": ln}
+            for rpw in (2, 4, 8):
+                if ln:
+                    fns = [lambda w=w: k.decode_gemv(None, resid, None, None, None, gamma, beta, 1e-5, w, None, out, 0, rpw)
+                           for w in ws]
+                else:
+                    fns = [lambda w=w: k.decode_gemv(x, None, None, None, None, None, None, 0.0, w, None, out, 0, rpw)
+                           for w in ws]
+                row[f"rpw{rpw}_us"] = round(timeit(fns), 2)
+            print(json.dumps(row), flush=True)
+        z = torch.zeros(1, device=dev)
+        print(json.dumps({"kernel": "torch add_ (1 element)", "us": round(timeit([lambda: z.add_(1.0)] * L), 2)}))
+        return
     resid = torch.randn(M, C, device=dev)
     gamma, beta = torch.ones(C, device=dev), torch.zeros(C, device=dev)
     for name, N, K in (("qkv", 3 * C, C), ("fc", 4 * C, C)):

@@ -83,6 +83,10 @@ void decode_ln_linear(torch::Tensor rin, c10::optional<torch::Tensor> delta, c10
 // decode_linear.hip
 void decode_ln_gemm(torch::Tensor resid, torch::Tensor gamma, torch::Tensor beta, double eps, torch::Tensor w,
                     c10::optional<torch::Tensor> bias, torch::Tensor out, int64_t act, int64_t flags);
+void decode_gemv(c10::optional<torch::Tensor> x, c10::optional<torch::Tensor> rin, c10::optional<torch::Tensor> delta,
+                 c10::optional<torch::Tensor> dbias, c10::optional<torch::Tensor> rout,
+                 c10::optional<torch::Tensor> gamma, c10::optional<torch::Tensor> beta, double eps, torch::Tensor w,
+                 c10::optional<torch::Tensor> bias, torch::Tensor out, int64_t act, int64_t rows_per_wave);
 void decode_gemm_acc(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> bias, torch::Tensor resid,
                      int64_t flags);
 // gemm_wgrad.hip
@@ -183,6 +187,11 @@ PYBIND11_MODULE(penroz_kernels, m) {
   m.def("decode_ln_gemm", &decode_ln_gemm, pybind11::arg("resid"), pybind11::arg("gamma"), pybind11::arg("beta"),
         pybind11::arg("eps"), pybind11::arg("w"), pybind11::arg("bias"), pybind11::arg("out"), pybind11::arg("act") = 0,
         pybind11::arg("flags") = 0, "batched decode: out = act(LayerNorm(resid)·wᵀ + bias), fp32 resid [M, K <= 1024]");
+  m.def("decode_gemv", &decode_gemv, pybind11::arg("x"), pybind11::arg("resid_in"), pybind11::arg("delta"),
+        pybind11::arg("dbias"), pybind11::arg("resid_out"), pybind11::arg("gamma"), pybind11::arg("beta"),
+        pybind11::arg("eps"), pybind11::arg("w"), pybind11::arg("bias"), pybind11::arg("out"), pybind11::arg("act") = 0,
+        pybind11::arg("rows_per_wave") = 0,
+        "decode GEMV for 1..4 rows: act(x · Wᵀ + bias), or act(LN(resid_in + delta + dbias) · Wᵀ + bias)");
   m.def("decode_gemm_acc", &decode_gemm_acc, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("bias"),
         pybind11::arg("resid"), pybind11::arg("flags") = 0,
         "batched decode: resid += x·wᵀ + bias (fp32 residual, in place)");

@@ -17,6 +17,7 @@
 // and a second kernel combines them. Enough splits are used to put ≥ 512 workgroups in
 // flight (256 CUs) even at batch 1.
 #include "common.h"
+#include <cstdlib>
 #include <type_traits>
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
@@ -431,7 +432,16 @@ torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c
   auto out = torch::empty({B, Tq, H * D}, q.options());
   const int64_t q_rs = Tq == 1 ? q.stride(0) : q.stride(1);
   const int items = B * Hkv * Tq;
-  int splits = std::max(1, std::min<int>((512 + items - 1) / items, (int)((S + 255) / 256)));
+  // keys per split: a split costs a second (combine) launch, ~4.6 µs in a replayed decode step, so
+  // only contexts longer than this are split (each workgroup sweeps its keys in chunks of 256; a
+  // graph captures S = the cache capacity and the kernel stops at the device-side length).
+  // PENROZ_DECODE_SPLIT_KEYS overrides (256: the round-4 rule)
+  static const int split_keys = [] {
+    const char* e = std::getenv("PENROZ_DECODE_SPLIT_KEYS");
+    const int v = e ? std::atoi(e) : 0;
+    return v >= 64 ? v : 1024;
+  }();
+  int splits = std::max(1, std::min<int>((512 + items - 1) / items, (int)((S + split_keys - 1) / split_keys)));
   torch::Tensor ws_o, ws_ml;
   float* wo = nullptr;
   float* wm = nullptr;

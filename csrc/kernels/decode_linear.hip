@@ -24,6 +24,7 @@
 // (decode rows m): lane holds D[n = 4(lane>>4) + r][m = lane & 15], r = 0..3 — four
 // consecutive outputs of one row, stored as 8 B (bf16) or RMW'd as 16 B (fp32).
 #include "common.h"
+#include <type_traits>
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 
@@ -228,6 +229,181 @@ __global__ void __launch_bounds__(256) decode_gemm_acc_kernel(const bf16* __rest
   *rp = cur;
 }
 
+// ------------------------------------------------------------------------------------------
+// Decode GEMV for M <= 4 rows (batch-1..4 decode): out[M, N] = act(x · Wᵀ + bias), x either a
+// bf16 matrix or — LN mode — LayerNorm(resid_in + delta + dbias) computed in the kernel (the
+// residual sum also written to resid_out by workgroup 0). At these shapes a kernel's time is its
+// fixed costs: launch, one memory round trip, reductions. So:
+//   * one wave per workgroup, no LDS, no barrier: a half-wave (32 lanes) owns one weight row, a
+//     wave 2·RP rows; lane l reads 16-B chunks l, l+32, ... of its row (512 contiguous bytes per
+//     half-wave instruction) and the matching chunks of x;
+//   * every load of the wave — all its weight chunks, its x (or residual / delta / bias / γ / β)
+//     chunks — is issued before the first use: one round trip;
+//   * LN mode normalises each row within the half-wave (fp32 two-pass on the register copy, the
+//     add+LayerNorm kernel's math), rounds to bf16 (the GEMM operand's precision);
+//   * products by v_dot2c_f32_bf16 (bf16 pairs into fp32), one 5-step half-wave reduction per
+//     (row, x row), stores from lane 0 of each half.
+// No MFMA: at M <= 4 a 16x16 MFMA tile would waste ≥ 3/4 of itself, and the VALU work is small.
+typedef __bf16 dv_bf16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float dot8_bf16(const uint4& a, const uint4& b, float c) {
+  c = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(dv_bf16x2, a.x), __builtin_bit_cast(dv_bf16x2, b.x), c, false);
+  c = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(dv_bf16x2, a.y), __builtin_bit_cast(dv_bf16x2, b.y), c, false);
+  c = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(dv_bf16x2, a.z), __builtin_bit_cast(dv_bf16x2, b.z), c, false);
+  c = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(dv_bf16x2, a.w), __builtin_bit_cast(dv_bf16x2, b.w), c, false);
+  return c;
+}
+
+__device__ __forceinline__ float half_sum(float v) {  // sum over the 32 lanes of this half-wave
+#pragma unroll
+  for (int o = 1; o < 32; o <<= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int M, bool LN, int RP, int CPL>
+__global__ void __launch_bounds__(64) decode_gemv_kernel(
+    const float* __restrict__ rin, const bf16* __restrict__ delta, const float* __restrict__ dbias,
+    float* __restrict__ rout, const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
+    const bf16* __restrict__ x, int64_t x_rs, const bf16* __restrict__ w, const bf16* __restrict__ bias,
+    bf16* __restrict__ out, int64_t o_rs, int N, int K, int act) {
+  const int lane = threadIdx.x, h = lane >> 5, l32 = lane & 31;
+  const int nc = K / 8;  // 16-B chunks per row
+  const int n0 = blockIdx.x * 2 * RP;
+  // 1. every load first: weight chunks of this half's rows
+  uint4 wv[RP][CPL];
+#pragma unroll
+  for (int rp = 0; rp < RP; ++rp) {
+    const bf16* wr = w + (size_t)min(n0 + 2 * rp + h, N - 1) * K;
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) {
+      const int c = l32 + 32 * i;
+      wv[rp][i] = c < nc ? *reinterpret_cast<const uint4*>(wr + 8 * c) : uint4{0u, 0u, 0u, 0u};
+    }
+  }
+  uint4 xb[M][CPL];
+  if constexpr (!LN) {
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+#pragma unroll
+      for (int i = 0; i < CPL; ++i) {
+        const int c = l32 + 32 * i;
+        xb[m][i] = c < nc ? *reinterpret_cast<const uint4*>(x + (size_t)m * x_rs + 8 * c) : uint4{0u, 0u, 0u, 0u};
+      }
+  } else {
+    float v[M][CPL][8];
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+#pragma unroll
+      for (int i = 0; i < CPL; ++i) {
+        const int c = l32 + 32 * i;
+        if (c < nc) {
+          const float4_t* rp = reinterpret_cast<const float4_t*>(rin + (size_t)m * K + 8 * c);
+          const float4_t a = rp[0], b = rp[1];
+          v[m][i][0] = a[0]; v[m][i][1] = a[1]; v[m][i][2] = a[2]; v[m][i][3] = a[3];
+          v[m][i][4] = b[0]; v[m][i][5] = b[1]; v[m][i][6] = b[2]; v[m][i][7] = b[3];
+          if (delta) {
+            float d[8];
+            Vec8<bf16>::load(delta + (size_t)m * K + 8 * c, d);
+            if (dbias) {
+              const float4_t* e = reinterpret_cast<const float4_t*>(dbias + 8 * c);
+              const float4_t e0 = e[0], e1 = e[1];
+              d[0] += e0[0]; d[1] += e0[1]; d[2] += e0[2]; d[3] += e0[3];
+              d[4] += e1[0]; d[5] += e1[1]; d[6] += e1[2]; d[7] += e1[3];
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[m][i][k] += d[k];
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[m][i][k] = 0.f;
+        }
+      }
+    if (delta && rout && blockIdx.x == 0 && h == 0) {
+#pragma unroll
+      for (int m = 0; m < M; ++m)
+#pragma unroll
+        for (int i = 0; i < CPL; ++i) {
+          const int c = l32 + 32 * i;
+          if (c < nc) {
+            float4_t* op = reinterpret_cast<float4_t*>(rout + (size_t)m * K + 8 * c);
+            op[0] = float4_t{v[m][i][0], v[m][i][1], v[m][i][2], v[m][i][3]};
+            op[1] = float4_t{v[m][i][4], v[m][i][5], v[m][i][6], v[m][i][7]};
+          }
+        }
+    }
+    const float inv_k = 1.f / (float)K;
+    float mean[M], rstd[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < CPL; ++i)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s += v[m][i][k];
+      mean[m] = half_sum(s) * inv_k;
+    }
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      float ss = 0.f;
+#pragma unroll
+      for (int i = 0; i < CPL; ++i) {
+        const bool ok = l32 + 32 * i < nc;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float d = v[m][i][k] - mean[m];
+          ss += ok ? d * d : 0.f;
+        }
+      }
+      rstd[m] = rsqrtf(half_sum(ss) * inv_k + eps);
+    }
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) {
+      const int c = l32 + 32 * i;
+      float g[8] = {}, bt[8] = {};
+      if (c < nc) {
+        const float4_t* gp = reinterpret_cast<const float4_t*>(gamma + 8 * c);
+        const float4_t* bp = reinterpret_cast<const float4_t*>(beta + 8 * c);
+        const float4_t g0 = gp[0], g1 = gp[1], b0 = bp[0], b1 = bp[1];
+        g[0] = g0[0]; g[1] = g0[1]; g[2] = g0[2]; g[3] = g0[3]; g[4] = g1[0]; g[5] = g1[1]; g[6] = g1[2]; g[7] = g1[3];
+        bt[0] = b0[0]; bt[1] = b0[1]; bt[2] = b0[2]; bt[3] = b0[3]; bt[4] = b1[0]; bt[5] = b1[1]; bt[6] = b1[2]; bt[7] = b1[3];
+      }
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        float y[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) y[k] = (v[m][i][k] - mean[m]) * rstd[m] * g[k] + bt[k];
+        xb[m][i] = uint4{pack_bf16x2(y[0], y[1]), pack_bf16x2(y[2], y[3]), pack_bf16x2(y[4], y[5]),
+                         pack_bf16x2(y[6], y[7])};
+      }
+    }
+  }
+  // 2. products and the half-wave reductions
+  float acc[RP][M];
+#pragma unroll
+  for (int rp = 0; rp < RP; ++rp)
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      float a = 0.f;
+#pragma unroll
+      for (int i = 0; i < CPL; ++i) a = dot8_bf16(wv[rp][i], xb[m][i], a);
+      acc[rp][m] = half_sum(a);
+    }
+  // 3. epilogue: lane 0 of each half stores its rows
+  if (l32 != 0) return;
+#pragma unroll
+  for (int rp = 0; rp < RP; ++rp) {
+    const int n = n0 + 2 * rp + h;
+    if (n >= N) continue;
+    const float bv = bias ? bf2f(bias[n]) : 0.f;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      float y = acc[rp][m] + bv;
+      if (act) y = gelu_f(bf2f(from_f<bf16>(y)), act - 1);
+      out[(size_t)m * o_rs + n] = from_f<bf16>(y);
+    }
+  }
+}
+
 }  // namespace penroz
 
 using namespace penroz;
@@ -291,4 +467,129 @@ void decode_gemm_acc(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tens
   hipLaunchKernelGGL(decode_gemm_acc_kernel, dim3(grid), dim3(256), 0, at::hip::getCurrentHIPStream(),
                      reinterpret_cast<const bf16*>(x.data_ptr()), (int64_t)x.stride(0),
                      reinterpret_cast<const bf16*>(w.data_ptr()), bp, resid.data_ptr<float>(), M, N, K, (int)flags);
+}
+
+// out[M, N] = act(x · Wᵀ + bias) for M <= 4 decode rows (decode_gemv_kernel). LN mode (x
+// undefined): x = LayerNorm(resid_in + delta + dbias) with γ / β, resid_out receives the sum.
+// act 0 none, 1 GELU (erf), 2 GELU (tanh). rows_per_wave 2, 4 or 8 (0: by N).
+void decode_gemv(c10::optional<torch::Tensor> x, c10::optional<torch::Tensor> rin, c10::optional<torch::Tensor> delta,
+                 c10::optional<torch::Tensor> dbias, c10::optional<torch::Tensor> rout,
+                 c10::optional<torch::Tensor> gamma, c10::optional<torch::Tensor> beta, double eps, torch::Tensor w,
+                 c10::optional<torch::Tensor> bias, torch::Tensor out, int64_t act, int64_t rows_per_wave) {
+  const bool ln = !(x.has_value() && x->defined());
+  const int N = w.size(0), K = w.size(1);
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == torch::kBFloat16 && w.dim() == 2 && w.is_contiguous() &&
+                  reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0 && K % 8 == 0,
+              "decode_gemv: bf16 contiguous 16-B aligned W [N, K], K % 8 == 0");
+  TORCH_CHECK(K <= 256 * 32, "decode_gemv: K <= 8192");
+  TORCH_CHECK(act >= 0 && act <= 2, "decode_gemv: act 0 (none), 1 (GELU erf), 2 (GELU tanh)");
+  int M;
+  const bf16* xp = nullptr;
+  int64_t x_rs = 0;
+  const float *rp = nullptr, *dbp = nullptr, *gp = nullptr, *bt = nullptr;
+  const bf16* dp = nullptr;
+  float* rop = nullptr;
+  if (!ln) {
+    TORCH_CHECK(x->scalar_type() == torch::kBFloat16 && x->dim() == 2 && x->size(1) == K && x->stride(1) == 1 &&
+                    x->stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(x->data_ptr()) % 16 == 0,
+                "decode_gemv: bf16 x [M, K], rows 16-B aligned");
+    M = x->size(0);
+    xp = reinterpret_cast<const bf16*>(x->data_ptr());
+    x_rs = x->stride(0);
+  } else {
+    TORCH_CHECK(rin.has_value() && rin->defined() && rin->scalar_type() == torch::kFloat32 && rin->dim() == 2 &&
+                    rin->is_contiguous() && rin->size(1) == K, "decode_gemv: fp32 contiguous resid_in [M, K]");
+    TORCH_CHECK(K <= 1024, "decode_gemv: LN mode needs K <= 1024");
+    TORCH_CHECK(gamma.has_value() && beta.has_value() && gamma->scalar_type() == torch::kFloat32 &&
+                    beta->scalar_type() == torch::kFloat32 && gamma->numel() == K && beta->numel() == K &&
+                    gamma->is_contiguous() && beta->is_contiguous(), "decode_gemv: fp32 gamma / beta [K]");
+    M = rin->size(0);
+    rp = rin->data_ptr<float>();
+    gp = gamma->data_ptr<float>();
+    bt = beta->data_ptr<float>();
+    if (delta.has_value() && delta->defined()) {
+      TORCH_CHECK(delta->scalar_type() == torch::kBFloat16 && delta->is_contiguous() && delta->numel() == (int64_t)M * K,
+                  "decode_gemv: bf16 contiguous delta [M, K]");
+      TORCH_CHECK(rout.has_value() && rout->defined() && rout->scalar_type() == torch::kFloat32 &&
+                      rout->is_contiguous() && rout->numel() == (int64_t)M * K && rout->data_ptr() != rin->data_ptr(),
+                  "decode_gemv: fp32 resid_out [M, K] (not aliasing resid_in) with a delta");
+      dp = reinterpret_cast<const bf16*>(delta->data_ptr());
+      rop = rout->data_ptr<float>();
+      if (dbias.has_value() && dbias->defined()) {
+        TORCH_CHECK(dbias->scalar_type() == torch::kFloat32 && dbias->is_contiguous() && dbias->numel() == K,
+                    "decode_gemv: fp32 dbias [K]");
+        dbp = dbias->data_ptr<float>();
+      }
+    }
+  }
+  TORCH_CHECK(M >= 1 && M <= 4, "decode_gemv: 1..4 rows");
+  TORCH_CHECK(out.scalar_type() == torch::kBFloat16 && out.dim() == 2 && out.size(0) == M && out.size(1) == N &&
+                  out.stride(1) == 1, "decode_gemv: bf16 out [M, N]");
+  const bf16* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->scalar_type() == torch::kBFloat16 && bias->is_contiguous() && bias->numel() == N,
+                "decode_gemv: bf16 bias [N]");
+    bp = reinterpret_cast<const bf16*>(bias->data_ptr());
+  }
+  const int cpl = (K / 8 + 31) / 32;
+  int rpw = (int)rows_per_wave;
+  // by shape (profiles/decode_gemv_r5.log, batch 1): narrow outputs want more waves (2 rows each),
+  // the vocabulary projection fewer, longer-lived waves (8 rows); K > 2048 keeps 2 rows per wave
+  if (rpw <= 0) rpw = N >= 16384 ? 8 : (cpl > 8 || N <= 1024) ? 2 : 4;
+  TORCH_CHECK(rpw == 2 || rpw == 4 || rpw == 8, "decode_gemv: rows_per_wave 2, 4 or 8");
+  const int RPv = rpw / 2;
+  const dim3 grid((N + rpw - 1) / rpw);
+  auto stream = at::hip::getCurrentHIPStream();
+  auto wp = reinterpret_cast<const bf16*>(w.data_ptr());
+  auto op = reinterpret_cast<bf16*>(out.data_ptr());
+  const int64_t o_rs = out.stride(0);
+  auto launch = [&](auto mt, auto lnt, auto rpt, auto cplt) {
+    constexpr int MM = decltype(mt)::value, RR = decltype(rpt)::value, CC = decltype(cplt)::value;
+    constexpr bool LL = decltype(lnt)::value;
+    hipLaunchKernelGGL((decode_gemv_kernel<MM, LL, RR, CC>), grid, dim3(64), 0, stream, rp, dp, dbp, rop, gp, bt,
+                       (float)eps, xp, x_rs, wp, bp, op, o_rs, N, K, (int)act);
+  };
+  auto by_cpl = [&](auto mt, auto lnt, auto rpt) {
+    using I = std::integral_constant<int, 0>;
+    (void)sizeof(I);
+    if (cpl <= 1) launch(mt, lnt, rpt, std::integral_constant<int, 1>{});
+    else if (cpl <= 2) launch(mt, lnt, rpt, std::integral_constant<int, 2>{});
+    else if (cpl <= 3) launch(mt, lnt, rpt, std::integral_constant<int, 3>{});
+    else if (cpl <= 4) launch(mt, lnt, rpt, std::integral_constant<int, 4>{});
+    else if (cpl <= 5) launch(mt, lnt, rpt, std::integral_constant<int, 5>{});
+    else if (cpl <= 7) launch(mt, lnt, rpt, std::integral_constant<int, 7>{});
+    else if (cpl <= 12) launch(mt, lnt, rpt, std::integral_constant<int, 12>{});
+    else if (cpl <= 16) launch(mt, lnt, rpt, std::integral_constant<int, 16>{});
+    else if (cpl <= 25) launch(mt, lnt, rpt, std::integral_constant<int, 25>{});
+    else launch(mt, lnt, rpt, std::integral_constant<int, 32>{});
+  };
+  auto by_rp = [&](auto mt, auto lnt) {
+    if (RPv == 1) by_cpl(mt, lnt, std::integral_constant<int, 1>{});
+    else if (RPv == 2) by_cpl(mt, lnt, std::integral_constant<int, 2>{});
+    else by_cpl(mt, lnt, std::integral_constant<int, 4>{});
+  };
+  auto by_ln = [&](auto mt) {
+    if (ln) {
+      TORCH_CHECK(cpl <= 4, "decode_gemv: LN mode needs K <= 1024");
+      // LN mode instantiates only the small chunk counts (K <= 1024)
+      if (RPv == 1) {
+        if (cpl <= 3) launch(mt, std::true_type{}, std::integral_constant<int, 1>{}, std::integral_constant<int, 3>{});
+        else launch(mt, std::true_type{}, std::integral_constant<int, 1>{}, std::integral_constant<int, 4>{});
+      } else if (RPv == 2) {
+        if (cpl <= 3) launch(mt, std::true_type{}, std::integral_constant<int, 2>{}, std::integral_constant<int, 3>{});
+        else launch(mt, std::true_type{}, std::integral_constant<int, 2>{}, std::integral_constant<int, 4>{});
+      } else {
+        if (cpl <= 3) launch(mt, std::true_type{}, std::integral_constant<int, 4>{}, std::integral_constant<int, 3>{});
+        else launch(mt, std::true_type{}, std::integral_constant<int, 4>{}, std::integral_constant<int, 4>{});
+      }
+    } else {
+      by_rp(mt, std::false_type{});
+    }
+  };
+  switch (M) {
+    case 1: by_ln(std::integral_constant<int, 1>{}); break;
+    case 2: by_ln(std::integral_constant<int, 2>{}); break;
+    case 3: by_ln(std::integral_constant<int, 3>{}); break;
+    default: by_ln(std::integral_constant<int, 4>{});
+  }
 }

@@ -78,6 +78,11 @@ FUSED_MAX_ROWS = int(os.environ.get("PENROZ_DECODE_FUSED_MAX_ROWS", "8"))
 # fp32 residual updated in place by the proj / fc2 epilogues, LayerNorm recomputed per 16-row
 # block inside the QKV / fc GEMMs; "0": add+LN, GEMM, GELU kernels (8 per block)
 BATCHED_BLOCK = os.environ.get("PENROZ_DECODE_BATCHED", "1") != "0"
+# ... and up to this many rows (batch 1-4) every linear of the GPT block — the LN-fused QKV and
+# fc(+GELU), proj, fc2 and the lm_head — runs as the one-wave-per-workgroup decode GEMV
+# (csrc/kernels/decode_linear.hip decode_gemv: one memory round trip, no LDS, no barrier, no
+# split-K hand-off); "0": decode_ln_linear + skinny GEMMs
+GEMV_MAX_ROWS = int(os.environ.get("PENROZ_DECODE_GEMV_MAX_ROWS", "4"))
 
 
 class _GraphMode:
@@ -174,6 +179,11 @@ class GPTDecodeProgram:
             return torch.addmm(b, x, lin.weight.t())
         return torch.mm(x, lin.weight.t())
 
+    def _gemv_ok(self, rows: int) -> bool:
+        sp = self.spec
+        return (1 <= rows <= min(4, GEMV_MAX_ROWS) and sp.C % 8 == 0 and sp.C <= 1024
+                and sp.blocks[0].fc.out_features % 8 == 0 and sp.gelu_approx in ("none", "tanh") and _ext.available())
+
     def _fused_ok(self, rows: int) -> bool:
         sp = self.spec
         return (FUSED_LN_LINEAR and 1 <= rows <= min(64, FUSED_MAX_ROWS) and sp.C % 32 == 0 and sp.C <= 1024
@@ -193,6 +203,8 @@ class GPTDecodeProgram:
         if self._batched_ok(rows):
             return self._forward_batched(x, rows, cache)
         x2 = torch.empty_like(x)  # the residual stream ping-pongs between x and x2 (no aliasing)
+        if self._gemv_ok(rows):
+            return self._forward_gemv(x, x2, rows, cache)
         if self._fused_ok(rows):
             return self._forward_fused(x, x2, rows, cache)
 
@@ -254,6 +266,42 @@ class GPTDecodeProgram:
         y, _, _ = norm_ops.add_ln_fwd(x, delta, x2, wf, bf, ef, delta_bias=dbias)
         return self._linear(y, sp.head)
 
+
+    def _forward_gemv(self, x: Tensor, x2: Tensor, rows: int, cache) -> Tensor:
+        """Batch 1-4, per block: [add + LN1 + QKV GEMV + bias] → decode attention (K/V append fused)
+        → proj GEMV → [add + proj bias + LN2 + fc GEMV + bias + GELU] → fc2 GEMV; then the final
+        add + LN and the lm_head GEMV — every linear one decode_gemv launch."""
+        sp = self.spec
+        K = _ext.kernels()
+        C, H, D = sp.C, sp.H, sp.D
+        act = 2 if sp.gelu_approx == "tanh" else 1
+        delta = dbias = None
+        for l, blk in enumerate(sp.blocks):
+            w1, b1, e1, w2, b2, e2 = self.ln[l]
+            pb, fb = self.out_bias[l]
+            qkv = torch.empty(rows, 3 * C, dtype=torch.bfloat16, device=x.device)
+            if delta is None:
+                K.decode_gemv(None, x, None, None, None, w1, b1, e1, blk.qkv.weight, blk.qkv.bias, qkv, 0)
+            else:
+                K.decode_gemv(None, x, delta, dbias, x2, w1, b1, e1, blk.qkv.weight, blk.qkv.bias, qkv, 0)
+                x, x2 = x2, x
+            qkv = qkv.view(rows, 1, 3 * C)
+            q = qkv[:, :, :C].view(rows, 1, H, D)
+            k = qkv[:, :, C:2 * C].view(rows, 1, H, D)
+            v = qkv[:, :, 2 * C:].view(rows, 1, H, D)
+            o = cache._attend_graph(l, q, k, v).view(rows, C)
+            d = torch.empty(rows, C, dtype=torch.bfloat16, device=x.device)
+            K.decode_gemv(o, None, None, None, None, None, None, 0.0, blk.proj.weight, None, d, 0)
+            h = torch.empty(rows, blk.fc.out_features, dtype=torch.bfloat16, device=x.device)
+            K.decode_gemv(None, x, d, pb, x2, w2, b2, e2, blk.fc.weight, blk.fc.bias, h, act)
+            x, x2 = x2, x
+            delta = torch.empty(rows, C, dtype=torch.bfloat16, device=x.device)
+            K.decode_gemv(h, None, None, None, None, None, None, 0.0, blk.fc2.weight, None, delta, 0)
+            dbias = fb
+        wf, bf, ef = self.lnf
+        logits = torch.empty(rows, sp.head.weight.shape[0], dtype=torch.bfloat16, device=x.device)
+        K.decode_gemv(None, x, delta, dbias, x2, wf, bf, ef, sp.head.weight, None, logits, 0)
+        return logits
 
     def _forward_batched(self, x: Tensor, rows: int, cache) -> Tensor:
         """Per block: [LN1 + QKV GEMM + bias] → decode attention (K/V append fused) → [proj GEMM +

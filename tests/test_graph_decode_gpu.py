@@ -82,7 +82,7 @@ class _EagerGraph:
         self.dec._step()
 
 
-@pytest.mark.parametrize("rows", [3, 40])
+@pytest.mark.parametrize("rows", [1, 3, 6, 40])
 def test_decode_program_graph_replay_matches_eager_program(monkeypatch, rows):
     m = _model(torch.bfloat16)
     assert gd.GPTDecodeProgram.build(m) is not None, "GPT pattern must select the decode program"
@@ -100,10 +100,10 @@ def test_decode_program_graph_replay_matches_eager_program(monkeypatch, rows):
     assert graphed == eager
 
 
-@pytest.mark.parametrize("rows", [3, 24, 64])
+@pytest.mark.parametrize("rows", [1, 3, 6, 24, 64])
 def test_decode_program_step_matches_module_step(rows):
-    """One decode-program step vs the module forward: rows 3 run the fused LN-linear path, 24 and
-    64 the batched block (decode_ln_gemm / decode_gemm_acc)."""
+    """One decode-program step vs the module forward: rows 1 and 3 run the decode GEMV path, 6 the
+    fused LN-linear path, 24 and 64 the batched block (decode_ln_gemm / decode_gemm_acc)."""
     m = _model(torch.bfloat16)
     cap = 32
     dec = gd.GraphDecoder(m, rows, cap, 0.0, None)

@@ -1085,6 +1085,54 @@ def test_decode_ln_linear(M, K, N, act, with_delta):
         _close(rout, s, 1e-6, 1e-6, "resid_out")
 
 
+@pytest.mark.parametrize("M,K,N", [(1, 768, 2304), (2, 768, 3072), (4, 1024, 75), (3, 96, 50), (1, 1152, 1024)])
+@pytest.mark.parametrize("act", [0, 1, 2])
+@pytest.mark.parametrize("with_delta", [True, False])
+@pytest.mark.parametrize("rpw", [0, 2, 8])
+def test_decode_gemv_ln(M, K, N, act, with_delta, rpw):
+    """Decode GEMV, LN mode: out = act(LN(resid + delta + dbias)·Wᵀ + b) vs fp32 torch (+ the
+    residual sum); partial last waves (N % rows-per-wave != 0) and chunk tails (K % 256 != 0)."""
+    if K > 1024:
+        pytest.skip("LN mode is K <= 1024")
+    torch.manual_seed(0)
+    rin = torch.randn(M, K, device=DEV) * 2 + 0.5
+    delta = torch.randn(M, K, device=DEV).to(torch.bfloat16) if with_delta else None
+    dbias = torch.randn(K, device=DEV) if with_delta else None
+    rout = torch.full((M, K), 7.0, device=DEV) if with_delta else None
+    gamma, beta = torch.randn(K, device=DEV), torch.randn(K, device=DEV)
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, device=DEV).to(torch.bfloat16)
+    full = torch.full((M, N + 3), 5.0, device=DEV, dtype=torch.bfloat16)
+    out = full[:, :N]
+    _ext.kernels().decode_gemv(None, rin, delta, dbias, rout, gamma, beta, 1e-5, w, b, out, act, rpw)
+    s = rin + (delta.float() + dbias) if with_delta else rin
+    y = F.layer_norm(s, (K,), gamma, beta, 1e-5).to(torch.bfloat16).float()
+    ref = y @ w.float().t() + b.float()
+    if act:
+        ref = F.gelu(ref.to(torch.bfloat16).float(), approximate="tanh" if act == 2 else "none")
+    _close(out, ref, 2e-2, 2e-2, "out")
+    assert torch.all(full[:, N:] == 5.0), "wrote past N"
+    if with_delta:
+        _close(rout, s, 1e-6, 1e-6, "resid_out")
+
+
+@pytest.mark.parametrize("M,K,N", [(1, 768, 768), (1, 3072, 768), (4, 768, 50304), (2, 6912, 1152), (3, 40, 33),
+                                   (1, 8192, 16)])
+@pytest.mark.parametrize("rpw", [0, 2, 4, 8])
+def test_decode_gemv_plain(M, K, N, rpw):
+    """Decode GEMV on a bf16 x (strided rows) vs fp32 torch, with and without bias."""
+    torch.manual_seed(1)
+    xb = torch.randn(M, K + 16, device=DEV).to(torch.bfloat16)
+    x = xb[:, :K]
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, device=DEV).to(torch.bfloat16)
+    for bias in (None, b):
+        out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        _ext.kernels().decode_gemv(x, None, None, None, None, None, None, 0.0, w, bias, out, 0, rpw)
+        ref = x.float() @ w.float().t() + (0 if bias is None else b.float())
+        _close(out, ref, 2e-2, 2e-2, "out")
+
+
 @pytest.mark.parametrize("M,K,N", [(64, 768, 2304), (64, 768, 3072), (37, 1024, 320), (16, 256, 64), (9, 96, 1040)])
 @pytest.mark.parametrize("act", [0, 2])
 def test_decode_ln_gemm(M, K, N, act):
