@@ -87,6 +87,9 @@ void decode_gemv(c10::optional<torch::Tensor> x, c10::optional<torch::Tensor> ri
                  c10::optional<torch::Tensor> dbias, c10::optional<torch::Tensor> rout,
                  c10::optional<torch::Tensor> gamma, c10::optional<torch::Tensor> beta, double eps, torch::Tensor w,
                  c10::optional<torch::Tensor> bias, torch::Tensor out, int64_t act, int64_t rows_per_wave);
+void decode_gemv_pair(torch::Tensor x, torch::Tensor w, torch::Tensor out, int64_t mode, int64_t kind, int64_t D,
+                      int64_t nrot, c10::optional<torch::Tensor> cosv, c10::optional<torch::Tensor> sinv,
+                      int64_t pairs_per_wave);
 void decode_gemm_acc(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> bias, torch::Tensor resid,
                      int64_t flags);
 // gemm_wgrad.hip
@@ -192,6 +195,11 @@ PYBIND11_MODULE(penroz_kernels, m) {
         pybind11::arg("eps"), pybind11::arg("w"), pybind11::arg("bias"), pybind11::arg("out"), pybind11::arg("act") = 0,
         pybind11::arg("rows_per_wave") = 0,
         "decode GEMV for 1..4 rows: act(x · Wᵀ + bias), or act(LN(resid_in + delta + dbias) · Wᵀ + bias)");
+  m.def("decode_gemv_pair", &decode_gemv_pair, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("out"),
+        pybind11::arg("mode"), pybind11::arg("kind") = 0, pybind11::arg("D") = 0, pybind11::arg("nrot") = 0,
+        pybind11::arg("cos") = pybind11::none(), pybind11::arg("sin") = pybind11::none(),
+        pybind11::arg("pairs_per_wave") = 0,
+        "paired-row decode GEMV for 1..4 rows: gated MLP (mode 1) or RoPE QKV (mode 2) epilogue");
   m.def("decode_gemm_acc", &decode_gemm_acc, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("bias"),
         pybind11::arg("resid"), pybind11::arg("flags") = 0,
         "batched decode: resid += x·wᵀ + bias (fp32 residual, in place)");

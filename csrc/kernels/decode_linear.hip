@@ -260,20 +260,38 @@ __device__ __forceinline__ float half_sum(float v) {  // sum over the 32 lanes o
   return v;
 }
 
-template <int M, bool LN, int RP, int CPL>
+// EPI (the two half-waves' rows as a pair): 0 — independent rows, act(y + bias); 1 — gated MLP
+// on the packed [gate; up] weight (N = 2I rows): half 0 takes gate row n, half 1 up row I + n,
+// out[n] = act_f(bf16(g), kind) · bf16(u) (skinny_gated's rounding); 2 — RoPE QKV: pair p of head
+// p / (D/2), j = p % (D/2): half 0 row head·D + j, half 1 row + D/2, both rounded to bf16, then
+// rotated by one position's cos / sin [D/2] for the first nrot heads (skinny_qkv_rope's math).
+// In modes 1 / 2 a wave owns RP output pairs.
+template <int M, bool LN, int RP, int CPL, int EPI = 0>
 __global__ void __launch_bounds__(64) decode_gemv_kernel(
     const float* __restrict__ rin, const bf16* __restrict__ delta, const float* __restrict__ dbias,
     float* __restrict__ rout, const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
     const bf16* __restrict__ x, int64_t x_rs, const bf16* __restrict__ w, const bf16* __restrict__ bias,
-    bf16* __restrict__ out, int64_t o_rs, int N, int K, int act) {
+    bf16* __restrict__ out, int64_t o_rs, int N, int K, int act, int D = 0, int nrot = 0,
+    const float* __restrict__ cosv = nullptr, const float* __restrict__ sinv = nullptr) {
   const int lane = threadIdx.x, h = lane >> 5, l32 = lane & 31;
   const int nc = K / 8;  // 16-B chunks per row
-  const int n0 = blockIdx.x * 2 * RP;
+  const int n0 = blockIdx.x * (EPI == 0 ? 2 * RP : RP);
+  const int npair = N / 2;  // modes 1 / 2: output pairs
+  auto row_of = [&](int rp) -> int {  // this half's weight row for its rp-th row (pair)
+    if constexpr (EPI == 0) {
+      return min(n0 + 2 * rp + h, N - 1);
+    } else if constexpr (EPI == 1) {
+      return min(n0 + rp, npair - 1) + h * npair;
+    } else {
+      const int p = min(n0 + rp, npair - 1), hd = D / 2, head = p / hd;
+      return head * D + (p - head * hd) + h * hd;
+    }
+  };
   // 1. every load first: weight chunks of this half's rows
   uint4 wv[RP][CPL];
 #pragma unroll
   for (int rp = 0; rp < RP; ++rp) {
-    const bf16* wr = w + (size_t)min(n0 + 2 * rp + h, N - 1) * K;
+    const bf16* wr = w + (size_t)row_of(rp) * K;
 #pragma unroll
     for (int i = 0; i < CPL; ++i) {
       const int c = l32 + 32 * i;
@@ -389,6 +407,35 @@ __global__ void __launch_bounds__(64) decode_gemv_kernel(
       acc[rp][m] = half_sum(a);
     }
   // 3. epilogue: lane 0 of each half stores its rows
+  if constexpr (EPI != 0) {
+    float other[RP][M];  // the partner half's sums (lane 0 <-> lane 32)
+#pragma unroll
+    for (int rp = 0; rp < RP; ++rp)
+#pragma unroll
+      for (int m = 0; m < M; ++m) other[rp][m] = __shfl_xor(acc[rp][m], 32, 64);
+    if (l32 != 0) return;
+#pragma unroll
+    for (int rp = 0; rp < RP; ++rp) {
+      const int p = n0 + rp;
+      if (p >= npair) continue;
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        const float mine = bf2f(from_f<bf16>(acc[rp][m])), theirs = bf2f(from_f<bf16>(other[rp][m]));
+        if constexpr (EPI == 1) {
+          if (h == 0) out[(size_t)m * o_rs + p] = from_f<bf16>(act_f(mine, act) * theirs);
+        } else {
+          const int hd = D / 2, head = p / hd, j = p - head * hd;
+          float y = mine;
+          if (head < nrot) {
+            const float cs = cosv[j], sn = sinv[j];
+            y = h == 0 ? mine * cs - theirs * sn : mine * cs + theirs * sn;
+          }
+          out[(size_t)m * o_rs + head * D + j + h * hd] = from_f<bf16>(y);
+        }
+      }
+    }
+    return;
+  }
   if (l32 != 0) return;
 #pragma unroll
   for (int rp = 0; rp < RP; ++rp) {
@@ -591,5 +638,77 @@ void decode_gemv(c10::optional<torch::Tensor> x, c10::optional<torch::Tensor> ri
     case 2: by_ln(std::integral_constant<int, 2>{}); break;
     case 3: by_ln(std::integral_constant<int, 3>{}); break;
     default: by_ln(std::integral_constant<int, 4>{});
+  }
+}
+
+// Paired-row decode GEMV for 1..4 rows on a bf16 x (decode_gemv_kernel modes 1 / 2):
+//   mode 1 (gated): out[M, I] = act_f(x·Wgᵀ, kind) ⊙ (x·Wuᵀ), w = [Wg; Wu] [2I, K];
+//   mode 2 (RoPE QKV): out[M, (H + 2Hkv)·D] = rope(x · Wᵀ) for the first nrot heads, cos / sin [D/2].
+void decode_gemv_pair(torch::Tensor x, torch::Tensor w, torch::Tensor out, int64_t mode, int64_t kind, int64_t D,
+                      int64_t nrot, c10::optional<torch::Tensor> cosv, c10::optional<torch::Tensor> sinv,
+                      int64_t pairs_per_wave) {
+  const int N = w.size(0), K = w.size(1);
+  TORCH_CHECK(mode == 1 || mode == 2, "decode_gemv_pair: mode 1 (gated) or 2 (RoPE)");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == torch::kBFloat16 && w.dim() == 2 && w.is_contiguous() &&
+                  reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0 && K % 8 == 0 && N % 2 == 0,
+              "decode_gemv_pair: bf16 contiguous 16-B aligned W [N, K], K % 8 == 0, N even");
+  TORCH_CHECK(x.scalar_type() == torch::kBFloat16 && x.dim() == 2 && x.size(1) == K && x.stride(1) == 1 &&
+                  x.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "decode_gemv_pair: bf16 x [M, K], rows 16-B aligned");
+  const int M = x.size(0);
+  TORCH_CHECK(M >= 1 && M <= 4, "decode_gemv_pair: 1..4 rows");
+  const int cpl = (K / 8 + 31) / 32;
+  TORCH_CHECK(cpl <= 7, "decode_gemv_pair: K <= 1792");
+  const int Nout = mode == 1 ? N / 2 : N;
+  TORCH_CHECK(out.scalar_type() == torch::kBFloat16 && out.dim() == 2 && out.size(0) == M && out.size(1) == Nout &&
+                  out.stride(1) == 1, "decode_gemv_pair: bf16 out [M, N/2] (gated) or [M, N] (RoPE)");
+  const float *cp = nullptr, *sp = nullptr;
+  if (mode == 1) {
+    TORCH_CHECK(kind >= 0 && kind <= 2, "decode_gemv_pair: kind 0 gelu, 1 gelu_tanh, 2 silu");
+  } else {
+    TORCH_CHECK(D >= 2 && D % 2 == 0 && N % D == 0 && nrot >= 0 && nrot <= N / D, "decode_gemv_pair: RoPE geometry");
+    TORCH_CHECK(cosv.has_value() && sinv.has_value() && cosv->is_cuda() && sinv->is_cuda() &&
+                    cosv->scalar_type() == torch::kFloat32 && sinv->scalar_type() == torch::kFloat32 &&
+                    cosv->numel() >= D / 2 && sinv->numel() >= D / 2 && cosv->is_contiguous() && sinv->is_contiguous(),
+                "decode_gemv_pair: fp32 cos / sin [D/2]");
+    cp = cosv->data_ptr<float>();
+    sp = sinv->data_ptr<float>();
+  }
+  int ppw = (int)pairs_per_wave;
+  if (ppw <= 0) ppw = N / 2 >= 16384 ? 4 : N / 2 <= 1024 ? 1 : 2;
+  TORCH_CHECK(ppw == 1 || ppw == 2 || ppw == 4, "decode_gemv_pair: pairs_per_wave 1, 2 or 4");
+  const dim3 grid((N / 2 + ppw - 1) / ppw);
+  auto stream = at::hip::getCurrentHIPStream();
+  auto xp = reinterpret_cast<const bf16*>(x.data_ptr());
+  auto wp = reinterpret_cast<const bf16*>(w.data_ptr());
+  auto op = reinterpret_cast<bf16*>(out.data_ptr());
+  const int64_t x_rs = x.stride(0), o_rs = out.stride(0);
+  auto launch = [&](auto mt, auto rpt, auto cplt, auto et) {
+    constexpr int MM = decltype(mt)::value, RR = decltype(rpt)::value, CC = decltype(cplt)::value;
+    constexpr int EE = decltype(et)::value;
+    hipLaunchKernelGGL((decode_gemv_kernel<MM, false, RR, CC, EE>), grid, dim3(64), 0, stream, nullptr, nullptr,
+                       nullptr, nullptr, nullptr, nullptr, 0.f, xp, x_rs, wp, nullptr, op, o_rs, N, K, (int)kind,
+                       (int)D, (int)nrot, cp, sp);
+  };
+  auto by_cpl = [&](auto mt, auto rpt, auto et) {
+    if (cpl <= 3) launch(mt, rpt, std::integral_constant<int, 3>{}, et);
+    else if (cpl <= 4) launch(mt, rpt, std::integral_constant<int, 4>{}, et);
+    else if (cpl <= 5) launch(mt, rpt, std::integral_constant<int, 5>{}, et);
+    else launch(mt, rpt, std::integral_constant<int, 7>{}, et);
+  };
+  auto by_rp = [&](auto mt, auto et) {
+    if (ppw == 1) by_cpl(mt, std::integral_constant<int, 1>{}, et);
+    else if (ppw == 2) by_cpl(mt, std::integral_constant<int, 2>{}, et);
+    else by_cpl(mt, std::integral_constant<int, 4>{}, et);
+  };
+  auto by_mode = [&](auto mt) {
+    if (mode == 1) by_rp(mt, std::integral_constant<int, 1>{});
+    else by_rp(mt, std::integral_constant<int, 2>{});
+  };
+  switch (M) {
+    case 1: by_mode(std::integral_constant<int, 1>{}); break;
+    case 2: by_mode(std::integral_constant<int, 2>{}); break;
+    case 3: by_mode(std::integral_constant<int, 3>{}); break;
+    default: by_mode(std::integral_constant<int, 4>{});
   }
 }

@@ -409,10 +409,25 @@ class GemmaDecodeProgram:
                 return None
         return GemmaDecodeProgram(mods[0], mods[1:-2], mods[-2], mods[-1])
 
+    def _gemv_ok(self, rows: int, C: int) -> bool:
+        """Batch 1-4: every projection as one decode GEMV (decode_gemv / decode_gemv_pair:
+        one wave per workgroup, one memory round trip; RoPE and the gated activation in the
+        paired-row epilogues)."""
+        return 1 <= rows <= min(4, GEMV_MAX_ROWS) and C % 8 == 0 and C <= 1792 and _ext.available()
+
     def forward(self, idx: Tensor, cache) -> Tensor:
         """idx [rows, 1] -> logits [rows, V] (bf16); appends this step's K/V at cache.pos_t."""
         K = _ext.kernels()
         rows = idx.shape[0]
+        gemv = self._gemv_ok(rows, self.emb.embedding_dim)
+
+        def lin(x: Tensor, w: Tensor) -> Tensor:
+            if gemv and w.shape[1] % 8 == 0:
+                out = torch.empty(rows, w.shape[0], device=x.device, dtype=torch.bfloat16)
+                K.decode_gemv(x.contiguous(), None, None, None, None, None, None, 0.0, w, None, out, 0)
+                return out
+            return _linear(x, w)
+
         x = torch.nn.functional.embedding(idx.view(rows), self.emb.weight) * self.emb.scale
         first = self.blocks[0]["in_norm"]
         y = K.rmsnorm_fwd(x, first.weight, first.eps)[0]
@@ -422,25 +437,33 @@ class GemmaDecodeProgram:
             if a.rope_theta is not None:
                 inv = a._inv_freq(D, y.device)
                 cos, sin = cache.rope_table((a.rope_theta, D), inv, 1)
-                if DECODE_EPILOGUES and rows <= SKINNY_MAX_ROWS and gemm_ops.skinny_qkv_rope_ok(y, b["qkv"], D):
+                if gemv and DECODE_EPILOGUES and D % 2 == 0:
+                    qkv = torch.empty(rows, b["qkv"].shape[0], device=y.device, dtype=torch.bfloat16)
+                    K.decode_gemv_pair(y.contiguous(), b["qkv"], qkv, 2, 0, D, H + Hkv, cos, sin)
+                    qkv = qkv.view(rows, 1, -1)
+                elif DECODE_EPILOGUES and rows <= SKINNY_MAX_ROWS and gemm_ops.skinny_qkv_rope_ok(y, b["qkv"], D):
                     qkv = gemm_ops.skinny_qkv_rope(y, b["qkv"], cos, sin, D, H + Hkv).view(rows, 1, -1)
                 else:
                     qkv = rope_ops.apply_rope_qkv(_linear(y, b["qkv"]).view(rows, 1, -1), H, Hkv, D, inv, 0,
                                                   table=(cos, sin))
             else:
-                qkv = _linear(y, b["qkv"]).view(rows, 1, -1)
+                qkv = lin(y, b["qkv"]).view(rows, 1, -1)
             q, k, v = qkv.split([H * D, Hkv * D, Hkv * D], dim=2)
             att = cache.attend(l, q.reshape(rows, 1, H, D), k.view(rows, 1, Hkv, D), v.view(rows, 1, Hkv, D))
-            o = _linear(att.view(rows, H * D), b["o"])
+            o = lin(att.view(rows, H * D), b["o"])
             pa, pm, pre = b["post_attn"], b["post_mlp"], b["pre_mlp"]
             h, y = K.rms_residual(x, o, pa.weight if pa is not None else None, pre.weight, b["mode"],
                                   pa.eps if pa is not None else 0.0, pre.eps)
-            g = _gated(y, b["gu"], b["kind"])
-            d = _linear(g, b["down"])
+            if gemv and DECODE_EPILOGUES:
+                g = torch.empty(rows, b["inter"], device=y.device, dtype=torch.bfloat16)
+                K.decode_gemv_pair(y.contiguous(), b["gu"], g, 1, b["kind"])
+            else:
+                g = _gated(y, b["gu"], b["kind"])
+            d = lin(g, b["down"])
             nxt = self.blocks[l + 1]["in_norm"] if l + 1 < len(self.blocks) else self.norm_f
             x, y = K.rms_residual(h, d, pm.weight if pm is not None else None, nxt.weight, b["mode"],
                                   pm.eps if pm is not None else 0.0, nxt.eps)
-        return _linear(y, self.head.weight)
+        return lin(y, self.head.weight)
 
 
 def _gated(x: Tensor, gu: Tensor, kind: int) -> Tensor:

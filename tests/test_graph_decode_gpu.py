@@ -157,9 +157,10 @@ def test_rope_model_graph_decode_matches_eager(monkeypatch, head_dim):
 
 
 @pytest.mark.parametrize("model_type", ["gemma", "gemma2", "gemma3_text"])  # post-norm modes 2, 1, 0
-def test_gemma_program_step_matches_module_step(model_type):
+@pytest.mark.parametrize("rows", [1, 3, 8])  # 1, 3: decode GEMV path; 8: skinny MFMA kernels
+def test_gemma_program_step_matches_module_step(model_type, rows):
     m = _gemma_model(256, model_type)
-    rows, cap = 3, 32
+    cap = 32
     dec = gd.GraphDecoder(m, rows, cap, 0.0, None)
     assert isinstance(dec.program, gd.GemmaDecodeProgram)
     idx = torch.randint(0, 256, (rows, 7), device="cuda", generator=torch.Generator("cuda").manual_seed(3))

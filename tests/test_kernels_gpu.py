@@ -1133,6 +1133,43 @@ def test_decode_gemv_plain(M, K, N, rpw):
         _close(out, ref, 2e-2, 2e-2, "out")
 
 
+@pytest.mark.parametrize("M,K,I", [(1, 1152, 6912), (3, 64, 128), (4, 1536, 1000), (2, 1792, 33)])
+@pytest.mark.parametrize("kind", [0, 1, 2])
+@pytest.mark.parametrize("ppw", [0, 1, 4])
+def test_decode_gemv_gated(M, K, I, kind, ppw):
+    """Paired-row GEMV, gated mode: act(x·Wgᵀ) ⊙ (x·Wuᵀ) on the packed [gate; up] weight, with
+    gate and up rounded to bf16 first (the unfused GEMM's output), vs fp32 torch."""
+    torch.manual_seed(2)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    gu = (torch.randn(2 * I, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    out = torch.empty(M, I, device=DEV, dtype=torch.bfloat16)
+    _ext.kernels().decode_gemv_pair(x, gu, out, 1, kind, pairs_per_wave=ppw)
+    y = (x.float() @ gu.float().t()).to(torch.bfloat16).float()
+    g, u = y[:, :I], y[:, I:]
+    a = {0: F.gelu(g), 1: F.gelu(g, approximate="tanh"), 2: F.silu(g)}[kind]
+    _close(out, a * u, 3e-2, 2e-2, "gated")
+
+
+@pytest.mark.parametrize("M,K,H,Hkv,D", [(1, 1152, 4, 1, 256), (3, 64, 2, 2, 64), (4, 1536, 8, 1, 512), (2, 96, 3, 1, 32)])
+@pytest.mark.parametrize("ppw", [0, 2])
+def test_decode_gemv_rope(M, K, H, Hkv, D, ppw):
+    """Paired-row GEMV, RoPE mode: rotate-half RoPE on the first H + Hkv heads of the QKV
+    projection (V passed through), both halves rounded to bf16 before the rotation."""
+    torch.manual_seed(3)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    N = (H + 2 * Hkv) * D
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    ang = torch.rand(D // 2, device=DEV) * 6.0
+    cos, sin = torch.cos(ang).view(1, -1).contiguous(), torch.sin(ang).view(1, -1).contiguous()
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    _ext.kernels().decode_gemv_pair(x, w, out, 2, 0, D, H + Hkv, cos, sin, ppw)
+    y = (x.float() @ w.float().t()).to(torch.bfloat16).float().view(M, H + 2 * Hkv, D)
+    x1, x2 = y[..., :D // 2], y[..., D // 2:]
+    rot = torch.cat([x1 * cos - x2 * sin, x2 * cos + x1 * sin], dim=-1)
+    ref = torch.cat([rot[:, :H + Hkv], y[:, H + Hkv:]], dim=1).view(M, N)
+    _close(out, ref, 3e-2, 2e-2, "rope")
+
+
 @pytest.mark.parametrize("M,K,N", [(64, 768, 2304), (64, 768, 3072), (37, 1024, 320), (16, 256, 64), (9, 96, 1040)])
 @pytest.mark.parametrize("act", [0, 2])
 def test_decode_ln_gemm(M, K, N, act):
