@@ -344,6 +344,178 @@ __global__ void __launch_bounds__(256) decode_kernel(const TQ* __restrict__ q, c
   }
 }
 
+// Small-batch decode attention (bf16 cache, one query row, query group G <= 16): one workgroup
+// per (batch, KV head), its 4 waves each own a contiguous quarter of the keys — no split-K launch,
+// no barrier inside the key loop. Per 16-key block a wave computes the scores of all G heads with
+// v_mfma_f32_16x16x32_bf16 (A = 16 K rows straight from global memory, B = the group's queries,
+// held in registers), runs the online softmax per head with two cross-lane exchanges, parks P in
+// its own LDS slice and accumulates P·V on the VALU with lane = D/64 output columns (the V rows
+// read whole and coalesced). The next block's K and V rows are issued before this block's math.
+// The 4 waves' (m, l, O) merge through LDS at the end. Made for the batch-1 GQA shapes where the
+// general kernel's thread-per-key loop is serial (Gemma-3 1B: G = 4, D = 256 — 19 µs per layer).
+// Fused append as in decode_kernel: key S-1 comes from k_new / v_new and is written to the cache.
+template <int D, int GMAX>  // GMAX: the exact query-group size H / Hkv
+__global__ void __launch_bounds__(256) decode_small_kernel(const bf16* __restrict__ q, bf16* __restrict__ kc,
+                                                           bf16* __restrict__ vc, bf16* __restrict__ out, int H,
+                                                           int Hkv, int cap, int S, float scale,
+                                                           const int64_t* __restrict__ S_dev, int64_t q_rs,
+                                                           const bf16* __restrict__ k_new,
+                                                           const bf16* __restrict__ v_new, int64_t kv_rs) {
+  constexpr int KS = D / 32;   // MFMA k-steps per score block
+  constexpr int EPL = D / 64;  // P·V output columns per lane
+  static_assert(EPL >= 1 && (EPL & (EPL - 1)) == 0 && GMAX <= 16, "decode_small geometry");
+  typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+  typedef float f32x4_t __attribute__((ext_vector_type(4)));
+  constexpr int G = GMAX;
+  const int g = blockIdx.x % Hkv, b = blockIdx.x / Hkv;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int r16 = lane & 15, qd = lane >> 4;
+  __shared__ float pl[4][16][16];           // a wave's P block [key][head]
+  __shared__ float wm[4][GMAX], wl[4][GMAX];
+  __shared__ float wo[4][GMAX][D];
+
+  if (S_dev != nullptr) S = (int)min<int64_t>(*S_dev, (int64_t)cap);
+  const size_t head_base = ((size_t)b * Hkv + g) * cap;
+  const size_t new_off = (size_t)b * kv_rs + (size_t)g * D;
+  const float c = scale * 1.4426950408889634f;
+
+  // this lane's query column (head r16 of the group), d-chunks 8qd + 32s
+  uint4 qf[KS];
+  {
+    const bool ok = r16 < G;
+    const bf16* qp = q + (size_t)b * q_rs + (size_t)(g * G + (ok ? r16 : 0)) * D + 8 * qd;
+#pragma unroll
+    for (int s2 = 0; s2 < KS; ++s2) qf[s2] = ok ? *reinterpret_cast<const uint4*>(qp + 32 * s2) : uint4{0u, 0u, 0u, 0u};
+  }
+  // keys of this wave
+  const int per = ((S + 63) / 64) * 16;  // 16-key blocks, a quarter each
+  const int k0 = w * per, k1 = min(S, k0 + per);
+  float m = -INFINITY, l = 0.f;  // for head r16 (replicated over qd)
+  float o[GMAX][EPL];
+#pragma unroll
+  for (int i = 0; i < GMAX; ++i)
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) o[i][e] = 0.f;
+
+  uint4 kf[KS];
+  uint32_t vraw[16][(EPL + 1) / 2];  // this lane's EPL bf16 of 16 V rows
+  auto load_block = [&](int kb) {
+    const int key = min(kb + r16, S - 1);
+    const bool fresh = k_new != nullptr && key == S - 1;
+    const bf16* kr = fresh ? k_new + new_off : kc + (head_base + key) * D;
+#pragma unroll
+    for (int s2 = 0; s2 < KS; ++s2) kf[s2] = *reinterpret_cast<const uint4*>(kr + 32 * s2 + 8 * qd);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int kj = min(kb + j, S - 1);
+      const bool fr = v_new != nullptr && kj == S - 1;
+      const bf16* vr = (fr ? v_new + new_off : vc + (head_base + kj) * D) + EPL * lane;
+      if constexpr (EPL == 1) vraw[j][0] = *reinterpret_cast<const uint16_t*>(vr);
+      else if constexpr (EPL == 2) vraw[j][0] = *reinterpret_cast<const uint32_t*>(vr);
+      else if constexpr (EPL == 4) {
+        const uint2 u = *reinterpret_cast<const uint2*>(vr);
+        vraw[j][0] = u.x;
+        vraw[j][1] = u.y;
+      } else {
+        const uint4 u = *reinterpret_cast<const uint4*>(vr);
+        vraw[j][0] = u.x; vraw[j][1] = u.y; vraw[j][2] = u.z; vraw[j][3] = u.w;
+      }
+    }
+  };
+  // fused append: the wave holding key S-1 writes this step's K / V row into the cache
+  if (k_new != nullptr && k0 < k1 && S - 1 >= k0 && S - 1 < k1) {
+    const bf16* ks = k_new + new_off;
+    const bf16* vs = v_new + new_off;
+    bf16* kd = kc + (head_base + S - 1) * D;
+    bf16* vd = vc + (head_base + S - 1) * D;
+    for (int d = 8 * lane; d < D; d += 512) {
+      *reinterpret_cast<uint4*>(kd + d) = *reinterpret_cast<const uint4*>(ks + d);
+      *reinterpret_cast<uint4*>(vd + d) = *reinterpret_cast<const uint4*>(vs + d);
+    }
+  }
+  if (k0 < k1) load_block(k0);
+  for (int kb = k0; kb < k1; kb += 16) {
+    f32x4_t sacc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s2 = 0; s2 < KS; ++s2)
+      sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, kf[s2]),
+                                                     __builtin_bit_cast(bf16x8_t, qf[s2]), sacc, 0, 0, 0);
+    float vf[16][EPL];  // this block's V values (fp32), taken before the next block's loads land
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) {
+        const uint32_t word = vraw[j][e >> 1];
+        vf[j][e] = EPL == 1 ? __uint_as_float(word << 16)
+                            : ((e & 1) ? __uint_as_float(word & 0xffff0000u) : __uint_as_float(word << 16));
+      }
+    const int nk = min(16, k1 - kb);
+    if (kb + 16 < k1) load_block(kb + 16);
+    // scores of keys kb + 4qd + r for head r16 (masked past the wave's range)
+    float sc[4], bmax = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      sc[r] = (4 * qd + r < nk) ? sacc[r] * c : -INFINITY;
+      bmax = fmaxf(bmax, sc[r]);
+    }
+    bmax = fmaxf(bmax, __shfl_xor(bmax, 16, 64));
+    bmax = fmaxf(bmax, __shfl_xor(bmax, 32, 64));
+    const float mn = fmaxf(m, bmax);
+    const float alpha = m == -INFINITY ? 0.f : exp2f(m - mn);
+    float ps = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float pv = exp2f(sc[r] - mn);
+      ps += pv;
+      pl[w][4 * qd + r][r16] = pv;
+    }
+    ps += __shfl_xor(ps, 16, 64);
+    ps += __shfl_xor(ps, 32, 64);
+    l = l * alpha + ps;
+    m = mn;
+    // every lane needs alpha of every head: head i's value lives in lane i
+    float al[GMAX];
+#pragma unroll
+    for (int i = 0; i < GMAX; ++i) al[i] = __shfl(alpha, i, 64);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's P writes visible to its reads
+#pragma unroll
+    for (int i = 0; i < G; ++i)
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) o[i][e] *= al[i];
+    // keys past the range have p = 0 (their scores are -inf): all 16 rows, no branch
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+#pragma unroll
+      for (int i = 0; i < G; ++i) {
+        const float pw = pl[w][j][i];
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) o[i][e] += pw * vf[j][e];
+      }
+  }
+  // merge the 4 waves
+  if (qd == 0 && r16 < G) {
+    wm[w][r16] = m;
+    wl[w][r16] = l;
+  }
+#pragma unroll
+  for (int i = 0; i < G; ++i)
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) wo[w][i][EPL * lane + e] = o[i][e];
+  __syncthreads();
+  for (int idx = t; idx < G * D; idx += 256) {
+    const int i = idx / D, d = idx - i * D;
+    const float M = fmaxf(fmaxf(wm[0][i], wm[1][i]), fmaxf(wm[2][i], wm[3][i]));
+    float O = 0.f, L = 0.f;
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      const float e = wm[x][i] == -INFINITY ? 0.f : exp2f(wm[x][i] - M);
+      O += e * wo[x][i][d];
+      L += e * wl[x][i];
+    }
+    out[((size_t)b * H + g * G + i) * D + d] = from_f<bf16>(L > 0.f ? O / L : 0.f);
+  }
+}
+
 template <typename TQ>
 __global__ void __launch_bounds__(256) decode_combine_kernel(const float* __restrict__ ws_o,
                                                              const float* __restrict__ ws_ml, TQ* __restrict__ out,
@@ -442,15 +614,6 @@ torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c
     return v >= 64 ? v : 1024;
   }();
   int splits = std::max(1, std::min<int>((512 + items - 1) / items, (int)((S + split_keys - 1) / split_keys)));
-  torch::Tensor ws_o, ws_ml;
-  float* wo = nullptr;
-  float* wm = nullptr;
-  if (splits > 1) {
-    ws_o = torch::empty({(int64_t)splits * B * Tq * H * D}, q.options().dtype(torch::kFloat32));
-    ws_ml = torch::empty({(int64_t)splits * B * Tq * H * 2}, q.options().dtype(torch::kFloat32));
-    wo = ws_o.data_ptr<float>();
-    wm = ws_ml.data_ptr<float>();
-  }
   const int64_t* sdev = nullptr;
   if (seq_len_dev.has_value() && seq_len_dev->defined()) {
     TORCH_CHECK(seq_len_dev->is_cuda() && seq_len_dev->scalar_type() == torch::kInt64 && seq_len_dev->numel() == 1,
@@ -473,6 +636,53 @@ torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c
   const float* ksp = quant ? k_scale->data_ptr<float>() : nullptr;
   const float* vsp = quant ? v_scale->data_ptr<float>() : nullptr;
   auto stream = at::hip::getCurrentHIPStream();
+  // small batches, bf16, one query row: the wave-parallel MFMA kernel (decode_small_kernel).
+  // PENROZ_DECODE_SMALL_ITEMS: the largest B·Hkv it takes (0 disables)
+  static const int small_items = [] {
+    const char* e = std::getenv("PENROZ_DECODE_SMALL_ITEMS");
+    return e ? std::atoi(e) : 64;
+  }();
+  const int G0 = H / Hkv;
+  if (!quant && q.scalar_type() == torch::kBFloat16 && Tq == 1 && items <= small_items &&
+      (G0 == 1 || G0 == 2 || G0 == 4 || G0 == 8 || G0 == 16) && (D == 64 || D == 128 || D == 256 || D == 512) &&
+      G0 * D <= 4096 && (!fuse || kv_rs % 8 == 0)) {
+    const bf16* qp = reinterpret_cast<const bf16*>(q.data_ptr());
+    bf16* kp = reinterpret_cast<bf16*>(kc.data_ptr());
+    bf16* vp = reinterpret_cast<bf16*>(vc.data_ptr());
+    bf16* op = reinterpret_cast<bf16*>(out.data_ptr());
+    const bf16* knp = fuse ? reinterpret_cast<const bf16*>(k_new->data_ptr()) : nullptr;
+    const bf16* vnp = fuse ? reinterpret_cast<const bf16*>(v_new->data_ptr()) : nullptr;
+#define PENROZ_DSMALL(DD, GG)                                                                                       \
+  hipLaunchKernelGGL((decode_small_kernel<DD, GG>), dim3(B * Hkv), dim3(256), 0, stream, qp, kp, vp, op, H, Hkv, cap, \
+                     (int)S, (float)scale, sdev, q_rs, knp, vnp, kv_rs)
+#define PENROZ_DSMALL_G(DD)                      \
+  switch (G0) {                                   \
+    case 1: PENROZ_DSMALL(DD, 1); break;          \
+    case 2: PENROZ_DSMALL(DD, 2); break;          \
+    case 4: PENROZ_DSMALL(DD, 4); break;          \
+    case 8: PENROZ_DSMALL(DD, 8); break;          \
+    default: PENROZ_DSMALL(DD, 16);               \
+  }
+    if (D == 64) PENROZ_DSMALL_G(64)
+    else if (D == 128) PENROZ_DSMALL_G(128)
+    else if (D == 256) PENROZ_DSMALL_G(256)
+    else if (G0 == 1) PENROZ_DSMALL(512, 1);
+    else if (G0 == 2) PENROZ_DSMALL(512, 2);
+    else if (G0 == 4) PENROZ_DSMALL(512, 4);
+    else PENROZ_DSMALL(512, 8);
+#undef PENROZ_DSMALL_G
+#undef PENROZ_DSMALL
+    return out;
+  }
+  torch::Tensor ws_o, ws_ml;
+  float* wo = nullptr;
+  float* wm = nullptr;
+  if (splits > 1) {
+    ws_o = torch::empty({(int64_t)splits * B * Tq * H * D}, q.options().dtype(torch::kFloat32));
+    ws_ml = torch::empty({(int64_t)splits * B * Tq * H * 2}, q.options().dtype(torch::kFloat32));
+    wo = ws_o.data_ptr<float>();
+    wm = ws_ml.data_ptr<float>();
+  }
   dim3 grid(items * splits);
   auto launch = [&](auto qtag, auto ktag) {
     using TQ = decltype(qtag);

@@ -266,13 +266,15 @@ __device__ __forceinline__ float half_sum(float v) {  // sum over the 32 lanes o
 // p / (D/2), j = p % (D/2): half 0 row head·D + j, half 1 row + D/2, both rounded to bf16, then
 // rotated by one position's cos / sin [D/2] for the first nrot heads (skinny_qkv_rope's math).
 // In modes 1 / 2 a wave owns RP output pairs.
-template <int M, bool LN, int RP, int CPL, int EPI = 0>
+// PRO: 0 — x is the bf16 operand; 1 — LN mode (GPT: fp32 residual + delta + dbias, LayerNorm)
+template <int M, int PRO, int RP, int CPL, int EPI = 0>
 __global__ void __launch_bounds__(64) decode_gemv_kernel(
     const float* __restrict__ rin, const bf16* __restrict__ delta, const float* __restrict__ dbias,
     float* __restrict__ rout, const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
     const bf16* __restrict__ x, int64_t x_rs, const bf16* __restrict__ w, const bf16* __restrict__ bias,
     bf16* __restrict__ out, int64_t o_rs, int N, int K, int act, int D = 0, int nrot = 0,
     const float* __restrict__ cosv = nullptr, const float* __restrict__ sinv = nullptr) {
+  constexpr bool LN = PRO == 1;
   const int lane = threadIdx.x, h = lane >> 5, l32 = lane & 31;
   const int nc = K / 8;  // 16-B chunks per row
   const int n0 = blockIdx.x * (EPI == 0 ? 2 * RP : RP);
@@ -299,7 +301,7 @@ __global__ void __launch_bounds__(64) decode_gemv_kernel(
     }
   }
   uint4 xb[M][CPL];
-  if constexpr (!LN) {
+  if constexpr (PRO == 0) {
 #pragma unroll
     for (int m = 0; m < M; ++m)
 #pragma unroll
@@ -592,7 +594,7 @@ void decode_gemv(c10::optional<torch::Tensor> x, c10::optional<torch::Tensor> ri
   const int64_t o_rs = out.stride(0);
   auto launch = [&](auto mt, auto lnt, auto rpt, auto cplt) {
     constexpr int MM = decltype(mt)::value, RR = decltype(rpt)::value, CC = decltype(cplt)::value;
-    constexpr bool LL = decltype(lnt)::value;
+    constexpr int LL = decltype(lnt)::value ? 1 : 0;
     hipLaunchKernelGGL((decode_gemv_kernel<MM, LL, RR, CC>), grid, dim3(64), 0, stream, rp, dp, dbp, rop, gp, bt,
                        (float)eps, xp, x_rs, wp, bp, op, o_rs, N, K, (int)act);
   };
@@ -665,7 +667,7 @@ void decode_gemv_pair(torch::Tensor x, torch::Tensor w, torch::Tensor out, int64
   const float *cp = nullptr, *sp = nullptr;
   if (mode == 1) {
     TORCH_CHECK(kind >= 0 && kind <= 2, "decode_gemv_pair: kind 0 gelu, 1 gelu_tanh, 2 silu");
-  } else {
+  } else if (mode == 2) {
     TORCH_CHECK(D >= 2 && D % 2 == 0 && N % D == 0 && nrot >= 0 && nrot <= N / D, "decode_gemv_pair: RoPE geometry");
     TORCH_CHECK(cosv.has_value() && sinv.has_value() && cosv->is_cuda() && sinv->is_cuda() &&
                     cosv->scalar_type() == torch::kFloat32 && sinv->scalar_type() == torch::kFloat32 &&
@@ -686,9 +688,9 @@ void decode_gemv_pair(torch::Tensor x, torch::Tensor w, torch::Tensor out, int64
   auto launch = [&](auto mt, auto rpt, auto cplt, auto et) {
     constexpr int MM = decltype(mt)::value, RR = decltype(rpt)::value, CC = decltype(cplt)::value;
     constexpr int EE = decltype(et)::value;
-    hipLaunchKernelGGL((decode_gemv_kernel<MM, false, RR, CC, EE>), grid, dim3(64), 0, stream, nullptr, nullptr,
-                       nullptr, nullptr, nullptr, nullptr, 0.f, xp, x_rs, wp, nullptr, op, o_rs, N, K, (int)kind,
-                       (int)D, (int)nrot, cp, sp);
+    hipLaunchKernelGGL((decode_gemv_kernel<MM, 0, RR, CC, EE>), grid, dim3(64), 0, stream, nullptr, nullptr,
+                       nullptr, nullptr, nullptr, nullptr, 0.f, xp, x_rs, wp, nullptr, op, o_rs, N, K,
+                       EE == 1 ? (int)kind : 0, (int)D, (int)nrot, cp, sp);
   };
   auto by_cpl = [&](auto mt, auto rpt, auto et) {
     if (cpl <= 3) launch(mt, rpt, std::integral_constant<int, 3>{}, et);

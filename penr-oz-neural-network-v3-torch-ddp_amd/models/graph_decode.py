@@ -431,6 +431,9 @@ class GemmaDecodeProgram:
         x = torch.nn.functional.embedding(idx.view(rows), self.emb.weight) * self.emb.scale
         first = self.blocks[0]["in_norm"]
         y = K.rmsnorm_fwd(x, first.weight, first.eps)[0]
+        if gemv and DECODE_EPILOGUES and all(b["attn"].rope_theta is not None and b["attn"].head_dim % 2 == 0
+                                             for b in self.blocks):
+            return self._forward_gemv(K, rows, x, y, cache)
         for l, b in enumerate(self.blocks):
             a = b["attn"]
             H, Hkv, D = a.num_heads, a.num_kv_heads, a.head_dim
@@ -464,6 +467,36 @@ class GemmaDecodeProgram:
             x, y = K.rms_residual(h, d, pm.weight if pm is not None else None, nxt.weight, b["mode"],
                                   pm.eps if pm is not None else 0.0, nxt.eps)
         return lin(y, self.head.weight)
+
+    def _forward_gemv(self, K, rows: int, x: Tensor, y: Tensor, cache) -> Tensor:
+        """Batch 1-4: QKV + RoPE, O, gate|up + activation, down and the lm_head as decode GEMVs (one
+        wave per workgroup, one memory round trip); the residual adds + RMSNorms stay the
+        rms_residual kernel (as the GEMVs' prologue — every workgroup normalising the rows itself —
+        it measured neutral: Gemma-3 1B B=1 1.576 / 1.579 vs 1.571 / 1.571 ms, profiles/decode_r5.md)."""
+        for l, b in enumerate(self.blocks):
+            a = b["attn"]
+            H, Hkv, D = a.num_heads, a.num_kv_heads, a.head_dim
+            cos, sin = cache.rope_table((a.rope_theta, D), a._inv_freq(D, x.device), 1)
+            qkv = torch.empty(rows, b["qkv"].shape[0], device=x.device, dtype=torch.bfloat16)
+            K.decode_gemv_pair(y.contiguous(), b["qkv"], qkv, 2, 0, D, H + Hkv, cos, sin)
+            qkv = qkv.view(rows, 1, -1)
+            q, k, v = qkv.split([H * D, Hkv * D, Hkv * D], dim=2)
+            att = cache.attend(l, q.reshape(rows, 1, H, D), k.view(rows, 1, Hkv, D), v.view(rows, 1, Hkv, D))
+            o = torch.empty(rows, b["o"].shape[0], device=x.device, dtype=torch.bfloat16)
+            K.decode_gemv(att.reshape(rows, H * D).contiguous(), None, None, None, None, None, None, 0.0, b["o"], None, o, 0)
+            pa, pm, pre = b["post_attn"], b["post_mlp"], b["pre_mlp"]
+            h, y = K.rms_residual(x, o, pa.weight if pa is not None else None, pre.weight, b["mode"],
+                                  pa.eps if pa is not None else 0.0, pre.eps)
+            g = torch.empty(rows, b["inter"], device=x.device, dtype=torch.bfloat16)
+            K.decode_gemv_pair(y, b["gu"], g, 1, b["kind"])
+            d = torch.empty(rows, b["down"].shape[0], device=x.device, dtype=torch.bfloat16)
+            K.decode_gemv(g, None, None, None, None, None, None, 0.0, b["down"], None, d, 0)
+            nxt = self.blocks[l + 1]["in_norm"] if l + 1 < len(self.blocks) else self.norm_f
+            x, y = K.rms_residual(h, d, pm.weight if pm is not None else None, nxt.weight, b["mode"],
+                                  pm.eps if pm is not None else 0.0, nxt.eps)
+        logits = torch.empty(rows, self.head.weight.shape[0], device=x.device, dtype=torch.bfloat16)
+        K.decode_gemv(y, None, None, None, None, None, None, 0.0, self.head.weight, None, logits, 0)
+        return logits
 
 
 def _gated(x: Tensor, gu: Tensor, kind: int) -> Tensor:
