@@ -12,6 +12,7 @@
 #                                            name contains one of the comma-separated KERNELS
 #   bash bench/gpu.sh decode [gpt2|gemma3-1b] decode bench: eager, graph; batch 64 and 1
 #   bash bench/gpu.sh gemma-train            Gemma-3 1B shaped training bench, B = 8 and 16
+#   bash bench/gpu.sh gemma4-train           Gemma-4-class (gemma4-e2b config) training bench, B = 8
 #   bash bench/gpu.sh attn                   flash attention vs SDPA, head_dim 64 / 128 / 256
 #   bash bench/gpu.sh ddp                    2-rank data-parallel rehearsal on one GPU (gloo)
 #
@@ -98,9 +99,14 @@ case $cmd in
         > gpurun_out/gemma_train_b$B.log 2>&1 || { tail -30 gpurun_out/gemma_train_b$B.log; exit 1; }
       grep '^{' gpurun_out/gemma_train_b$B.log | cut -c1-400
     done ;;
+  gemma4-train)
+    timeout -k 10 400 python bench.py --model gemma4-e2b --batch 8 --steps 5 --warmup 2 --ref-steps 0 \
+      > gpurun_out/gemma4_train_b8.log 2>&1 || { tail -30 gpurun_out/gemma4_train_b8.log; exit 1; }
+    grep '^{' gpurun_out/gemma4_train_b8.log | cut -c1-400 ;;
   attn)
     for cfg in "--B 64 --T 1024 --H 12 --Hkv 12 --D 64" "--B 16 --T 2048 --H 16 --Hkv 8 --D 128" \
-               "--B 16 --T 2048 --H 4 --Hkv 1 --D 256" "--B 8 --T 4096 --H 4 --Hkv 1 --D 256"; do
+               "--B 16 --T 2048 --H 4 --Hkv 1 --D 256" "--B 8 --T 4096 --H 4 --Hkv 1 --D 256" \
+               "--B 8 --T 1024 --H 8 --Hkv 1 --D 512" "--B 8 --T 1024 --H 8 --Hkv 1 --D 256"; do
       timeout -k 10 120 python bench/attn_bench.py $cfg --iters 10 --sdpa > gpurun_out/attn.log 2>&1 \
         || { tail -20 gpurun_out/attn.log; exit 1; }
       grep '^{' gpurun_out/attn.log
