@@ -96,6 +96,8 @@ class GemmaSpec:
 
 
 class GemmaExecutor(GPTExecutor):
+    MAIN_PRIORITY_DEFAULT = False  # measured slightly slower at B = 8 (GPTExecutor._main_stream)
+
     # ------------------------------------------------------------------ pattern match
     @staticmethod
     def match(model, require_fp32: bool = False) -> GemmaSpec | None:
