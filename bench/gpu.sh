@@ -109,7 +109,7 @@ case $cmd in
                "--B 8 --T 1024 --H 8 --Hkv 1 --D 512" "--B 8 --T 1024 --H 8 --Hkv 1 --D 256"; do
       timeout -k 10 120 python bench/attn_bench.py $cfg --iters 10 --sdpa > gpurun_out/attn.log 2>&1 \
         || { tail -20 gpurun_out/attn.log; exit 1; }
-      grep '^{' gpurun_out/attn.log
+      grep '^{' gpurun_out/attn.log | tee -a gpurun_out/attn_all.jsonl
     done ;;
   ddp)
     export PENROZ_BENCH_DEVICE=0 PENROZ_DIST_BACKEND=gloo

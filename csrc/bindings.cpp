@@ -1,5 +1,7 @@
 // Python bindings for the penroz CDNA4 kernels (module ``penroz_kernels``).
 #include <torch/extension.h>
+#include <hip/hip_runtime.h>
+#include <vector>
 
 // layernorm.hip
 void layernorm_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor b, double eps, torch::Tensor y, torch::Tensor mean,
@@ -109,6 +111,29 @@ void flash_attn_gen_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out
                         torch::Tensor dqkv, int64_t H, int64_t Hkv, int64_t D, double scale, double p_drop,
                         int64_t seed);
 
+// A stream whose kernels may only run on the CUs set in `mask` (32-bit words, CU i = bit i % 32
+// of word i / 32): the executor's side stream can be confined to a CU subset so the critical-path
+// GEMMs keep the rest (A/B switch PENROZ_SIDE_CUS). Returned as the raw hipStream_t for
+// torch.cuda.ExternalStream; the stream lives for the process.
+static int64_t cu_masked_stream(int64_t device, std::vector<int64_t> mask) {
+  std::vector<uint32_t> m(mask.begin(), mask.end());
+  int prev = 0;
+  TORCH_CHECK(hipGetDevice(&prev) == hipSuccess, "hipGetDevice failed");
+  TORCH_CHECK(hipSetDevice((int)device) == hipSuccess, "hipSetDevice failed");
+  hipStream_t st = nullptr;
+  const hipError_t e = hipExtStreamCreateWithCUMask(&st, (uint32_t)m.size(), m.data());
+  (void)hipSetDevice(prev);
+  TORCH_CHECK(e == hipSuccess, "hipExtStreamCreateWithCUMask: ", hipGetErrorString(e));
+  return reinterpret_cast<int64_t>(st);
+}
+
+static int64_t cu_count(int64_t device) {
+  int n = 0;
+  TORCH_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, (int)device) == hipSuccess,
+              "hipDeviceGetAttribute failed");
+  return n;
+}
+
 PYBIND11_MODULE(penroz_kernels, m) {
   m.doc() = "penroz hand-written HIP kernels for MI355X (gfx950)";
   m.def("layernorm_fwd", &layernorm_fwd);
@@ -213,6 +238,8 @@ PYBIND11_MODULE(penroz_kernels, m) {
         pybind11::arg("lse"), pybind11::arg("dqkv"), pybind11::arg("H"), pybind11::arg("Hkv"), pybind11::arg("D"),
         pybind11::arg("scale"), pybind11::arg("p_drop"), pybind11::arg("seed"), pybind11::arg("dbias") = pybind11::none(),
         "causal flash-attention backward (head_dim 64) into dqkv; dbias += column sums of dqkv when given");
+  m.def("cu_masked_stream", &cu_masked_stream, "stream restricted to a CU mask (raw hipStream_t)");
+  m.def("cu_count", &cu_count, "compute units of a device");
   m.def("flash_bwd_stamps", &flash_bwd_stamps, pybind11::arg("buf") = pybind11::none(),
         "diagnostic: s_memtime phase sums of the dK/dV kernel into an int64 [6] GPU tensor (None: off)");
   m.def("flash_attn_gen_fwd", &flash_attn_gen_fwd, "causal flash attention forward, head_dim 128 / 256");

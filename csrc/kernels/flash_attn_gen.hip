@@ -20,11 +20,11 @@
 //               forward-shaped, a wave keeps 32 query rows' Q, dO and dQᵀ in registers.
 // At D = 256 the register-resident operands exceed 256 VGPRs: those kernels run one wave per
 // SIMD with the accumulators in the AGPR half of the unified 512-entry register file.
-// D = 512 (Gemma-4 full-attention layers, global_head_dim): the forward keeps Q in registers
-// (128 VGPRs) beside the Oᵀ accumulators (256, the AGPR half); the backward splits D across
-// workgroups — the dK / dV kernel into four column quarters (K / V fragments 256 VGPRs,
-// dKᵀ / dVᵀ quarters 128), the dQ kernel into two halves (Q, dO 256 VGPRs, dQᵀ half 128) — each
-// part recomputing S and dP over the full D.
+// D = 512 (Gemma-4 full-attention layers, global_head_dim): the head dimension is split across the
+// waves of one workgroup, never recomputed — forward and dQ: a wave pair shares 32 query rows,
+// each wave computes the partial S (dP) over its half of D and owns half of the Oᵀ (dQᵀ) columns,
+// the partials meet in LDS; dK / dV (fa512_bwd_dkdv_kernel): an S-wave (K, dVᵀ) and a dP-wave
+// (V, dKᵀ) per 32 keys, P handed over through LDS.
 #include "attn_common.h"
 #include <algorithm>
 #include <cstdlib>
@@ -76,11 +76,16 @@ __device__ __forceinline__ void dma_rows(const bf16* base, size_t RS, int r0, in
 template <int D> constexpr int fwd_waves() { return D >= 256 ? 4 : 2; }
 // column parts of the backward kernels (folded into the 1-D grid as virtual heads, see
 // item_head): dK / dV and dQ accumulators per part
-template <int D> constexpr int kv_parts() { return D >= 512 ? 4 : (D >= 256 ? 2 : 1); }
-template <int D> constexpr int dq_parts() { return D >= 512 ? 2 : 1; }
-// forward: Oᵀ column halves per workgroup at D = 512 (virtual heads; S recomputed by both halves) —
-// Q (128 VGPRs) beside a full Oᵀ (256 accumulators) spilled 2 KB per lane
-template <int D> constexpr int fwd_parts() { return D >= 512 ? 2 : 1; }
+template <int D> constexpr int kv_parts() { return D >= 256 && D < 512 ? 2 : 1; }
+// D = 512 splits the head dimension across the waves of ONE workgroup instead (no recomputation):
+//   forward / dQ: a wave pair shares 32 query rows, each wave holds half of Q (dO) in registers,
+//   computes the partial S (dP) over its half of D and owns half of the Oᵀ (dQᵀ) columns; the
+//   partials meet in LDS (one exchange per tile: S = S_a + S_b, bitwise the same in both waves);
+//   dK / dV: fa512_bwd_dkdv_kernel below (S-wave / dP-wave roles).
+// (The round-4 design recomputed S over the full D in every column part — forward 2×, dQ 2×,
+// dK / dV 4× — and still spilled 350-560 B per lane: 106 / 64 TF fwd / bwd, slower than SDPA.)
+template <int D> constexpr int fwd_dsplit() { return D >= 512 ? 2 : 1; }
+template <int D> constexpr int dq_dsplit() { return D >= 512 ? 2 : 1; }
 
 // ---- work lists (causal balance) ---------------------------------------------------------
 // A causal query block's cost grows with its index, so a grid that fits in ONE round of
@@ -137,48 +142,51 @@ template <int D, bool DROPOUT>
 __global__ void __launch_bounds__(64 * fwd_waves<D>(), (D >= 256 ? 1 : 2))
     fa_gen_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out, float* __restrict__ lse, int T, int H,
                       int Hkv, float scale, float p_drop, uint64_t seed, const WorkList wl, float* __restrict__ ws) {
-  constexpr int NP = D / 64, NS = D / 16, ND = D / 32, NW = fwd_waves<D>();
-  constexpr int BM = 32 * NW, BN = 32, TILE = BN * 128 * NP;
+  constexpr int NP = D / 64, NS = D / 16, ND = D / 32, NW = fwd_waves<D>(), ZS = fwd_dsplit<D>();
+  constexpr int BM = 32 * NW / ZS, BN = 32, TILE = BN * 128 * NP;
   // D = 256: the 32 Q fragments would not fit beside Oᵀ (128 accumulators) in registers; the
   // workgroup's query rows sit in LDS instead (read as B-operand row fragments per tile).
-  // D = 512: the K / V double buffer alone is 128 KB, so Q (128 VGPRs) stays in registers and
-  // each workgroup accumulates one half of Oᵀ (fwd_parts)
+  // D = 512: the K / V double buffer alone is 128 KB; a wave keeps its half of Q (64 VGPRs) in
+  // registers and accumulates its half of Oᵀ (fwd_dsplit)
   constexpr bool QLDS = D == 256;
-  constexpr int NDO = ND / fwd_parts<D>();
+  constexpr int NDO = ND / ZS, NSH = NS / ZS;
   constexpr int QTILE = QLDS ? BM * 128 * NP : 16;
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE + QTILE];
+  constexpr int XB = ZS > 1 ? NW * 16 * 64 * 4 : 16;  // partial-S exchange: [wave][16][64] fp32
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE + QTILE + XB];
   const int nqb = (T + BM - 1) / BM;
   int item, vh, qb, part;
   item_head(wl.n, item, vh);
   item_block(wl, nqb, item, qb, part);
-  const int nbh = gridDim.x / (wl.n * fwd_parts<D>());
-  const int z = vh / nbh, bh = vh - z * nbh;
-  const int do0 = z * NDO;
+  const int nbh = gridDim.x / wl.n;
+  const int bh = vh;
   const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
   const int lane = threadIdx.x & 63, w = wave_id(), hh = lane >> 5;
+  const int rg = w / ZS, dz = w % ZS;  // row group (32 query rows), half of D (ZS = 2)
+  const int do0 = dz * NDO, sq0 = dz * NSH;
   const size_t RS = (size_t)(H + 2 * Hkv) * D;
   const bf16* qbase = qkv + (size_t)b * T * RS + (size_t)h * D;
   const bf16* kbase = qkv + (size_t)b * T * RS + (size_t)(H + hk) * D;
   const bf16* vbase = qkv + (size_t)b * T * RS + (size_t)(H + Hkv + hk) * D;
-  const int q0 = qb * BM + 32 * w;
+  const int q0 = qb * BM + 32 * rg;
   const int qrow = q0 + (lane & 31);
   const float c = scale * kLog2e;
   const float inv_keep = DROPOUT ? 1.f / (1.f - p_drop) : 1.f;
   const char* Qs = smem + 4 * TILE;
+  float* xb = reinterpret_cast<float*>(smem + 4 * TILE + QTILE);
 
-  uint4 qf[QLDS ? 1 : NS];
+  uint4 qf[QLDS ? 1 : NSH];
   if constexpr (QLDS) {
     // both waves' rows, 32 per wave, into one 64-row paneled image
     dma_rows<NP, 32, BM>(qbase, RS, qb * BM + 32 * w, T,
                          __builtin_amdgcn_readfirstlane(lds_addr_of(smem + 4 * TILE)) + w * 32 * 128, lane);
   } else {
 #pragma unroll
-    for (int s = 0; s < NS; ++s)
-      qf[s] = qrow < T ? *reinterpret_cast<const uint4*>(qbase + (size_t)qrow * RS + 16 * s + 8 * hh) : zero4();
+    for (int s = 0; s < NSH; ++s)
+      qf[s] = qrow < T ? *reinterpret_cast<const uint4*>(qbase + (size_t)qrow * RS + 16 * (sq0 + s) + 8 * hh) : zero4();
 #pragma unroll
-    for (int s = 0; s < NS; ++s) launder(qf[s]);
+    for (int s = 0; s < NSH; ++s) launder(qf[s]);
   }
-  // B fragment s of Qᵀ: element j = Q[qrow][16s + 8hh + j]
+  // B fragment s (of this wave's NSH) of Qᵀ: element j = Q[qrow][16(sq0 + s) + 8hh + j]
   auto qfrag = [&](int s) -> uint4 {
     if constexpr (QLDS) return row_frag(panel(Qs, BM, s >> 2), 32 * w, s & 3, lane);
     else return qf[s];
@@ -210,15 +218,31 @@ __global__ void __launch_bounds__(64 * fwd_waves<D>(), (D >= 256 ? 1 : 2))
     if (j + 1 < j1) dma(j + 1);  // buffer (j+1)&1 was released by the previous barrier
     const char* Kt = smem + (j & 1) * 2 * TILE;
     const char* Vt = Kt + TILE;
-    if (kt0 <= q0 + 31 && q0 < T) {
-      f32x16 st;
+    const bool act = kt0 <= q0 + 31 && q0 < T;  // uniform over a wave pair (same rows)
+    f32x16 st;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) st[i] = 0.f;
+    for (int i = 0; i < 16; ++i) st[i] = 0.f;
+    if (act) {
+      const char* Kh = Kt + (sq0 >> 2) * BN * 128;  // this wave's half of D (compile-time offsets below)
 #pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        st = mfma32(row_frag(panel(Kt, BN, s >> 2), 0, s & 3, lane), qfrag(s), st);
+      for (int s = 0; s < NSH; ++s) {
+        st = mfma32(row_frag(panel(Kh, BN, s >> 2), 0, s & 3, lane), qfrag(s), st);
         if ((s & 3) == 3) d_fence<D>();
       }
+    }
+    if constexpr (ZS > 1) {  // S = own half + partner's half (commutative: identical in both waves)
+      // (bases per wave, then immediate offsets: an XOR-indexed address per i was hoisted and spilled)
+      float* xo = xb + w * 16 * 64 + lane;
+      const float* xq = xb + (w + 1 - 2 * dz) * 16 * 64 + lane;
+      if (act)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) xo[64 * i] = st[i];
+      __syncthreads();
+      if (act)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) st[i] += xq[64 * i];
+    }
+    if (act) {
       auto softmax = [&](auto mask_tag) {
         constexpr bool MASK = decltype(mask_tag)::value;
         float tmax = -INFINITY;
@@ -259,13 +283,13 @@ __global__ void __launch_bounds__(64 * fwd_waves<D>(), (D >= 256 ? 1 : 2))
         softmax(std::true_type{});
       else
         softmax(std::false_type{});
+      const char* Vh = Vt + (do0 >> 1) * BN * 128;  // do0 even
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) {
         const uint4 pf = acc_frag(st, ss);
 #pragma unroll
         for (int j = 0; j < NDO; ++j) {
-          const int dh = do0 + j;
-          o[j] = mfma32(tr_frag(panel(Vt, BN, dh >> 1), 16 * ss, 32 * (dh & 1), lane), pf, o[j]);
+          o[j] = mfma32(tr_frag(panel(Vh, BN, j >> 1), 16 * ss, 32 * (j & 1), lane), pf, o[j]);
           if (j & 1) d_fence<D>();
         }
       }
@@ -351,7 +375,7 @@ __global__ void __launch_bounds__(128, 1)
   // stay in registers: no per-slice K / V LDS reads, and 65 KB of LDS per workgroup lets two
   // workgroups (all four SIMDs) share a CU. (Keeping K / V in LDS for one workgroup per CU left
   // two SIMDs idle, spilled 72 registers and was LDS-bandwidth-bound at 87 TF.)
-  constexpr int NDH = ND / kv_parts<D>();  // dKᵀ / dVᵀ column blocks of 32 owned here (D = 512: a quarter)
+  constexpr int NDH = ND / kv_parts<D>();  // dKᵀ / dVᵀ column blocks of 32 owned here (D = 256: a half)
   constexpr bool KVLDS = false;
   constexpr int KVT = BK * 128 * NP;           // 64 key rows
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + (KVLDS ? 2 * KVT : 16)];
@@ -528,6 +552,188 @@ __global__ void __launch_bounds__(128, 1)
   }
 }
 
+// dK / dV at D = 512: 4 waves = 2 key groups (32 keys each, BK = 64) × 2 roles. The S-wave holds
+// cK (32 fragments, full D) and accumulates dVᵀ over all of D; the dP-wave holds V and accumulates
+// dKᵀ. Per 32-row query slice the S-wave computes S and P and hands P (fp32) to its dP-wave through
+// LDS; the dP-wave forms dS = P ⊙ (dP − δ). Each wave then runs 32 MFMAs of S or dP and 32 of dV or
+// dK. The dVᵀ / dKᵀ columns are split over kParts512 workgroups (virtual heads): a wave's 256
+// accumulators for all of D beside its 128 operand registers spilled ~800 B, so S and dP are
+// computed twice instead of four times (the round-4 kernel: column quarters, each wave computing
+// both S and dP). Same work order, query-head split and outputs as fa_gen_bwd_dkdv_kernel.
+constexpr int kParts512 = 2;
+
+template <bool DROPOUT>
+__global__ void __launch_bounds__(256, 1)
+    fa512_bwd_dkdv_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
+                          const float* __restrict__ delta, bf16* __restrict__ dqkv, float* __restrict__ part, int T,
+                          int H, int Hkv, float scale, float p_drop, uint64_t seed) {
+  constexpr int D = 512, NP = D / 64, NS = D / 16, ND = D / 32, NDW = ND / kParts512;
+  constexpr int BK = 64, QS = 32;
+  constexpr int TILE = QS * 128 * NP;          // one 32-row slice of Q (or dO): 32 KB
+  constexpr int STAGE = 2 * TILE + 2 * 256;    // Q | dO | LSE[64] | δ[64]
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 2 * 16 * 64 * 4];
+  float* xp = reinterpret_cast<float*>(smem + 2 * STAGE);  // P hand-over: [key group][16][64]
+  int kb, vh;
+  item_head((T + BK - 1) / BK, kb, vh);
+  const int nbhx = gridDim.x / (((T + BK - 1) / BK) * kParts512);
+  const int zc = vh / nbhx, bhx = vh - zc * nbhx;
+  const int dh0 = zc * NDW;  // this workgroup's dVᵀ / dKᵀ column blocks
+  const int G = H / Hkv;
+  const int GS = part != nullptr ? G : 1;
+  const int gi = bhx % GS, bh = bhx / GS;
+  const int b = bh / Hkv, hk = bh % Hkv;
+  const int lane = threadIdx.x & 63, w = wave_id(), hh = lane >> 5;
+  const int kg = w >> 1, role = w & 1;  // role 0: S, P, dV; role 1: dP, dS, dK
+  const size_t RS = (size_t)(H + 2 * Hkv) * D;
+  const size_t ORS = (size_t)H * D;
+  const int kw0 = kb * BK + 32 * kg;
+  const int key = kw0 + (lane & 31);
+  const float c = scale * kLog2e;
+  const float inv_keep = DROPOUT ? 1.f / (1.f - p_drop) : 1.f;
+
+  const bf16* kbase = qkv + (size_t)b * T * RS + (size_t)(H + hk) * D;
+  const bf16* vbase = qkv + (size_t)b * T * RS + (size_t)(H + Hkv + hk) * D;
+  const bf16* obase = role == 0 ? kbase : vbase;
+  uint4 of[NS];  // role 0: cK, role 1: V (B fragments of Kᵀ / Vᵀ: element j = X[key][16s + 8hh + j])
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+    of[s] = key < T ? *reinterpret_cast<const uint4*>(obase + (size_t)key * RS + 16 * s + 8 * hh) : zero4();
+  if (role == 0)
+#pragma unroll
+    for (int s = 0; s < NS; ++s) of[s] = scale_bf16x8(of[s], c);  // S = Q·(cK)ᵀ (attn_common.h)
+#pragma unroll
+  for (int s = 0; s < NS; ++s) launder(of[s]);
+  f32x16 acc[NDW];  // role 0: dVᵀ, role 1: dKᵀ (column block dh: columns 32(dh0 + dh) ..)
+#pragma unroll
+  for (int dh = 0; dh < NDW; ++dh)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[dh][i] = 0.f;
+
+  const int s_first = (kb * BK) / QS;
+  const int nslices = (T + QS - 1) / QS;
+  const int per_head = nslices - s_first;
+  const int total = (GS == 1 ? G : 1) * per_head;
+  auto head_of = [&](int it) { return hk * G + (GS == 1 ? it / per_head : gi); };
+
+  auto dma = [&](int it) {  // role 0: Q slice (+ LSE), role 1: dO slice (+ δ); key groups take half the panels
+    const int hq = head_of(it);
+    const int qs0 = (s_first + it % per_head) * QS;
+    const unsigned st = __builtin_amdgcn_readfirstlane(lds_addr_of(smem + (it & 1) * STAGE));
+    constexpr int NPW = NP / 2;
+    const int p0 = kg * NPW;
+    if (role == 0)
+      dma_rows<NPW>(qkv + (size_t)b * T * RS + (size_t)hq * D + 64 * p0, RS, qs0, T, st + p0 * QS * 128, lane);
+    else
+      dma_rows<NPW>(dout + (size_t)b * T * ORS + (size_t)hq * D + 64 * p0, ORS, qs0, T, st + TILE + p0 * QS * 128,
+                    lane);
+    if (kg == 0) {
+      const float* sp = (role == 0 ? lse : delta) + ((size_t)b * H + hq) * T + min(qs0 + lane, T - 1);
+      glds4(sp, st + 2 * TILE + 256 * role);
+    }
+  };
+
+  if (total > 0) dma(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int it = 0; it < total; ++it) {
+    if (it + 1 < total) dma(it + 1);
+    const char* stg = smem + (it & 1) * STAGE;
+    const char* Qt = stg;
+    const char* Dt = stg + TILE;
+    const float* lse_s = reinterpret_cast<const float*>(stg + 2 * TILE);
+    const float* del_s = lse_s + 64;
+    const int hq = head_of(it);
+    const int qs0 = (s_first + it % per_head) * QS;
+    const bool act = qs0 + QS - 1 >= kw0 && kw0 < T && qs0 < T;  // uniform over the key group
+    const bool mask = kw0 + 31 > qs0 || qs0 + QS > T || kw0 + 32 > T;
+    f32x16 sc;  // role 0: S (onto −LSE·log2 e), role 1: dP (onto −δ)
+    if (act) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4_t cs = role == 0 ? *reinterpret_cast<const float4_t*>(&lse_s[8 * g + 4 * hh]) * (-kLog2e)
+                                      : (DROPOUT ? float4_t{0.f, 0.f, 0.f, 0.f}
+                                                 : -*reinterpret_cast<const float4_t*>(&del_s[8 * g + 4 * hh]));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) sc[4 * g + k] = cs[k];
+      }
+      const char* At = role == 0 ? Qt : Dt;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        sc = mfma32(row_frag(panel(At, QS, s >> 2), 0, s & 3, lane), of[s], sc);
+        if ((s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+      }
+      if (role == 0) {  // P (masked, before dropout) to the dP-wave; P with dropout for dV
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int i = 4 * g + k, q = qs0 + 8 * g + 4 * hh + k;
+            float p = fexp2(sc[i]);
+            if (mask) p = (key > q || q >= T || key >= T) ? 0.f : p;
+            xp[(kg * 16 + i) * 64 + lane] = p;
+            if constexpr (DROPOUT) p = dropout_keep(seed, b, hq, H, T, q, key, p_drop) ? p * inv_keep : 0.f;
+            sc[i] = p;
+          }
+      }
+    }
+    __syncthreads();
+    if (act) {
+      if (role == 1) {  // dS = P ⊙ (dP − δ)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          float4_t dl = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (DROPOUT) dl = *reinterpret_cast<const float4_t*>(&del_s[8 * g + 4 * hh]);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int i = 4 * g + k;
+            const float p = xp[(kg * 16 + i) * 64 + lane];
+            if constexpr (DROPOUT) {
+              const int q = qs0 + 8 * g + 4 * hh + k;
+              const bool keep = dropout_keep(seed, b, hq, H, T, q, key, p_drop);
+              sc[i] = p * ((keep ? sc[i] * inv_keep : 0.f) - dl[k]);
+            } else {
+              sc[i] = p * sc[i];
+            }
+          }
+        }
+      }
+      // role 0: dVᵀ += dOᵀ·P, role 1: dKᵀ += Qᵀ·dS
+      const char* Bt = (role == 0 ? Dt : Qt) + (dh0 >> 1) * QS * 128;
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const uint4 pf = acc_frag(sc, ss);
+#pragma unroll
+        for (int dh = 0; dh < NDW; ++dh) {
+          acc[dh] = mfma32(tr_frag(panel(Bt, QS, dh >> 1), 16 * ss, 32 * (dh & 1), lane), pf, acc[dh]);
+          if (dh & 1) __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  const float mul = role == 0 ? 1.f : scale;
+  if (key < T && part != nullptr) {  // fp32 partials of this query head: [gi][b·T + key][K | V][hk·D + d]
+    const int Bn = nbhx / (Hkv * GS);
+    float* prow = part + ((size_t)gi * Bn * T + (size_t)b * T + key) * (2 * Hkv * D) + (size_t)hk * D +
+                  (role == 0 ? (size_t)Hkv * D : 0);
+#pragma unroll
+    for (int dh = 0; dh < NDW; ++dh)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<float4*>(prow + 32 * (dh0 + dh) + 8 * g + 4 * hh) =
+            float4{acc[dh][4 * g] * mul, acc[dh][4 * g + 1] * mul, acc[dh][4 * g + 2] * mul, acc[dh][4 * g + 3] * mul};
+  } else if (key < T) {
+    bf16* row = dqkv + ((size_t)b * T + key) * RS + (size_t)(role == 0 ? H + Hkv + hk : H + hk) * D;
+#pragma unroll
+    for (int dh = 0; dh < NDW; ++dh)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        store4(row + 32 * (dh0 + dh) + 8 * g + 4 * hh, acc[dh][4 * g] * mul, acc[dh][4 * g + 1] * mul,
+               acc[dh][4 * g + 2] * mul, acc[dh][4 * g + 3] * mul);
+  }
+}
+
 // Σ over the G query-head partials -> the K | V columns of dqkv (bf16). One thread per 8 columns.
 __global__ void __launch_bounds__(256) fa_gen_kv_reduce(const float* __restrict__ part, bf16* __restrict__ dqkv,
                                                         int64_t rows, int W2, int G, int64_t RS, int64_t col0) {
@@ -591,49 +797,57 @@ __global__ void __launch_bounds__(256) fa_gen_combine(const float* __restrict__ 
 // ------------------------------------------------------------------------------------------
 // dQ: grid (ceil(T/64) query blocks, heaviest first, B*H); forward-shaped: a wave keeps 32
 // query rows' Q, dO, LSE, δ and dQᵀ in registers while sweeping 32-key K/V tiles.
+template <int D> constexpr int dq_waves() { return 2 * dq_dsplit<D>(); }
+
 template <int D, bool DROPOUT>
-__global__ void __launch_bounds__(128, (D >= 256 ? 1 : 2))
+__global__ void __launch_bounds__(64 * dq_waves<D>(), (D >= 256 ? 1 : 2))
     fa_gen_bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
                          const float* __restrict__ delta, bf16* __restrict__ dqkv, int T, int H, int Hkv, float scale,
                          float p_drop, uint64_t seed, const WorkList wl, float* __restrict__ ws) {
-  constexpr int NP = D / 64, NS = D / 16, ND = D / 32;
+  constexpr int NP = D / 64, NS = D / 16, ND = D / 32, ZS = dq_dsplit<D>(), NWQ = dq_waves<D>();
   constexpr int BM = 64, BN = 32, TILE = BN * 128 * NP;
-  __shared__ __attribute__((aligned(16))) char smem[2][2][TILE];
+  constexpr int NSH = NS / ZS;
+  // [stage][K | V] tiles, then (ZS = 2) the partial S / dP exchange [wave][32][64] fp32 — 160 KB at D = 512
+  constexpr int XB = ZS > 1 ? NWQ * 32 * 64 * 4 : 16;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE + XB];
+  float* xb = reinterpret_cast<float*>(smem + 4 * TILE);
   const int nqb = (T + BM - 1) / BM;
   int item, vh, qb, part;
   item_head(wl.n, item, vh);
   item_block(wl, nqb, item, qb, part);
-  const int nbh = gridDim.x / (wl.n * dq_parts<D>());
-  const int z = vh / nbh, bh = vh - z * nbh;
+  const int nbh = gridDim.x / wl.n;
+  const int bh = vh;
   const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
   const int lane = threadIdx.x & 63, w = wave_id(), hh = lane >> 5;
+  const int rg = w / ZS, dz = w % ZS;  // row group (32 query rows), half of D (ZS = 2)
+  const int sq0 = dz * NSH;
   const size_t RS = (size_t)(H + 2 * Hkv) * D;
   const size_t ORS = (size_t)H * D;
   const bf16* kbase = qkv + (size_t)b * T * RS + (size_t)(H + hk) * D;
   const bf16* vbase = qkv + (size_t)b * T * RS + (size_t)(H + Hkv + hk) * D;
-  const int q0 = qb * BM + 32 * w;
+  const int q0 = qb * BM + 32 * rg;
   const int qrow = q0 + (lane & 31);
   const bool qok = qrow < T;
   const float c = scale * kLog2e;
   const float inv_keep = DROPOUT ? 1.f / (1.f - p_drop) : 1.f;
 
-  constexpr int NDQ = ND / dq_parts<D>();  // dQᵀ column blocks of 32 owned here (D = 512: a half)
-  const int dq0 = z * NDQ;
-  uint4 qf[NS], dof[NS];
+  constexpr int NDQ = ND / ZS;  // dQᵀ column blocks of 32 owned here (D = 512: a half)
+  const int dq0 = dz * NDQ;
+  uint4 qf[NSH], dof[NSH];
 #pragma unroll
-  for (int s = 0; s < NS; ++s) {
+  for (int s = 0; s < NSH; ++s) {
     qf[s] = qok ? *reinterpret_cast<const uint4*>(qkv + (size_t)b * T * RS + (size_t)h * D + (size_t)qrow * RS +
-                                                  16 * s + 8 * hh)
+                                                  16 * (sq0 + s) + 8 * hh)
                 : zero4();
     dof[s] = qok ? *reinterpret_cast<const uint4*>(dout + (size_t)b * T * ORS + (size_t)h * D + (size_t)qrow * ORS +
-                                                   16 * s + 8 * hh)
+                                                   16 * (sq0 + s) + 8 * hh)
                  : zero4();
   }
   const size_t rr = ((size_t)b * H + h) * T + qrow;
   float l2 = qok ? lse[rr] * kLog2e : 0.f;
   float dl = qok ? delta[rr] : 0.f;
 #pragma unroll
-  for (int s = 0; s < NS; ++s) {
+  for (int s = 0; s < NSH; ++s) {
     qf[s] = scale_bf16x8(qf[s], c);  // S = (cQ)·Kᵀ (attn_common.h); dQ uses K, not Q
     launder(qf[s]);
     launder(dof[s]);
@@ -649,9 +863,12 @@ __global__ void __launch_bounds__(128, (D >= 256 ? 1 : 2))
 #pragma unroll
     for (int i = 0; i < 16; ++i) dq[dh][i] = 0.f;
 
-  auto dma = [&](int j) {  // wave 0: K tile, wave 1: V tile
-    const unsigned dst = __builtin_amdgcn_readfirstlane(lds_addr_of(smem[j & 1][w]));
-    dma_rows<NP>(w == 0 ? kbase : vbase, RS, j * BN, T, dst, lane);
+  auto dma = [&](int j) {  // even waves: K tile, odd waves: V tile (NWQ = 4: half the panels each)
+    constexpr int NPW = NP * 2 / NWQ;
+    const int role = w & 1, p0 = (w >> 1) * NPW;
+    const unsigned dst = __builtin_amdgcn_readfirstlane(lds_addr_of(smem + ((j & 1) * 2 + role) * TILE)) +
+                         p0 * BN * 128;
+    dma_rows<NPW>((role == 0 ? kbase : vbase) + 64 * p0, RS, j * BN, T, dst, lane);
   };
   if (j0 < j1) dma(j0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -659,21 +876,43 @@ __global__ void __launch_bounds__(128, (D >= 256 ? 1 : 2))
   for (int j = j0; j < j1; ++j) {
     const int kt0 = j * BN;
     if (j + 1 < j1) dma(j + 1);
-    const char* Kt = smem[j & 1][0];
-    const char* Vt = smem[j & 1][1];
-    if (kt0 <= q0 + 31 && q0 < T) {
-      f32x16 st, dp;
+    const char* Kt = smem + (j & 1) * 2 * TILE;
+    const char* Vt = Kt + TILE;
+    const bool act = kt0 <= q0 + 31 && q0 < T;  // uniform over a wave pair (same rows)
+    f32x16 st, dp;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        st[i] = -l2;  // S accumulates onto −LSE·log2(e): P = exp2(S)
-        dp[i] = DROPOUT ? 0.f : -dl;
-      }
+    for (int i = 0; i < 16; ++i) {  // the row constants enter one half's partial only
+      st[i] = dz == 0 ? -l2 : 0.f;  // S accumulates onto −LSE·log2(e): P = exp2(S)
+      dp[i] = DROPOUT || dz != 0 ? 0.f : -dl;
+    }
+    if (act) {
+      const char* Kh = Kt + (sq0 >> 2) * BN * 128;  // this wave's half of D (compile-time offsets below)
+      const char* Vh = Vt + (sq0 >> 2) * BN * 128;
 #pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        st = mfma32(row_frag(panel(Kt, BN, s >> 2), 0, s & 3, lane), qf[s], st);
-        dp = mfma32(row_frag(panel(Vt, BN, s >> 2), 0, s & 3, lane), dof[s], dp);
+      for (int s = 0; s < NSH; ++s) {
+        st = mfma32(row_frag(panel(Kh, BN, s >> 2), 0, s & 3, lane), qf[s], st);
+        dp = mfma32(row_frag(panel(Vh, BN, s >> 2), 0, s & 3, lane), dof[s], dp);
         if (s & 1) d_fence<D>();
       }
+    }
+    if constexpr (ZS > 1) {  // full S, dP = own half + partner's half (identical in both waves)
+      float* xo = xb + w * 32 * 64 + lane;  // per-wave bases, immediate offsets
+      const float* xq = xb + (w + 1 - 2 * dz) * 32 * 64 + lane;
+      if (act)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          xo[64 * i] = st[i];
+          xo[64 * (16 + i)] = dp[i];
+        }
+      __syncthreads();
+      if (act)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          st[i] += xq[64 * i];
+          dp[i] += xq[64 * (16 + i)];
+        }
+    }
+    if (act) {
       auto grads = [&](auto mask_tag) {
         constexpr bool MASK = decltype(mask_tag)::value;
 #pragma unroll
@@ -693,13 +932,13 @@ __global__ void __launch_bounds__(128, (D >= 256 ? 1 : 2))
         grads(std::true_type{});
       else
         grads(std::false_type{});
+      const char* Kq = Kt + (dq0 >> 1) * BN * 128;  // dq0 even (or 0)
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) {
         const uint4 sf = acc_frag(st, ss);
 #pragma unroll
         for (int j = 0; j < NDQ; ++j) {
-          const int dh = dq0 + j;
-          dq[j] = mfma32(tr_frag(panel(Kt, BN, dh >> 1), 16 * ss, 32 * (dh & 1), lane), sf, dq[j]);
+          dq[j] = mfma32(tr_frag(panel(Kq, BN, j >> 1), 16 * ss, 32 * (j & 1), lane), sf, dq[j]);
           if (j & 1) d_fence<D>();
         }
       }
@@ -864,10 +1103,10 @@ void flash_attn_gen_fwd(torch::Tensor qkv, torch::Tensor out, torch::Tensor lse,
   const bf16* q = reinterpret_cast<const bf16*>(qkv.data_ptr());
   bf16* o = reinterpret_cast<bf16*>(out.data_ptr());
   FA_GEN_DISPATCH(D, p_drop > 0.0, {
-    constexpr int NW = fwd_waves<DD>(), BM = 32 * NW, ZP = fwd_parts<DD>();
-    const int nqb = (T + BM - 1) / BM, nvh = B * (int)H * ZP;
+    constexpr int NW = fwd_waves<DD>(), BM = 32 * NW / fwd_dsplit<DD>();
+    const int nqb = (T + BM - 1) / BM, nvh = B * (int)H;
     // measured: ~2.7 µs per 32-key tile for a 128-row, D = 256 block (Gemma-3 1B step)
-    const double tile_us = 2.7 * (BM / 128.0) * (DD + DD / ZP) / 512.0;
+    const double tile_us = 2.7 * (BM / 128.0) * DD / 256.0;
     const auto kern = fa_gen_fwd_kernel<DD, DR>;
     const WorkList wl = attn_plan(nqb, nvh, chip_slots((const void*)kern, 64 * NW), BM, 32, T, DD, tile_us);
     torch::Tensor ws;
@@ -905,31 +1144,36 @@ void flash_attn_gen_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out
   if (split) part = torch::empty({(int64_t)G * B * T, 2 * Hkv * D}, qkv.options().dtype(torch::kFloat32));
   // 1-D grids: items (key / query blocks) × the column parts of D (dK / dV: 2 at D = 256, 4 at
   // 512; dQ: 2 at 512) × heads
-  const int64_t nkv = (int64_t)nkb * B * Hkv * (split ? G : 1) * (D >= 512 ? 4 : (D >= 256 ? 2 : 1));
+  const int64_t nkv = (int64_t)nkb * B * Hkv * (split ? G : 1) * (D == 256 ? 2 : (D == 512 ? kParts512 : 1));
   FA_GEN_DISPATCH(D, p_drop > 0.0, {
     hipLaunchKernelGGL((fa_gen_bwd_pre_kernel<DD>), dim3(((int64_t)rows * (DD / 8) + 255) / 256), dim3(256), 0,
                        stream, d, reinterpret_cast<const bf16*>(out.data_ptr()), delta.data_ptr<float>(), B, T,
                        (int)H);
-    hipLaunchKernelGGL((fa_gen_bwd_dkdv_kernel<DD, DR>), dim3((unsigned)nkv), dim3(128), 0, stream, q, d,
-                       lse.data_ptr<float>(), delta.data_ptr<float>(), g, split ? part.data_ptr<float>() : nullptr, T,
-                       (int)H, (int)Hkv, (float)scale, (float)p_drop, (uint64_t)seed);
+    if constexpr (DD == 512)
+      hipLaunchKernelGGL((fa512_bwd_dkdv_kernel<DR>), dim3((unsigned)nkv), dim3(256), 0, stream, q, d,
+                         lse.data_ptr<float>(), delta.data_ptr<float>(), g, split ? part.data_ptr<float>() : nullptr,
+                         T, (int)H, (int)Hkv, (float)scale, (float)p_drop, (uint64_t)seed);
+    else
+      hipLaunchKernelGGL((fa_gen_bwd_dkdv_kernel<DD, DR>), dim3((unsigned)nkv), dim3(128), 0, stream, q, d,
+                         lse.data_ptr<float>(), delta.data_ptr<float>(), g, split ? part.data_ptr<float>() : nullptr,
+                         T, (int)H, (int)Hkv, (float)scale, (float)p_drop, (uint64_t)seed);
     if (split) {
       const int64_t n8 = (int64_t)B * T * (2 * Hkv * DD / 8);
       hipLaunchKernelGGL(fa_gen_kv_reduce, dim3((unsigned)std::min<int64_t>((n8 + 255) / 256, 4096)), dim3(256), 0,
                          stream, part.data_ptr<float>(), g, (int64_t)B * T, (int)(2 * Hkv * DD), G,
                          (int64_t)(H + 2 * Hkv) * DD, (int64_t)H * DD);
     }
-    constexpr int ZQ = dq_parts<DD>();
-    const int nqb = (T + 63) / 64, nvh = B * (int)H * ZQ;
+    constexpr int NWQ = dq_waves<DD>();
+    const int nqb = (T + 63) / 64, nvh = B * (int)H;
     // measured: ~2.9 µs per 32-key tile for a 64-row, D = 256 block (Gemma-3 1B step)
-    const double tile_us = 2.9 * (DD + DD / ZQ) / 512.0;
+    const double tile_us = 2.9 * DD / 256.0;
     const auto kq = fa_gen_bwd_dq_kernel<DD, DR>;
-    const WorkList wl = attn_plan(nqb, nvh, chip_slots((const void*)kq, 128), 64, 32, T, DD, tile_us);
+    const WorkList wl = attn_plan(nqb, nvh, chip_slots((const void*)kq, 64 * NWQ), 64, 32, T, DD, tile_us);
     torch::Tensor ws;
     const int nsr = (nqb - wl.split0) * 64;
     if (wl.split0 < nqb) ws = torch::empty({2 * (int64_t)B * H * nsr * DD}, lse.options());
     float* wsp = wl.split0 < nqb ? ws.data_ptr<float>() : nullptr;
-    hipLaunchKernelGGL(kq, dim3(wl.n * nvh), dim3(128), 0, stream, q, d, lse.data_ptr<float>(),
+    hipLaunchKernelGGL(kq, dim3(wl.n * nvh), dim3(64 * NWQ), 0, stream, q, d, lse.data_ptr<float>(),
                        delta.data_ptr<float>(), g, T, (int)H, (int)Hkv, (float)scale, (float)p_drop, (uint64_t)seed,
                        wl, wsp);
     if (wsp)

@@ -127,6 +127,33 @@ def _site_seed(seed: int, site: int) -> int:
     return (seed * 1_000_003 + 7_919 * (site + 1) + 0x5BD1E995) & 0x7FFFFFFFFFFFFFFF
 
 
+def cu_mask_words(spec: str, n_cu: int) -> list[int]:
+    """CU mask words for PENROZ_SIDE_CUS: ``stride:k[:o]`` = CUs i with i % k == o, ``first:n`` =
+    CUs 0..n-1 (bit i of word i // 32 = CU i)."""
+    kind, _, rest = spec.partition(":")
+    if kind == "stride":
+        k, _, o = rest.partition(":")
+        sel = [i for i in range(n_cu) if i % int(k) == int(o or 0)]
+    elif kind == "first":
+        sel = list(range(min(int(rest), n_cu)))
+    else:
+        raise ValueError(f"PENROZ_SIDE_CUS: want stride:k[:o] or first:n, got {spec!r}")
+    if not sel:
+        raise ValueError(f"PENROZ_SIDE_CUS={spec!r} selects no CU")
+    words = [0] * ((n_cu + 31) // 32)
+    for i in sel:
+        words[i // 32] |= 1 << (i % 32)
+    return words
+
+
+def _cu_masked_stream(device: torch.device, spec: str):
+    """The side stream confined to a CU subset (A/B of critical-path GEMM interference)."""
+    k = _ext.kernels()
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    ptr = k.cu_masked_stream(idx, cu_mask_words(spec, k.cu_count(idx)))
+    return torch.cuda.ExternalStream(ptr, device=device)
+
+
 class GPTExecutor:
     # ------------------------------------------------------------------ pattern match
     @staticmethod
@@ -563,7 +590,8 @@ class GPTExecutor:
         import os
         self._side = None
         if self.device.type == "cuda" and os.environ.get("PENROZ_WGRAD_STREAM", "1") != "0":
-            self._side = torch.cuda.Stream(device=self.device)
+            cus = os.environ.get("PENROZ_SIDE_CUS", "")
+            self._side = _cu_masked_stream(self.device, cus) if cus else torch.cuda.Stream(device=self.device)
         self._buf_free = {}
 
     def _side_call(self, operand: Tensor, fn):

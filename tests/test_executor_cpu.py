@@ -1,6 +1,8 @@
 """GPT pattern lowering (CPU): which layer lists the fused executor accepts."""
 import copy
 
+import pytest
+
 import bench
 from penroz.models.executor import GPTExecutor
 from penroz.models.mapper import Mapper
@@ -173,3 +175,14 @@ def test_wgrad_ranges_chunked_after_learning(monkeypatch):
     assert torch.allclose(A[0:3], d1[:, :3].t() @ xA, atol=1e-5) and torch.all(A[3:] == 0)
     # the changed pattern makes zero_grad clear everything from now on
     assert ex._wgrad_ranges_invalid and ex._zero_gaps is None
+
+
+def test_side_stream_cu_mask_words():
+    from penroz.models.executor import cu_mask_words
+    w = cu_mask_words("stride:4", 256)
+    assert len(w) == 8 and all(x == 0x11111111 for x in w)
+    w = cu_mask_words("stride:8:1", 256)
+    assert all(x == 0x02020202 for x in w)
+    assert cu_mask_words("first:40", 256)[:2] == [0xFFFFFFFF, 0xFF] and cu_mask_words("first:40", 256)[2:] == [0] * 6
+    with pytest.raises(ValueError):
+        cu_mask_words("half", 256)
