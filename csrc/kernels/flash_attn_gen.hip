@@ -69,23 +69,50 @@ __device__ __forceinline__ void dma_rows(const bf16* base, size_t RS, int r0, in
     }
 }
 
+// D-split exchange (D = 512): the ZS waves of row group rg each hold a partial accumulator over
+// their part of D; after this every one of them holds the sum, added in part order (so the ZS
+// copies are bitwise identical). x4 = this lane's slot of an LDS [wave][4][64] float4 image
+// (conflict-free b128 rows); `act` is uniform over the row group. Ends with the readers done
+// only if the caller adds a barrier before reusing the image.
+template <int ZS>
+__device__ __forceinline__ void dsplit_sum(f32x16& v, float4_t* x4, int w, int rg, bool act) {
+  if (act)
+#pragma unroll
+    for (int i4 = 0; i4 < 4; ++i4) x4[(w * 4 + i4) * 64] = float4_t{v[4 * i4], v[4 * i4 + 1], v[4 * i4 + 2], v[4 * i4 + 3]};
+  __syncthreads();
+  if (act) {
+    const float4_t* r4 = x4 + rg * ZS * 4 * 64;
+#pragma unroll
+    for (int i4 = 0; i4 < 4; ++i4) {
+      float4_t a = r4[i4 * 64];
+#pragma unroll
+      for (int z = 1; z < ZS; ++z) a += r4[(z * 4 + i4) * 64];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[4 * i4 + k] = a[k];
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // forward
 // D = 256 runs 4 waves per workgroup (128 query rows): its LDS (K/V double buffer + the Q image,
 // 128 KB) admits one workgroup per CU, and 4 waves then occupy all four SIMDs.
-template <int D> constexpr int fwd_waves() { return D >= 256 ? 4 : 2; }
+template <int D> constexpr int fwd_waves() { return D >= 512 ? 8 : (D >= 256 ? 4 : 2); }
 // column parts of the backward kernels (folded into the 1-D grid as virtual heads, see
 // item_head): dK / dV and dQ accumulators per part
 template <int D> constexpr int kv_parts() { return D >= 256 && D < 512 ? 2 : 1; }
 // D = 512 splits the head dimension across the waves of ONE workgroup instead (no recomputation):
-//   forward / dQ: a wave pair shares 32 query rows, each wave holds half of Q (dO) in registers,
-//   computes the partial S (dP) over its half of D and owns half of the Oᵀ (dQᵀ) columns; the
-//   partials meet in LDS (one exchange per tile: S = S_a + S_b, bitwise the same in both waves);
+//   forward: 8 waves, a group of four shares 32 query rows; each wave holds a quarter of Q in
+//   registers, computes the partial S over its quarter of D and owns a quarter of the Oᵀ columns;
+//   the partials meet in LDS (one exchange per tile, summed in quarter order: bitwise the same S
+//   in all four waves). ≤ 256 registers per wave: two waves per SIMD, no spills (the 4-wave halves
+//   version spilled ~90 B per lane and ran fwd at 195 TF);
+//   dQ: the same (8 waves, quarters of Q, dO; partial S, then partial dP exchanged);
 //   dK / dV: fa512_bwd_dkdv_kernel below (S-wave / dP-wave roles).
 // (The round-4 design recomputed S over the full D in every column part — forward 2×, dQ 2×,
 // dK / dV 4× — and still spilled 350-560 B per lane: 106 / 64 TF fwd / bwd, slower than SDPA.)
-template <int D> constexpr int fwd_dsplit() { return D >= 512 ? 2 : 1; }
-template <int D> constexpr int dq_dsplit() { return D >= 512 ? 2 : 1; }
+template <int D> constexpr int fwd_dsplit() { return D >= 512 ? 4 : 1; }
+template <int D> constexpr int dq_dsplit() { return D >= 512 ? 4 : 1; }
 
 // ---- work lists (causal balance) ---------------------------------------------------------
 // A causal query block's cost grows with its index, so a grid that fits in ONE round of
@@ -146,12 +173,12 @@ __global__ void __launch_bounds__(64 * fwd_waves<D>(), (D >= 256 ? 1 : 2))
   constexpr int BM = 32 * NW / ZS, BN = 32, TILE = BN * 128 * NP;
   // D = 256: the 32 Q fragments would not fit beside Oᵀ (128 accumulators) in registers; the
   // workgroup's query rows sit in LDS instead (read as B-operand row fragments per tile).
-  // D = 512: the K / V double buffer alone is 128 KB; a wave keeps its half of Q (64 VGPRs) in
-  // registers and accumulates its half of Oᵀ (fwd_dsplit)
+  // D = 512: the K / V double buffer alone is 128 KB; a wave keeps its quarter of Q (32 VGPRs) in
+  // registers and accumulates its quarter of Oᵀ (fwd_dsplit)
   constexpr bool QLDS = D == 256;
   constexpr int NDO = ND / ZS, NSH = NS / ZS;
-  constexpr int QTILE = QLDS ? BM * 128 * NP : 16;
-  constexpr int XB = ZS > 1 ? NW * 16 * 64 * 4 : 16;  // partial-S exchange: [wave][16][64] fp32
+  constexpr int QTILE = QLDS ? BM * 128 * NP : (ZS > 1 ? 0 : 16);
+  constexpr int XB = ZS > 1 ? NW * 16 * 64 * 4 : 16;  // partial-S exchange: [wave][4][64 lanes] float4
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE + QTILE + XB];
   const int nqb = (T + BM - 1) / BM;
   int item, vh, qb, part;
@@ -161,7 +188,7 @@ __global__ void __launch_bounds__(64 * fwd_waves<D>(), (D >= 256 ? 1 : 2))
   const int bh = vh;
   const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
   const int lane = threadIdx.x & 63, w = wave_id(), hh = lane >> 5;
-  const int rg = w / ZS, dz = w % ZS;  // row group (32 query rows), half of D (ZS = 2)
+  const int rg = w / ZS, dz = w % ZS;  // row group (32 query rows), part of D (ZS = 4: a quarter)
   const int do0 = dz * NDO, sq0 = dz * NSH;
   const size_t RS = (size_t)(H + 2 * Hkv) * D;
   const bf16* qbase = qkv + (size_t)b * T * RS + (size_t)h * D;
@@ -202,20 +229,21 @@ __global__ void __launch_bounds__(64 * fwd_waves<D>(), (D >= 256 ? 1 : 2))
     for (int i = 0; i < 16; ++i) o[dh][i] = 0.f;
   float m = -1e30f, l = 0.f;
 
-  auto dma = [&](int j) {  // even waves: K tile, odd waves: V tile (NW = 4: half the panels each)
+  auto dma = [&](int j, int ln) {  // even waves: K tile, odd waves: V tile (NW = 4: half the panels each)
     constexpr int NPW = NP * 2 / NW;
     const int p0 = (w >> 1) * NPW;
     const unsigned dst = __builtin_amdgcn_readfirstlane(lds_addr_of(smem + ((j & 1) * 2 + (w & 1)) * TILE)) +
                          p0 * BN * 128;
-    dma_rows<NPW>(((w & 1) == 0 ? kbase : vbase) + 64 * p0, RS, j * BN, T, dst, lane);
+    dma_rows<NPW>(((w & 1) == 0 ? kbase : vbase) + 64 * p0, RS, j * BN, T, dst, ln);
   };
 
-  if (j0 < j1) dma(j0);
+  if (j0 < j1) dma(j0, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int j = j0; j < j1; ++j) {
     const int kt0 = j * BN;
-    if (j + 1 < j1) dma(j + 1);  // buffer (j+1)&1 was released by the previous barrier
+    const int ln = lane;
+    if (j + 1 < j1) dma(j + 1, ln);  // buffer (j+1)&1 was released by the previous barrier
     const char* Kt = smem + (j & 1) * 2 * TILE;
     const char* Vt = Kt + TILE;
     const bool act = kt0 <= q0 + 31 && q0 < T;  // uniform over a wave pair (same rows)
@@ -226,22 +254,11 @@ __global__ void __launch_bounds__(64 * fwd_waves<D>(), (D >= 256 ? 1 : 2))
       const char* Kh = Kt + (sq0 >> 2) * BN * 128;  // this wave's half of D (compile-time offsets below)
 #pragma unroll
       for (int s = 0; s < NSH; ++s) {
-        st = mfma32(row_frag(panel(Kh, BN, s >> 2), 0, s & 3, lane), qfrag(s), st);
+        st = mfma32(row_frag(panel(Kh, BN, s >> 2), 0, s & 3, ln), qfrag(s), st);
         if ((s & 3) == 3) d_fence<D>();
       }
     }
-    if constexpr (ZS > 1) {  // S = own half + partner's half (commutative: identical in both waves)
-      // (bases per wave, then immediate offsets: an XOR-indexed address per i was hoisted and spilled)
-      float* xo = xb + w * 16 * 64 + lane;
-      const float* xq = xb + (w + 1 - 2 * dz) * 16 * 64 + lane;
-      if (act)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) xo[64 * i] = st[i];
-      __syncthreads();
-      if (act)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) st[i] += xq[64 * i];
-    }
+    if constexpr (ZS > 1) dsplit_sum<ZS>(st, reinterpret_cast<float4_t*>(xb) + ln, w, rg, act);
     if (act) {
       auto softmax = [&](auto mask_tag) {
         constexpr bool MASK = decltype(mask_tag)::value;
@@ -289,7 +306,7 @@ __global__ void __launch_bounds__(64 * fwd_waves<D>(), (D >= 256 ? 1 : 2))
         const uint4 pf = acc_frag(st, ss);
 #pragma unroll
         for (int j = 0; j < NDO; ++j) {
-          o[j] = mfma32(tr_frag(panel(Vh, BN, j >> 1), 16 * ss, 32 * (j & 1), lane), pf, o[j]);
+          o[j] = mfma32(tr_frag(panel(Vh, BN, j >> 1), 16 * ss, 32 * (j & 1), ln), pf, o[j]);
           if (j & 1) d_fence<D>();
         }
       }
@@ -807,8 +824,9 @@ __global__ void __launch_bounds__(64 * dq_waves<D>(), (D >= 256 ? 1 : 2))
   constexpr int NP = D / 64, NS = D / 16, ND = D / 32, ZS = dq_dsplit<D>(), NWQ = dq_waves<D>();
   constexpr int BM = 64, BN = 32, TILE = BN * 128 * NP;
   constexpr int NSH = NS / ZS;
-  // [stage][K | V] tiles, then (ZS = 2) the partial S / dP exchange [wave][32][64] fp32 — 160 KB at D = 512
-  constexpr int XB = ZS > 1 ? NWQ * 32 * 64 * 4 : 16;
+  // [stage][K | V] tiles, then (ZS > 1) the partial S / dP exchange image [wave][4][64] float4 —
+  // 160 KB at D = 512 (S and dP go through it one after the other)
+  constexpr int XB = ZS > 1 ? NWQ * 16 * 64 * 4 : 16;
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE + XB];
   float* xb = reinterpret_cast<float*>(smem + 4 * TILE);
   const int nqb = (T + BM - 1) / BM;
@@ -819,7 +837,7 @@ __global__ void __launch_bounds__(64 * dq_waves<D>(), (D >= 256 ? 1 : 2))
   const int bh = vh;
   const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
   const int lane = threadIdx.x & 63, w = wave_id(), hh = lane >> 5;
-  const int rg = w / ZS, dz = w % ZS;  // row group (32 query rows), half of D (ZS = 2)
+  const int rg = w / ZS, dz = w % ZS;  // row group (32 query rows), part of D (ZS = 4: a quarter)
   const int sq0 = dz * NSH;
   const size_t RS = (size_t)(H + 2 * Hkv) * D;
   const size_t ORS = (size_t)H * D;
@@ -831,7 +849,7 @@ __global__ void __launch_bounds__(64 * dq_waves<D>(), (D >= 256 ? 1 : 2))
   const float c = scale * kLog2e;
   const float inv_keep = DROPOUT ? 1.f / (1.f - p_drop) : 1.f;
 
-  constexpr int NDQ = ND / ZS;  // dQᵀ column blocks of 32 owned here (D = 512: a half)
+  constexpr int NDQ = ND / ZS;  // dQᵀ column blocks of 32 owned here (D = 512: a quarter)
   const int dq0 = dz * NDQ;
   uint4 qf[NSH], dof[NSH];
 #pragma unroll
@@ -863,7 +881,7 @@ __global__ void __launch_bounds__(64 * dq_waves<D>(), (D >= 256 ? 1 : 2))
 #pragma unroll
     for (int i = 0; i < 16; ++i) dq[dh][i] = 0.f;
 
-  auto dma = [&](int j) {  // even waves: K tile, odd waves: V tile (NWQ = 4: half the panels each)
+  auto dma = [&](int j) {  // even waves: K tile, odd waves: V tile (NWQ = 8: a quarter of the panels each)
     constexpr int NPW = NP * 2 / NWQ;
     const int role = w & 1, p0 = (w >> 1) * NPW;
     const unsigned dst = __builtin_amdgcn_readfirstlane(lds_addr_of(smem + ((j & 1) * 2 + role) * TILE)) +
@@ -881,9 +899,9 @@ __global__ void __launch_bounds__(64 * dq_waves<D>(), (D >= 256 ? 1 : 2))
     const bool act = kt0 <= q0 + 31 && q0 < T;  // uniform over a wave pair (same rows)
     f32x16 st, dp;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {  // the row constants enter one half's partial only
-      st[i] = dz == 0 ? -l2 : 0.f;  // S accumulates onto −LSE·log2(e): P = exp2(S)
-      dp[i] = DROPOUT || dz != 0 ? 0.f : -dl;
+    for (int i = 0; i < 16; ++i) {  // (ZS > 1: the row constants are added after the exchange)
+      st[i] = ZS > 1 ? 0.f : -l2;  // S accumulates onto −LSE·log2(e): P = exp2(S)
+      dp[i] = DROPOUT || ZS > 1 ? 0.f : -dl;
     }
     if (act) {
       const char* Kh = Kt + (sq0 >> 2) * BN * 128;  // this wave's half of D (compile-time offsets below)
@@ -895,22 +913,16 @@ __global__ void __launch_bounds__(64 * dq_waves<D>(), (D >= 256 ? 1 : 2))
         if (s & 1) d_fence<D>();
       }
     }
-    if constexpr (ZS > 1) {  // full S, dP = own half + partner's half (identical in both waves)
-      float* xo = xb + w * 32 * 64 + lane;  // per-wave bases, immediate offsets
-      const float* xq = xb + (w + 1 - 2 * dz) * 32 * 64 + lane;
-      if (act)
+    if constexpr (ZS > 1) {  // full S, then full dP (Σ of the row group's parts, in part order)
+      float4_t* x4 = reinterpret_cast<float4_t*>(xb) + lane;
+      dsplit_sum<ZS>(st, x4, w, rg, act);
+      __syncthreads();  // every S read done before the image takes dP
+      dsplit_sum<ZS>(dp, x4, w, rg, act);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          xo[64 * i] = st[i];
-          xo[64 * (16 + i)] = dp[i];
-        }
-      __syncthreads();
-      if (act)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          st[i] += xq[64 * i];
-          dp[i] += xq[64 * (16 + i)];
-        }
+      for (int i = 0; i < 16; ++i) {
+        st[i] -= l2;
+        if constexpr (!DROPOUT) dp[i] -= dl;
+      }
     }
     if (act) {
       auto grads = [&](auto mask_tag) {
