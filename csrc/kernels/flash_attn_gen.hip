@@ -97,7 +97,7 @@ __device__ __forceinline__ void dsplit_sum(f32x16& v, float4_t* x4, int w, int r
 // forward
 // D = 256 runs 4 waves per workgroup (128 query rows): its LDS (K/V double buffer + the Q image,
 // 128 KB) admits one workgroup per CU, and 4 waves then occupy all four SIMDs.
-template <int D> constexpr int fwd_waves() { return D >= 512 ? 8 : (D >= 256 ? 4 : 2); }
+template <int D> constexpr int fwd_waves() { return D >= 256 ? 8 : 2; }
 // column parts of the backward kernels (folded into the 1-D grid as virtual heads, see
 // item_head): dK / dV and dQ accumulators per part
 template <int D> constexpr int kv_parts() { return D >= 256 && D < 512 ? 2 : 1; }
@@ -111,8 +111,8 @@ template <int D> constexpr int kv_parts() { return D >= 256 && D < 512 ? 2 : 1; 
 //   dK / dV: fa512_bwd_dkdv_kernel below (S-wave / dP-wave roles).
 // (The round-4 design recomputed S over the full D in every column part — forward 2×, dQ 2×,
 // dK / dV 4× — and still spilled 350-560 B per lane: 106 / 64 TF fwd / bwd, slower than SDPA.)
-template <int D> constexpr int fwd_dsplit() { return D >= 512 ? 4 : 1; }
-template <int D> constexpr int dq_dsplit() { return D >= 512 ? 4 : 1; }
+template <int D> constexpr int fwd_dsplit() { return D >= 512 ? 4 : (D >= 256 ? 2 : 1); }
+template <int D> constexpr int dq_dsplit() { return D >= 512 ? 4 : (D >= 256 ? 2 : 1); }
 
 // ---- work lists (causal balance) ---------------------------------------------------------
 // A causal query block's cost grows with its index, so a grid that fits in ONE round of
@@ -175,7 +175,7 @@ __global__ void __launch_bounds__(64 * fwd_waves<D>(), (D >= 256 ? 1 : 2))
   // workgroup's query rows sit in LDS instead (read as B-operand row fragments per tile).
   // D = 512: the K / V double buffer alone is 128 KB; a wave keeps its quarter of Q (32 VGPRs) in
   // registers and accumulates its quarter of Oᵀ (fwd_dsplit)
-  constexpr bool QLDS = D == 256;
+  constexpr bool QLDS = D == 256 && ZS == 1;
   constexpr int NDO = ND / ZS, NSH = NS / ZS;
   constexpr int QTILE = QLDS ? BM * 128 * NP : (ZS > 1 ? 0 : 16);
   constexpr int XB = ZS > 1 ? NW * 16 * 64 * 4 : 16;  // partial-S exchange: [wave][4][64 lanes] float4
@@ -817,7 +817,7 @@ __global__ void __launch_bounds__(256) fa_gen_combine(const float* __restrict__ 
 template <int D> constexpr int dq_waves() { return 2 * dq_dsplit<D>(); }
 
 template <int D, bool DROPOUT>
-__global__ void __launch_bounds__(64 * dq_waves<D>(), (D >= 256 ? 1 : 2))
+__global__ void __launch_bounds__(64 * dq_waves<D>(), (D >= 512 ? 1 : 2))
     fa_gen_bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
                          const float* __restrict__ delta, bf16* __restrict__ dqkv, int T, int H, int Hkv, float scale,
                          float p_drop, uint64_t seed, const WorkList wl, float* __restrict__ ws) {
