@@ -1,4 +1,4 @@
-// Causal flash attention for head_dim 128 and 256 (Gemma-family training / prefill; the tuned
+// Causal flash attention for head_dim 128, 256 and 512 (Gemma-family training / prefill; the tuned
 // head_dim-64 kernels live in flash_attn.hip). bf16 in/out, fp32 accumulate, GQA by index math.
 //
 // Same algebra and operand maps as the head_dim-64 kernels (v_mfma_f32_32x32x16_bf16 with the
@@ -10,21 +10,19 @@
 // swizzle applied on the per-lane SOURCE address, the LDS image stays lane-linear), double
 // buffered: tile j+1 is in flight while tile j computes.
 //
-//   forward   — workgroup = 2 (D = 128) or 4 (D = 256) waves × 32 query rows; 32-key tiles; Sᵀ = K·Qᵀ (Q in D/16
-//               registers), online softmax per lane (one query row per lane), Oᵀ += Vᵀ·Pᵀ
-//               with Oᵀ in D/32 accumulators; heaviest query blocks first; writes O head-merged
-//               and the row log-sum-exp (natural log), like the head_dim-64 kernel.
-//   backward  — δ = rowsum(dO·O); dK/dV kernel: a wave keeps 32 keys' K, V fragments and
-//               dKᵀ, dVᵀ accumulators in registers while sweeping 32-row query slices of every
-//               query head of its KV group (no cross-workgroup sum, deterministic); dQ kernel:
-//               forward-shaped, a wave keeps 32 query rows' Q, dO and dQᵀ in registers.
-// At D = 256 the register-resident operands exceed 256 VGPRs: those kernels run one wave per
-// SIMD with the accumulators in the AGPR half of the unified 512-entry register file.
-// D = 512 (Gemma-4 full-attention layers, global_head_dim): the head dimension is split across the
-// waves of one workgroup, never recomputed — forward and dQ: a wave pair shares 32 query rows,
-// each wave computes the partial S (dP) over its half of D and owns half of the Oᵀ (dQᵀ) columns,
-// the partials meet in LDS; dK / dV (fa512_bwd_dkdv_kernel): an S-wave (K, dVᵀ) and a dP-wave
-// (V, dKᵀ) per 32 keys, P handed over through LDS.
+//   forward   — 32-key tiles; Sᵀ = K·Qᵀ (Q in registers), online softmax per lane (one query row
+//               per lane), Oᵀ += Vᵀ·Pᵀ; heaviest query blocks first; writes O head-merged and the
+//               row log-sum-exp (natural log), like the head_dim-64 kernel. D = 128: 2 waves ×
+//               32 rows. D = 256 / 512: 8 waves, the head dimension split over 2 / 4 waves that
+//               share 32 query rows — each holds its part of Q, computes the partial S over it and
+//               owns that part of the Oᵀ columns; the partials are summed through LDS in part order
+//               (bitwise the same S in every wave of the group), ≤ 256 registers: 2 waves / SIMD.
+//   backward  — δ = rowsum(dO·O); dK/dV kernel (fa_roles_bwd_dkdv_kernel): per 32 keys an S-wave
+//               (cK in registers, dVᵀ accumulators) and a dP-wave (V, dKᵀ) sweep the 32-row query
+//               slices of every query head of the KV group, P handed over through LDS (no
+//               cross-workgroup sum, deterministic); dQ kernel: forward-shaped, Q, dO and dQᵀ in
+//               registers (D = 256 / 512: split over 2 / 4 waves, partial S and dP exchanged).
+// D = 512 (Gemma-4 full-attention layers, global_head_dim) splits dVᵀ / dKᵀ over two workgroups.
 #include "attn_common.h"
 #include <algorithm>
 #include <cstdlib>
@@ -100,7 +98,6 @@ __device__ __forceinline__ void dsplit_sum(f32x16& v, float4_t* x4, int w, int r
 template <int D> constexpr int fwd_waves() { return D >= 256 ? 8 : 2; }
 // column parts of the backward kernels (folded into the 1-D grid as virtual heads, see
 // item_head): dK / dV and dQ accumulators per part
-template <int D> constexpr int kv_parts() { return D >= 256 && D < 512 ? 2 : 1; }
 // D = 512 splits the head dimension across the waves of ONE workgroup instead (no recomputation):
 //   forward: 8 waves, a group of four shares 32 query rows; each wave holds a quarter of Q in
 //   registers, computes the partial S over its quarter of D and owns a quarter of the Oᵀ columns;
@@ -108,7 +105,7 @@ template <int D> constexpr int kv_parts() { return D >= 256 && D < 512 ? 2 : 1; 
 //   in all four waves). ≤ 256 registers per wave: two waves per SIMD, no spills (the 4-wave halves
 //   version spilled ~90 B per lane and ran fwd at 195 TF);
 //   dQ: the same (8 waves, quarters of Q, dO; partial S, then partial dP exchanged);
-//   dK / dV: fa512_bwd_dkdv_kernel below (S-wave / dP-wave roles).
+//   dK / dV: fa_roles_bwd_dkdv_kernel below (S-wave / dP-wave roles, every D).
 // (The round-4 design recomputed S over the full D in every column part — forward 2×, dQ 2×,
 // dK / dV 4× — and still spilled 350-560 B per lane: 106 / 64 TF fwd / bwd, slower than SDPA.)
 template <int D> constexpr int fwd_dsplit() { return D >= 512 ? 4 : (D >= 256 ? 2 : 1); }
@@ -371,228 +368,36 @@ __global__ void __launch_bounds__(256) fa_gen_bwd_pre_kernel(const bf16* __restr
 }
 
 // ------------------------------------------------------------------------------------------
-// dK / dV: grid (ceil(T/64) key blocks, B*Hkv); wave w owns keys kb*64 + 32w + (lane&31) and
-// sweeps 32-row query slices (every query head of its KV group) staged in LDS: Q | dO | LSE | δ.
-// Query-head split (part != nullptr, grid y = B*Hkv*G): each workgroup sweeps ONE query head of
-// its group and writes fp32 partial dK / dV ([G][B·T][K | V][Hkv·D]) that fa_gen_kv_reduce sums —
-// at Gemma-3 1B shapes (Hkv = 1, G = 4, B = 8) the unsplit grid is 128 workgroups of 2 waves for
-// 256 CUs.
-template <int D, bool DROPOUT>
-__global__ void __launch_bounds__(128, 1)
-    fa_gen_bwd_dkdv_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
-                           const float* __restrict__ delta, bf16* __restrict__ dqkv, float* __restrict__ part, int T,
-                           int H, int Hkv, float scale, float p_drop, uint64_t seed) {
-  constexpr int NP = D / 64, NS = D / 16, ND = D / 32;
-  constexpr int BK = 64, QS = 32;
-  constexpr int TILE = QS * 128 * NP;          // one 32-row slice of Q (or dO)
-  constexpr int STAGE = 2 * TILE + 2 * 256;    // Q | dO | LSE[64] | δ[64] (64-lane DMA pieces)
-  // D = 256: the K / V fragments (128 registers) and the full dKᵀ / dVᵀ accumulators (256) do
-  // not fit one wave's register file together. Each workgroup accumulates dK / dV for HALF of D
-  // (grid z = the half) — S and dP, which need all of D, are computed by both halves — so K / V
-  // stay in registers: no per-slice K / V LDS reads, and 65 KB of LDS per workgroup lets two
-  // workgroups (all four SIMDs) share a CU. (Keeping K / V in LDS for one workgroup per CU left
-  // two SIMDs idle, spilled 72 registers and was LDS-bandwidth-bound at 87 TF.)
-  constexpr int NDH = ND / kv_parts<D>();  // dKᵀ / dVᵀ column blocks of 32 owned here (D = 256: a half)
-  constexpr bool KVLDS = false;
-  constexpr int KVT = BK * 128 * NP;           // 64 key rows
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + (KVLDS ? 2 * KVT : 16)];
-  // 1-D grid: key block kb ascending = heaviest first (causal) across every (column part, head)
-  int kb, vh;
-  item_head((T + BK - 1) / BK, kb, vh);
-  const int nbhx = gridDim.x / (((T + BK - 1) / BK) * kv_parts<D>());
-  const int zc = vh / nbhx, bhx = vh - zc * nbhx;
-  const int dh0 = zc * NDH;
-  const int G = H / Hkv;
-  const int GS = part != nullptr ? G : 1;  // workgroups per KV group (query-head split)
-  const int gi = bhx % GS, bh = bhx / GS;
-  const int b = bh / Hkv, hk = bh % Hkv;
-  const int lane = threadIdx.x & 63, w = wave_id(), hh = lane >> 5;
-  const size_t RS = (size_t)(H + 2 * Hkv) * D;
-  const size_t ORS = (size_t)H * D;
-  const int kw0 = kb * BK + 32 * w;
-  const int key = kw0 + (lane & 31);
-  const float c = scale * kLog2e;
-  const float inv_keep = DROPOUT ? 1.f / (1.f - p_drop) : 1.f;
-
-  const bf16* kbase = qkv + (size_t)b * T * RS + (size_t)(H + hk) * D;
-  const bf16* vbase = qkv + (size_t)b * T * RS + (size_t)(H + Hkv + hk) * D;
-  const char* KVs = smem + 2 * STAGE;  // [K 64 rows | V 64 rows] paneled images (KVLDS)
-  uint4 kf[KVLDS ? 1 : NS], vf[KVLDS ? 1 : NS];
-  if constexpr (KVLDS) {
-    dma_rows<NP, BK>(w == 0 ? kbase : vbase, RS, kb * BK, T,
-                     __builtin_amdgcn_readfirstlane(lds_addr_of(smem + 2 * STAGE)) + w * KVT, lane);
-  } else {
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      kf[s] = key < T ? *reinterpret_cast<const uint4*>(kbase + (size_t)key * RS + 16 * s + 8 * hh) : zero4();
-      vf[s] = key < T ? *reinterpret_cast<const uint4*>(vbase + (size_t)key * RS + 16 * s + 8 * hh) : zero4();
-    }
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      kf[s] = scale_bf16x8(kf[s], c);  // S = Q·(cK)ᵀ (attn_common.h); dK uses Q, not K
-      launder(kf[s]);
-      launder(vf[s]);
-    }
-  }
-  static_assert(!KVLDS, "the prescaled-K form keeps K in registers");
-  // B fragment s of Kᵀ (Vᵀ): element j = K[key][16s + 8hh + j]
-  auto kfrag = [&](int s) -> uint4 {
-    if constexpr (KVLDS) return row_frag(panel(KVs, BK, s >> 2), 32 * w, s & 3, lane);
-    else return kf[s];
-  };
-  auto vfrag = [&](int s) -> uint4 {
-    if constexpr (KVLDS) return row_frag(panel(KVs + KVT, BK, s >> 2), 32 * w, s & 3, lane);
-    else return vf[s];
-  };
-  f32x16 dk[NDH], dv[NDH];
-#pragma unroll
-  for (int dh = 0; dh < NDH; ++dh)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) dk[dh][i] = dv[dh][i] = 0.f;
-
-  const int s_first = (kb * BK) / QS;
-  const int nslices = (T + QS - 1) / QS;
-  const int per_head = nslices - s_first;
-  const int total = (GS == 1 ? G : 1) * per_head;
-  auto head_of = [&](int it) { return hk * G + (GS == 1 ? it / per_head : gi); };
-
-  auto dma = [&](int it) {  // wave 0: Q slice + LSE rows, wave 1: dO slice + δ rows
-    const int hq = head_of(it);
-    const int qs0 = (s_first + it % per_head) * QS;
-    const unsigned st = __builtin_amdgcn_readfirstlane(lds_addr_of(smem + (it & 1) * STAGE));
-    if (w == 0)
-      dma_rows<NP>(qkv + (size_t)b * T * RS + (size_t)hq * D, RS, qs0, T, st, lane);
-    else
-      dma_rows<NP>(dout + (size_t)b * T * ORS + (size_t)hq * D, ORS, qs0, T, st + TILE, lane);
-    const float* sp = (w == 0 ? lse : delta) + ((size_t)b * H + hq) * T + min(qs0 + lane, T - 1);
-    glds4(sp, st + 2 * TILE + 256 * w);
-  };
-
-  if (total > 0) dma(0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int it = 0; it < total; ++it) {
-    if (it + 1 < total) dma(it + 1);  // the other stage, released by the previous barrier
-    const char* stg = smem + (it & 1) * STAGE;
-    const char* Qt = stg;
-    const char* Dt = stg + TILE;
-    const float* lse_s = reinterpret_cast<const float*>(stg + 2 * TILE);
-    const float* del_s = lse_s + 64;
-    const int hq = head_of(it);
-    const int qs0 = (s_first + it % per_head) * QS;
-    if (qs0 + QS - 1 >= kw0 && kw0 < T && qs0 < T) {
-      f32x16 sp, dp;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4_t dl = *reinterpret_cast<const float4_t*>(&del_s[8 * g + 4 * hh]);
-        const float4_t l2 = *reinterpret_cast<const float4_t*>(&lse_s[8 * g + 4 * hh]) * kLog2e;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          sp[4 * g + k] = -l2[k];  // S accumulates onto −LSE·log2(e): P = exp2(S)
-          dp[4 * g + k] = DROPOUT ? 0.f : -dl[k];
-        }
-      }
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        sp = mfma32(row_frag(panel(Qt, QS, s >> 2), 0, s & 3, lane), kfrag(s), sp);
-        dp = mfma32(row_frag(panel(Dt, QS, s >> 2), 0, s & 3, lane), vfrag(s), dp);
-        if (s & 1) d_fence<D>();
-      }
-      auto grads = [&](auto mask_tag) {
-        constexpr bool MASK = decltype(mask_tag)::value;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int r0 = 8 * g + 4 * hh;
-          float4_t dl = {0.f, 0.f, 0.f, 0.f};
-          if constexpr (DROPOUT) dl = *reinterpret_cast<const float4_t*>(&del_s[r0]);
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int i = 4 * g + k;
-            const int q = qs0 + r0 + k;
-            float p = fexp2(sp[i]);
-            if constexpr (MASK) p = (key > q || q >= T || key >= T) ? 0.f : p;
-            if constexpr (DROPOUT) {
-              const bool keep = dropout_keep(seed, b, hq, H, T, q, key, p_drop);
-              sp[i] = keep ? p * inv_keep : 0.f;
-              dp[i] = p * ((keep ? dp[i] * inv_keep : 0.f) - dl[k]);
-            } else {
-              sp[i] = p;
-              dp[i] = p * dp[i];
-            }
-          }
-        }
-      };
-      if (kw0 + 31 > qs0 || qs0 + QS > T || kw0 + 32 > T)
-        grads(std::true_type{});
-      else
-        grads(std::false_type{});
-#pragma unroll
-      for (int ss = 0; ss < 2; ++ss) {
-        const uint4 pf = acc_frag(sp, ss), sf = acc_frag(dp, ss);
-#pragma unroll
-        for (int j = 0; j < NDH; ++j) {
-          const int dh = dh0 + j;
-          dv[j] = mfma32(tr_frag(panel(Dt, QS, dh >> 1), 16 * ss, 32 * (dh & 1), lane), pf, dv[j]);
-          dk[j] = mfma32(tr_frag(panel(Qt, QS, dh >> 1), 16 * ss, 32 * (dh & 1), lane), sf, dk[j]);
-          if (j & 1) d_fence<D>();
-        }
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-  if (key < T && part != nullptr) {  // fp32 partials of this query head: [gi][b·T + key][K | V][hk·D + d]
-    const int Bn = nbhx / (Hkv * GS);
-    float* prow = part + ((size_t)gi * Bn * T + (size_t)b * T + key) * (2 * Hkv * D) + (size_t)hk * D;
-#pragma unroll
-    for (int j = 0; j < NDH; ++j)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d = 32 * (dh0 + j) + 8 * g + 4 * hh;
-        *reinterpret_cast<float4*>(prow + d) = float4{dk[j][4 * g] * scale, dk[j][4 * g + 1] * scale,
-                                                      dk[j][4 * g + 2] * scale, dk[j][4 * g + 3] * scale};
-        *reinterpret_cast<float4*>(prow + (size_t)Hkv * D + d) =
-            float4{dv[j][4 * g], dv[j][4 * g + 1], dv[j][4 * g + 2], dv[j][4 * g + 3]};
-      }
-  } else if (key < T) {
-    bf16* dkrow = dqkv + ((size_t)b * T + key) * RS + (size_t)(H + hk) * D;
-    bf16* dvrow = dqkv + ((size_t)b * T + key) * RS + (size_t)(H + Hkv + hk) * D;
-#pragma unroll
-    for (int j = 0; j < NDH; ++j)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d = 32 * (dh0 + j) + 8 * g + 4 * hh;
-        store4(dkrow + d, dk[j][4 * g] * scale, dk[j][4 * g + 1] * scale, dk[j][4 * g + 2] * scale,
-               dk[j][4 * g + 3] * scale);
-        store4(dvrow + d, dv[j][4 * g], dv[j][4 * g + 1], dv[j][4 * g + 2], dv[j][4 * g + 3]);
-      }
-  }
-}
-
-// dK / dV at D = 512: 4 waves = 2 key groups (32 keys each, BK = 64) × 2 roles. The S-wave holds
+// dK / dV: 1-D grid over (key block of 64, KV head [, query head: split], column part); heaviest
+// key block first. 4 waves = 2 key groups (32 keys each) × 2 roles, sweeping the 32-row query
+// slices (Q | dO | LSE | δ, double-buffered by LDS-DMA) of every query head of the KV group. The S-wave holds
 // cK (32 fragments, full D) and accumulates dVᵀ over all of D; the dP-wave holds V and accumulates
 // dKᵀ. Per 32-row query slice the S-wave computes S and P and hands P (fp32) to its dP-wave through
 // LDS; the dP-wave forms dS = P ⊙ (dP − δ). Each wave then runs 32 MFMAs of S or dP and 32 of dV or
-// dK. The dVᵀ / dKᵀ columns are split over kParts512 workgroups (virtual heads): a wave's 256
-// accumulators for all of D beside its 128 operand registers spilled ~800 B, so S and dP are
-// computed twice instead of four times (the round-4 kernel: column quarters, each wave computing
-// both S and dP). Same work order, query-head split and outputs as fa_gen_bwd_dkdv_kernel.
-constexpr int kParts512 = 2;
+// dK. D = 128 / 256: 32 / 64 operand + 64 / 128 accumulator registers, 3 / 2 waves per SIMD, no
+// recomputation (the round-4 kernel held K and V in every wave and computed both S and dP —
+// at D = 256 in both column halves of two workgroups: D = 128 bwd 1855 -> 1502 µs, D = 256
+// 227 -> 177 µs). D = 512: the dVᵀ / dKᵀ columns are split over kv_role_parts = 2 workgroups
+// (virtual heads) — a wave's 256 accumulators for all of D beside its 128 operand registers
+// spilled ~800 B — so S and dP are computed twice (the round-4 kernel: four times).
+// Query-head split (part != nullptr): each workgroup sweeps ONE query head of its group and writes
+// fp32 partial dK / dV ([G][B·T][K | V][Hkv·D]) that fa_gen_kv_reduce sums (Gemma-3 1B: Hkv = 1).
+template <int D> constexpr int kv_role_parts() { return D >= 512 ? 2 : 1; }
 
-template <bool DROPOUT>
-__global__ void __launch_bounds__(256, 1)
-    fa512_bwd_dkdv_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
+template <int D, bool DROPOUT>
+__global__ void __launch_bounds__(256, (D >= 512 ? 1 : 2))
+    fa_roles_bwd_dkdv_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
                           const float* __restrict__ delta, bf16* __restrict__ dqkv, float* __restrict__ part, int T,
                           int H, int Hkv, float scale, float p_drop, uint64_t seed) {
-  constexpr int D = 512, NP = D / 64, NS = D / 16, ND = D / 32, NDW = ND / kParts512;
+  constexpr int NP = D / 64, NS = D / 16, ND = D / 32, NDW = ND / kv_role_parts<D>();
   constexpr int BK = 64, QS = 32;
-  constexpr int TILE = QS * 128 * NP;          // one 32-row slice of Q (or dO): 32 KB
+  constexpr int TILE = QS * 128 * NP;          // one 32-row slice of Q (or dO)
   constexpr int STAGE = 2 * TILE + 2 * 256;    // Q | dO | LSE[64] | δ[64]
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 2 * 16 * 64 * 4];
   float* xp = reinterpret_cast<float*>(smem + 2 * STAGE);  // P hand-over: [key group][16][64]
   int kb, vh;
   item_head((T + BK - 1) / BK, kb, vh);
-  const int nbhx = gridDim.x / (((T + BK - 1) / BK) * kParts512);
+  const int nbhx = gridDim.x / (((T + BK - 1) / BK) * kv_role_parts<D>());
   const int zc = vh / nbhx, bhx = vh - zc * nbhx;
   const int dh0 = zc * NDW;  // this workgroup's dVᵀ / dKᵀ column blocks
   const int G = H / Hkv;
@@ -1156,19 +961,15 @@ void flash_attn_gen_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out
   if (split) part = torch::empty({(int64_t)G * B * T, 2 * Hkv * D}, qkv.options().dtype(torch::kFloat32));
   // 1-D grids: items (key / query blocks) × the column parts of D (dK / dV: 2 at D = 256, 4 at
   // 512; dQ: 2 at 512) × heads
-  const int64_t nkv = (int64_t)nkb * B * Hkv * (split ? G : 1) * (D == 256 ? 2 : (D == 512 ? kParts512 : 1));
+  const int64_t nkv = (int64_t)nkb * B * Hkv * (split ? G : 1) * (D == 512 ? 2 : 1);  // kv_role_parts
+
   FA_GEN_DISPATCH(D, p_drop > 0.0, {
     hipLaunchKernelGGL((fa_gen_bwd_pre_kernel<DD>), dim3(((int64_t)rows * (DD / 8) + 255) / 256), dim3(256), 0,
                        stream, d, reinterpret_cast<const bf16*>(out.data_ptr()), delta.data_ptr<float>(), B, T,
                        (int)H);
-    if constexpr (DD == 512)
-      hipLaunchKernelGGL((fa512_bwd_dkdv_kernel<DR>), dim3((unsigned)nkv), dim3(256), 0, stream, q, d,
-                         lse.data_ptr<float>(), delta.data_ptr<float>(), g, split ? part.data_ptr<float>() : nullptr,
-                         T, (int)H, (int)Hkv, (float)scale, (float)p_drop, (uint64_t)seed);
-    else
-      hipLaunchKernelGGL((fa_gen_bwd_dkdv_kernel<DD, DR>), dim3((unsigned)nkv), dim3(128), 0, stream, q, d,
-                         lse.data_ptr<float>(), delta.data_ptr<float>(), g, split ? part.data_ptr<float>() : nullptr,
-                         T, (int)H, (int)Hkv, (float)scale, (float)p_drop, (uint64_t)seed);
+    hipLaunchKernelGGL((fa_roles_bwd_dkdv_kernel<DD, DR>), dim3((unsigned)nkv), dim3(256), 0, stream, q, d,
+                       lse.data_ptr<float>(), delta.data_ptr<float>(), g, split ? part.data_ptr<float>() : nullptr, T,
+                       (int)H, (int)Hkv, (float)scale, (float)p_drop, (uint64_t)seed);
     if (split) {
       const int64_t n8 = (int64_t)B * T * (2 * Hkv * DD / 8);
       hipLaunchKernelGGL(fa_gen_kv_reduce, dim3((unsigned)std::min<int64_t>((n8 + 255) / 256, 4096)), dim3(256), 0,
