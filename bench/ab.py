@@ -6,7 +6,8 @@
 
 An arm is ``name:ENV=VAL ENV2=VAL2`` (empty env = the working tree as is). A baseline build is an
 arm whose env sets ``PENROZ_EXT_DIR`` to a second in-tree build directory; a GEMM-table variant sets
-``PENROZ_TUNED_GEMM_FILE``. Workloads:
+``PENROZ_TUNED_GEMM_FILE``; ``AB_CWD=dir`` runs the arm from another in-tree checkout (e.g. the
+previous commit's Python, ``git archive HEAD | tar -x -C ab_head`` with ``build_ext`` linked in). Workloads:
 
 * ``headline`` — ``bench.py`` (GPT-2 124M, B = 64, T = 1024), 20 timed / 5 warmup steps;
 * ``bench:<model>[:<batch>]`` / ``gemma3-1b[:<batch>]`` — ``bench.py --model …``;
@@ -89,9 +90,11 @@ def main(argv=None) -> int:
             for work in works:
                 cmd, limit = work_cmd(work, args.steps, args.warmup)
                 for name, env in arms:
+                    env = dict(env)
+                    cwd = os.path.join(ROOT, env.pop("AB_CWD")) if "AB_CWD" in env else ROOT
                     full = dict(os.environ, **env)
                     t0 = time.time()
-                    r = subprocess.run(["timeout", "-k", "10", str(limit)] + cmd, cwd=ROOT, env=full,
+                    r = subprocess.run(["timeout", "-k", "10", str(limit)] + cmd, cwd=cwd, env=full,
                                        capture_output=True, text=True)
                     rec = {"pass": p, "work": work, "arm": name, "env": env, "rc": r.returncode,
                            "wall_s": round(time.time() - t0, 1), **headline_number(r.stdout)}

@@ -299,12 +299,15 @@ class GPTExecutor:
     # ---- transposed bf16 weight copies for the data-gradient GEMMs ----------------------------
     # dx = dy·W with W [out, in] as stored reaches 0.94-1.32 PF on hipBLASLt at GPT-2 shapes; with
     # W transposed ([in, out], so both operands are reduction-contiguous as in the forward) it
-    # reaches 1.11-1.53 PF (profiles/dgrad_layout_r1.log). The copies are rebuilt from the bf16
-    # shadow at the start of every micro-step on the side stream (overlapping the forward; ~0.2
-    # ms of memory traffic) and the backward's first dgrad waits for them. PENROZ_DGRAD_T=0: off.
+    # reaches 1.11-1.53 PF (profiles/dgrad_layout_r1.log). With the optimizer fused into the
+    # backward, a segment's copies are rebuilt right after its optimizer pass on the side stream
+    # (overlapping the rest of the backward; _t_fresh); otherwise — and for anything not yet
+    # rebuilt — at the start of the micro-step on the side stream, and the backward's first dgrad
+    # waits for them (Gemma-3 1B: the 1.1 ms of transposes sat between the step's last AdamW pass
+    # and the next forward, profiles/notes_r5.md). PENROZ_DGRAD_T=0: off.
     def _init_transposed(self):
         import os
-        self._tw, self._t_ready = {}, None
+        self._tw, self._t_ready, self._t_fresh = {}, None, set()
         if self.device.type != "cuda" or os.environ.get("PENROZ_DGRAD_T", "1") == "0" or not _ext.available():
             return
         s = self.spec
@@ -322,9 +325,13 @@ class GPTExecutor:
             return
         k = _ext.kernels()
         side = getattr(self, "_side", None)
+        todo = [(key, e) for key, e in self._tw.items() if key not in self._t_fresh]
+        self._t_fresh.clear()
         if side is None:
-            for w, t in self._tw.values():
-                k.transpose_bf16(self.bf16(w), t)
+            for _, e in todo:
+                k.transpose_bf16(self._tw_source(e), e[1])
+            return
+        if not todo:  # all rebuilt after their segments' optimizer passes (the main stream joined)
             return
         # the copies must see this step's weights: the side stream waits for everything the main
         # stream has queued (the optimizer's shadow refresh). The main stream is captured BEFORE
@@ -333,10 +340,30 @@ class GPTExecutor:
         main = torch.cuda.current_stream(self.device)
         with torch.cuda.stream(side):
             side.wait_stream(main)
-            for w, t in self._tw.values():
-                k.transpose_bf16(self.bf16(w), t)
+            for _, e in todo:
+                k.transpose_bf16(self._tw_source(e), e[1])
             self._t_ready = torch.cuda.Event()
             self._t_ready.record(side)
+
+    def _tw_source(self, entry) -> Tensor:
+        return self.bf16(entry[0])
+
+    # rebuild a segment's transposed copies right after its optimizer pass: Gemma-3 1B B=8 −0.2 to
+    # −0.3 ms, Gemma-4 e2b −0.4 ms; GPT-2 +0.16 / +0.19 ms (its start-of-step transposes already
+    # overlap the forward), so the GPT executor keeps them at the step start
+    SEGMENT_TRANSPOSE = False
+
+    def _transpose_segment(self, s: int, e: int):
+        """Rebuild the transposed dgrad copies of the parameters in flat range [s, e) on the current
+        stream, right after that range's optimizer pass (their shadow is final for the next step)."""
+        if not getattr(self, "_tw", None) or not self.SEGMENT_TRANSPOSE:
+            return
+        k = _ext.kernels()
+        for key, ent in self._tw.items():
+            off = self.offsets.get(key)
+            if off is not None and s <= off < e:
+                k.transpose_bf16(self._tw_source(ent), ent[1])
+                self._t_fresh.add(key)
 
     def _dgrad_w(self, w: Tensor) -> Tensor:
         """The weight operand of dx = dy·W: the transposed copy (viewed back as [out, in]) or the shadow."""
@@ -554,11 +581,13 @@ class GPTExecutor:
             s, e = self.segments[seg_index]
             if getattr(self, "_side", None) is None:
                 self._opt_apply(s, e)
+                self._transpose_segment(s, e)
                 return
             main = torch.cuda.current_stream(self.device)
             with torch.cuda.stream(self._side):
                 self._side.wait_stream(main)
                 self._opt_apply(s, e)
+                self._transpose_segment(s, e)
             return
         if self.reducer is None or not sync:
             return

@@ -97,6 +97,7 @@ class GemmaSpec:
 
 class GemmaExecutor(GPTExecutor):
     MAIN_PRIORITY_DEFAULT = False  # measured slightly slower at B = 8 (GPTExecutor._main_stream)
+    SEGMENT_TRANSPOSE = True  # see GPTExecutor._transpose_segment
 
     # ------------------------------------------------------------------ pattern match
     @staticmethod
@@ -215,7 +216,7 @@ class GemmaExecutor(GPTExecutor):
     # ---- transposed bf16 weight copies for the data-gradient GEMMs (see GPTExecutor) ---------
     def _init_transposed(self):
         import os
-        self._tw, self._t_ready = {}, None
+        self._tw, self._t_ready, self._t_fresh = {}, None, set()
         if self.device.type != "cuda" or os.environ.get("PENROZ_DGRAD_T", "1") == "0" or not _ext.available():
             return
         s = self.spec
@@ -240,16 +241,25 @@ class GemmaExecutor(GPTExecutor):
         k = _ext.kernels()
         side = getattr(self, "_side", None)
         if side is None:
-            for f, t in self._tw.values():
-                k.transpose_bf16(f(), t)
+            for key, (f, t) in self._tw.items():
+                if key not in self._t_fresh:
+                    k.transpose_bf16(f(), t)
+            self._t_fresh.clear()
+            return
+        todo = [(f, t) for key, (f, t) in self._tw.items() if key not in self._t_fresh]
+        self._t_fresh.clear()
+        if not todo:  # all rebuilt after their segments' optimizer passes (the main stream joined)
             return
         main = torch.cuda.current_stream(self.device)
         with torch.cuda.stream(side):
             side.wait_stream(main)
-            for f, t in self._tw.values():
+            for f, t in todo:
                 k.transpose_bf16(f(), t)
             self._t_ready = torch.cuda.Event()
             self._t_ready.record(side)
+
+    def _tw_source(self, entry) -> Tensor:
+        return entry[0]()
 
     def _dgrad(self, key_param: Tensor, src: Tensor) -> Tensor:
         """The weight operand of dx = dy·W: the transposed copy (viewed back as [out, in]) or ``src``."""
@@ -308,7 +318,10 @@ class GemmaExecutor(GPTExecutor):
         QKV, A, F = max(qkv_w(b) for b in bs), max(b.H * b.D for b in bs), max(b.F for b in bs)
         self.qkv_raw = e(N * QKV)                          # QKV GEMM output before RoPE
         self.dresid = e(N, C, dt=f32)
-        self.d_branch2 = [e(N, C) for _ in range(2)]       # rotating: read by side-stream wgrads
+        # rotating, read by side-stream wgrads: 4 deep — the side stream starts the backward ~7 ms
+        # behind (lm_head wgrad, head-segment AdamW), and with 2 buffers the main stream stalled
+        # 2.9 ms at block L-1 for the reader of its reuse (profiles/notes_r5.md, timeline gaps)
+        self.d_branch2 = [e(N, C) for _ in range(4)]
         self.d_g = e(N * F)
         self.d_gu2 = [e(N * 2 * F) for _ in range(2)]
         self.d_att2 = [e(N * A) for _ in range(2)]
@@ -459,7 +472,7 @@ class GemmaExecutor(GPTExecutor):
             self._wgrad_into(id(b.mlp.gate_proj.weight), dgu, self.y_mlp[l], self.gu_grad(b))
             # ---- attention combine: dy = d(pre-MLP norm output), dh_in = dresid (grad of mid[l])
             pa = b.post_attn
-            rb ^= 1
+            rb = (rb + 1) % len(self.d_branch2)
             db = self._reuse(self.d_branch2[rb])
             self._combine_bwd(mode, self.d_c, self.dresid, self.mid[l], self.s_attn[l] if self.s_attn else None,
                               self.r_pa[l] if self.r_pa else None, self.r_pre[l],
@@ -481,7 +494,7 @@ class GemmaExecutor(GPTExecutor):
             if l > 0:
                 pb = s.blocks[l - 1]
                 pm = pb.post_mlp
-                rb ^= 1
+                rb = (rb + 1) % len(self.d_branch2)
                 db = self._reuse(self.d_branch2[rb])
                 self._combine_bwd(mode, self.d_c, self.dresid, self.resid[l],
                                   self.s_mlp[l - 1] if self.s_mlp else None, self.r_pm[l - 1] if self.r_pm else None,
