@@ -54,6 +54,9 @@ void adam_step(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor 
 void multi_tensor_adam(std::vector<torch::Tensor> ps, std::vector<torch::Tensor> gs, std::vector<torch::Tensor> ms,
                        std::vector<torch::Tensor> vs, double lr, double b1, double b2, double eps, double wd,
                        int64_t step, double grad_scale, bool maximize, bool decoupled);
+void adam_rows_step(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, c10::optional<torch::Tensor> shadow,
+                    int64_t C, torch::Tensor mask, c10::optional<torch::Tensor> rows, int64_t mode, double lr, double b1,
+                    double b2, double eps, double wd, int64_t step, double grad_scale, bool maximize, bool decoupled);
 // sampling.hip
 torch::Tensor sample_tokens(torch::Tensor logits, c10::optional<torch::Tensor> uniform, double temperature,
                             int64_t top_k);
@@ -180,6 +183,7 @@ PYBIND11_MODULE(penroz_kernels, m) {
         pybind11::arg("scale"), pybind11::arg("ignore_index"), pybind11::arg("grad_out") = pybind11::none());
   m.def("adamw_step", &adamw_step);
   m.def("adam_step", &adam_step);
+  m.def("adam_rows_step", &adam_rows_step, "row-split Adam/AdamW step of an embedding table (mode 0: untouched rows, 1: touched rows)");
   m.def("multi_tensor_adam", &multi_tensor_adam);
   m.def("sample_tokens", &sample_tokens);
   m.def("sample_step", &sample_step, "decode-step sampler: device-hashed uniforms, writes idx_out and out_buf[:, *step]");

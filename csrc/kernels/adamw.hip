@@ -80,6 +80,63 @@ __global__ void __launch_bounds__(256) adam_flat_kernel(float* __restrict__ p, c
   }
 }
 
+// Row-split step of an embedding table [R, C] inside the flat buffers (C % 4 == 0). A step's
+// gradient is zero on every row its tokens did not touch, and those rows' update (moment decay,
+// weight decay) does not depend on the backward: MODE 0 updates the rows with mask[row] == 0 as
+// for g = 0 (no gradient read), any time during the step; MODE 1 then updates the touched rows —
+// one workgroup per token, the first of a row's tokens claims it (mask 1 -> 2, vector
+// compare-and-swap) — and clears their gradient, so the table's gradient is all zero again and
+// zero_grad can skip it. Bitwise the same result as the dense step (adam_elem with g = 0.0f).
+template <int MODE>
+__global__ void __launch_bounds__(256) adam_rows_kernel(float* __restrict__ p, float* __restrict__ g,
+                                                        float* __restrict__ m, float* __restrict__ v,
+                                                        bf16* __restrict__ shadow, int64_t R, int C,
+                                                        int* __restrict__ mask, const int64_t* __restrict__ rows,
+                                                        int64_t nrows, AdamHyper h) {
+  const int c4 = C / 4;
+  auto row_update = [&](int64_t row, int64_t j) {  // float4 j of row
+    const int64_t i = row * c4 + j;
+    float4_t pv = reinterpret_cast<float4_t*>(p)[i];
+    float4_t mv = reinterpret_cast<float4_t*>(m)[i];
+    float4_t vv = reinterpret_cast<float4_t*>(v)[i];
+    float4_t gv = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (MODE == 1) {
+      gv = reinterpret_cast<float4_t*>(g)[i];
+      reinterpret_cast<float4_t*>(g)[i] = float4_t{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float pk = pv[k], mk = mv[k], vk = vv[k];
+      adam_elem(pk, gv[k], mk, vk, h);
+      pv[k] = pk; mv[k] = mk; vv[k] = vk;
+    }
+    reinterpret_cast<float4_t*>(p)[i] = pv;
+    reinterpret_cast<float4_t*>(m)[i] = mv;
+    reinterpret_cast<float4_t*>(v)[i] = vv;
+    if (shadow) {
+      typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+      reinterpret_cast<u32x2*>(shadow)[i] = u32x2{pack_bf16x2(pv[0], pv[1]), pack_bf16x2(pv[2], pv[3])};
+    }
+  };
+  if constexpr (MODE == 0) {
+    const int64_t n4 = R * c4;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+      const int64_t row = i / c4;
+      if (mask[row] == 0) row_update(row, i - row * c4);
+    }
+  } else {
+    __shared__ int claimed;
+    for (int64_t t = blockIdx.x; t < nrows; t += gridDim.x) {
+      const int64_t row = rows[t];
+      if (threadIdx.x == 0) claimed = (row >= 0 && row < R) ? atomicCAS(mask + row, 1, 2) == 1 : 0;
+      __syncthreads();
+      if (claimed)
+        for (int j = threadIdx.x; j < c4; j += blockDim.x) row_update(row, j);
+      __syncthreads();
+    }
+  }
+}
+
 struct TensorEntry {
   void* p;
   const void* g;
@@ -161,6 +218,44 @@ void adamw_step(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor
 void adam_step(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, c10::optional<torch::Tensor> shadow,
                double lr, double b1, double b2, double eps, double wd, int64_t step, double grad_scale, bool maximize) {
   flat_step(p, g, m, v, shadow, make_hyper(lr, b1, b2, eps, wd, step, grad_scale, maximize, false));
+}
+
+// mode 0: rows with mask == 0 as for a zero gradient; mode 1: the rows of `rows` whose mask is 1
+// (claimed once each, mask -> 2), with their gradient, which is then cleared
+void adam_rows_step(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, c10::optional<torch::Tensor> shadow,
+                    int64_t C, torch::Tensor mask, c10::optional<torch::Tensor> rows, int64_t mode, double lr, double b1,
+                    double b2, double eps, double wd, int64_t step, double grad_scale, bool maximize, bool decoupled) {
+  for (auto* t : {&p, &g, &m, &v}) {
+    TORCH_CHECK(t->is_cuda() && t->is_contiguous() && t->scalar_type() == torch::kFloat32, "row buffers must be fp32");
+    TORCH_CHECK(t->numel() == p.numel(), "row buffer sizes differ");
+  }
+  TORCH_CHECK(C > 0 && C % 4 == 0 && p.numel() % C == 0, "row width must divide the range and be a multiple of 4");
+  const int64_t R = p.numel() / C;
+  TORCH_CHECK(mask.is_cuda() && mask.scalar_type() == torch::kInt32 && mask.numel() == R, "mask: int32 [rows]");
+  bf16* sp = nullptr;
+  if (shadow.has_value() && shadow->defined()) {
+    TORCH_CHECK(shadow->scalar_type() == torch::kBFloat16 && shadow->numel() == p.numel());
+    sp = reinterpret_cast<bf16*>(shadow->data_ptr());
+  }
+  for (auto* t : {&p, &g, &m, &v})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "row buffers must be 16-B aligned");
+  const AdamHyper h = make_hyper(lr, b1, b2, eps, wd, step, grad_scale, maximize, decoupled);
+  auto stream = at::hip::getCurrentHIPStream();
+  if (mode == 0) {
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((R * (C / 4) + 255) / 256, 1 << 20));
+    hipLaunchKernelGGL(adam_rows_kernel<0>, dim3(grid), dim3(256), 0, stream, p.data_ptr<float>(), g.data_ptr<float>(),
+                       m.data_ptr<float>(), v.data_ptr<float>(), sp, R, (int)C, mask.data_ptr<int>(),
+                       (const int64_t*)nullptr, (int64_t)0, h);
+  } else {
+    TORCH_CHECK(rows.has_value() && rows->is_cuda() && rows->scalar_type() == torch::kInt64 && rows->is_contiguous(),
+                "mode 1 needs the token rows (int64)");
+    const int64_t n = rows->numel();
+    if (n == 0) return;
+    const int grid = (int)std::min<int64_t>(n, 65536);
+    hipLaunchKernelGGL(adam_rows_kernel<1>, dim3(grid), dim3(256), 0, stream, p.data_ptr<float>(), g.data_ptr<float>(),
+                       m.data_ptr<float>(), v.data_ptr<float>(), sp, R, (int)C, mask.data_ptr<int>(),
+                       rows->data_ptr<int64_t>(), n, h);
+  }
 }
 
 void multi_tensor_adam(std::vector<torch::Tensor> ps, std::vector<torch::Tensor> gs, std::vector<torch::Tensor> ms,

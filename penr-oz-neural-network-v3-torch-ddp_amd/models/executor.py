@@ -127,6 +127,20 @@ def _site_seed(seed: int, site: int) -> int:
     return (seed * 1_000_003 + 7_919 * (site + 1) + 0x5BD1E995) & 0x7FFFFFFFFFFFFFFF
 
 
+def _minus(ranges, cut):
+    """[(a, b)] ranges with the range ``cut`` (or None) removed."""
+    if cut is None:
+        return list(ranges)
+    c0, c1 = cut
+    out = []
+    for a, b in ranges:
+        if a < c0:
+            out.append((a, min(b, c0)))
+        if b > c1:
+            out.append((max(a, c1), b))
+    return [(a, b) for a, b in out if b > a]
+
+
 def cu_mask_words(spec: str, n_cu: int) -> list[int]:
     """CU mask words for PENROZ_SIDE_CUS: ``stride:k[:o]`` = CUs i with i % k == o, ``first:n`` =
     CUs 0..n-1 (bit i of word i // 32 = CU i)."""
@@ -541,15 +555,20 @@ class GPTExecutor:
         GEMM into each writes instead of accumulating (``gemm_ops.wgrad(accumulate=False)``), so
         the step neither clears them nor reads them back (PENROZ_GRAD_OVERWRITE=0: clear all)."""
         self.wait_gradients()
+        # a flat range the last backward left all-zero itself (the Gemma row-split embedding step)
+        skip, self._zero_skip = getattr(self, "_zero_skip", None), None
+        self._micro_since_zero = 0
         gaps = getattr(self, "_zero_gaps", None)
         if gaps is not None:
-            if getattr(self, "_zero_views_of", None) is not self.flat_grad:  # views of THIS buffer
-                self._zero_views = [self.flat_grad[a:b] for a, b in gaps]
-                self._zero_views_of = self.flat_grad
+            key = (self.flat_grad.data_ptr(), skip)
+            if getattr(self, "_zero_views_key", None) != key:  # views of THIS buffer
+                self._zero_views = [self.flat_grad[a:b] for a, b in _minus(gaps, skip)]
+                self._zero_views_key = key
             torch._foreach_zero_(self._zero_views)
             self._stale = {k: [r] for k, r in self._wgrad_ranges.items()}
         else:
-            self.flat_grad.zero_()
+            for a, b in _minus([(0, self.flat_grad.numel())], skip):
+                self.flat_grad[a:b].zero_()
             self._stale = {}
         self._captured = None
 

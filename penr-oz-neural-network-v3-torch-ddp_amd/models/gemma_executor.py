@@ -355,6 +355,50 @@ class GemmaExecutor(GPTExecutor):
     def _mm(self, x: Tensor, w: Tensor, out: Tensor) -> Tensor:
         return torch.mm(x, w.t(), out=out)
 
+    # ---- row-split AdamW of the embedding table ------------------------------------------------
+    # The table's gradient is zero on every row this step's tokens do not touch (8k of 262k rows
+    # at Gemma-3 1B B=8), and those rows' AdamW update does not depend on the backward. With the
+    # optimizer fused into the backward and one micro-step per optimizer step, the untouched rows
+    # are updated on the side stream while the forward runs (no gradient read); the touched rows
+    # follow the embedding backward, which leaves the table's gradient all-zero again, so zero_grad
+    # skips the 1.2 GB range. Bitwise the same update as the dense step. PENROZ_EMB_ROW_ADAM=0: off.
+    def _row_split_begin(self, idx: Tensor):
+        import os
+        self._row_split = None
+        app = self._opt_apply
+        side = getattr(self, "_side", None)
+        C = self.spec.C
+        if (app is None or not hasattr(app, "rows") or side is None or self._micro_since_zero != 1
+                or C % 4 or os.environ.get("PENROZ_EMB_ROW_ADAM", "1") == "0"):
+            return
+        es, ee = self.segments[self.L + 1]
+        V = self.spec.V
+        if (ee - es) != V * C or es % 4:
+            return
+        if getattr(self, "_emb_mask", None) is None:
+            self._emb_mask = torch.zeros(V, dtype=torch.int32, device=self.device)
+        rows = idx.reshape(-1).to(torch.int64)
+        main = torch.cuda.current_stream(self.device)
+        with torch.cuda.stream(side):
+            side.wait_stream(main)
+            self._emb_mask.zero_()
+            self._emb_mask.index_fill_(0, rows, 1)
+            app.rows(es, ee, C, self._emb_mask, None, 0)
+        rows.record_stream(side)
+        self._row_split = (es, ee, rows)
+
+    def _segment_done(self, seg_index: int, sync: bool):
+        rs = getattr(self, "_row_split", None)
+        if rs is None or seg_index != self.L + 1 or self._opt_apply is None or not sync:
+            return super()._segment_done(seg_index, sync)
+        es, ee, rows = rs
+        main = torch.cuda.current_stream(self.device)
+        with torch.cuda.stream(self._side):
+            self._side.wait_stream(main)
+            self._opt_apply.rows(es, ee, self.spec.C, self._emb_mask, rows, 1)
+        self._row_split = None
+        self._zero_skip = (es, ee)  # the touched rows' gradient was cleared by the kernel
+
     # ------------------------------------------------------------------ forward
     def _combine_fwd(self, mode, x, a, w1, w2, eps1, eps2, h_out, y_out, s_save, r1, r2):
         _ext.kernels().gemma_combine_fwd(mode, x, a, w1, w2, float(eps1), float(eps2), h_out, y_out, s_save, r1, r2)
@@ -417,6 +461,8 @@ class GemmaExecutor(GPTExecutor):
         f, gr = self.f32, self.grad
         k = _ext.kernels()
         self._refresh_transposed()
+        self._micro_since_zero = getattr(self, "_micro_since_zero", 0) + 1
+        self._row_split_begin(idx)
         with trace_range("forward"):
             self._forward(idx, training=True, dropout_seed=seed)
         cap = capture and self._captured is None

@@ -168,6 +168,13 @@ class _FusedMixin:
         def apply(s: int, e: int):
             fn(f["param"][s:e], f["grad"][s:e], f["m"][s:e], f["v"][s:e], sh[s:e] if sh is not None else None,
                lr, b1, b2, eps, wd, step, grad_scale, maximize)
+
+        def apply_rows(s: int, e: int, C: int, mask, rows, mode: int):
+            """[s, e) as an embedding table of width C: fused_ops.adam_rows_step (same math)."""
+            fused_ops.adam_rows_step(f["param"][s:e], f["grad"][s:e], f["m"][s:e], f["v"][s:e],
+                                     sh[s:e] if sh is not None else None, C, mask, rows, mode, lr, b1, b2, eps, wd,
+                                     step, grad_scale, maximize, self._decoupled)
+        apply.rows = apply_rows
         return apply
 
     def flat_step_ranges(self, ranges, grad_scale: float = 1.0) -> bool:

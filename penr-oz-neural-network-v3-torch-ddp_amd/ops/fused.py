@@ -125,6 +125,18 @@ def adamw_step(params: Tensor, grads: Tensor, exp_avg: Tensor, exp_avg_sq: Tenso
                          bool(maximize))
 
 
+def adam_rows_step(params: Tensor, grads: Tensor, exp_avg: Tensor, exp_avg_sq: Tensor, shadow: Tensor | None,
+                   C: int, mask: Tensor, rows: Tensor | None, mode: int, lr: float, beta1: float, beta2: float,
+                   eps: float, weight_decay: float, step: int, grad_scale: float = 1.0, maximize: bool = False,
+                   decoupled: bool = True):
+    """Row-split Adam(W) of an embedding table held in flat fp32 buffers ([R·C]): mode 0 updates
+    the rows with ``mask == 0`` as for a zero gradient (no gradient read); mode 1 the rows listed
+    in ``rows`` whose mask is 1 (each claimed once, mask -> 2), then clears their gradient."""
+    kernels().adam_rows_step(params, grads, exp_avg, exp_avg_sq, shadow, int(C), mask, rows, int(mode), float(lr),
+                             float(beta1), float(beta2), float(eps), float(weight_decay), int(step),
+                             float(grad_scale), bool(maximize), bool(decoupled))
+
+
 def adam_step(params, grads, exp_avg, exp_avg_sq, shadow, lr, beta1, beta2, eps, weight_decay, step,
               grad_scale: float = 1.0, maximize: bool = False):
     """Flat-buffer Adam (L2 weight decay added to the gradient, torch ``Adam`` semantics)."""

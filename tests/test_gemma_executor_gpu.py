@@ -316,6 +316,33 @@ def test_optimizer_in_backward_matches_the_separate_step(micro):
             assert torch.equal(p, q), n
 
 
+def test_row_split_embedding_adamw_matches_dense(monkeypatch):
+    """The embedding table's AdamW split into untouched rows (during the forward, zero gradient)
+    and touched rows (after the embedding backward, gradient cleared) == the dense fused step; the
+    gradient buffer's table range stays zero between steps (zero_grad skips it)."""
+    from penroz.models.model import _FusedRunner
+    a, b = _gemma("gemma3_text", seed=4).to(DEV), _gemma("gemma3_text", seed=4).to(DEV)
+    monkeypatch.setenv("PENROZ_EMB_ROW_ADAM", "0")
+    la = _train(a, 3, True)
+    monkeypatch.setenv("PENROZ_EMB_ROW_ADAM", "1")
+    lb = _train(b, 3, True)
+    assert la == pytest.approx(lb, abs=1e-5)
+    for (n, p), (_, q) in zip(a.named_parameters(), b.named_parameters()):
+        if n == "layers.0.weight":  # scatter-add order of the table gradient
+            assert torch.allclose(p, q, rtol=0, atol=1e-5), n
+        else:
+            assert torch.equal(p, q), n
+    runner = _FusedRunner(b, torch.device(DEV), False)
+    ex = runner.exec
+    x = torch.randint(0, 512, (2, 64), device=DEV)
+    runner.zero_grad()
+    ex.train_micro_step(x, x, 1.0, fuse_optimizer=True)
+    torch.cuda.synchronize()
+    assert getattr(ex, "_zero_skip", None) is not None, "row-split path not taken"
+    es, ee = ex._zero_skip
+    assert ex.flat_grad[es:ee].abs().max().item() == 0.0
+
+
 def test_capture_returns_activation_and_gradient_pairs():
     m = _gemma("gemma2").to(DEV)
     ex = GemmaExecutor(m, torch.device(DEV))
