@@ -36,7 +36,12 @@ class NativeComm:
         uid = store.get(key)
         # the protocol (Simple / LL / LL128) and algorithm (Ring / Tree) are fixed per communicator:
         # RCCL reads NCCL_PROTO / NCCL_ALGO while tuning a communicator at init, so they are set for
-        # this init only (a user's own setting is left alone when nothing is asked for)
+        # this init only (a user's own setting is left alone when nothing is asked for).
+        # Threading assumption: setenv is not safe against a concurrent getenv in another thread.
+        # Forced arms are opt-in (PENROZ_COMM_SWEEP_ARMS=full, commtune.sweep_arms) and are built in the
+        # first-contact sweep, before training starts, with no collective in flight on any other
+        # communicator of this process (the sweep's own c10d agreement calls have returned).
+        # That leaves only RCCL's idle proxy threads, which read NCCL_PROTO / NCCL_ALGO at init only.
         forced = {k: v for k, v in (("NCCL_PROTO", proto), ("NCCL_ALGO", algo)) if v}
         prev = {k: os.environ.get(k) for k in forced}
         os.environ.update(forced)
