@@ -186,3 +186,12 @@ def test_side_stream_cu_mask_words():
     assert cu_mask_words("first:40", 256)[:2] == [0xFFFFFFFF, 0xFF] and cu_mask_words("first:40", 256)[2:] == [0] * 6
     with pytest.raises(ValueError):
         cu_mask_words("half", 256)
+
+
+def test_zero_gap_minus_skip_range():
+    from penroz.models.executor import _minus
+    assert _minus([(0, 10), (20, 30)], None) == [(0, 10), (20, 30)]
+    assert _minus([(0, 10), (20, 30)], (5, 25)) == [(0, 5), (25, 30)]
+    assert _minus([(0, 10)], (0, 10)) == []
+    assert _minus([(0, 100)], (40, 60)) == [(0, 40), (60, 100)]
+    assert _minus([(10, 20)], (30, 40)) == [(10, 20)]
