@@ -61,7 +61,8 @@ void adam_rows_step(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Te
 torch::Tensor sample_tokens(torch::Tensor logits, c10::optional<torch::Tensor> uniform, double temperature,
                             int64_t top_k);
 void sample_step(torch::Tensor logits, double temperature, int64_t top_k, torch::Tensor seed, torch::Tensor step,
-                 torch::Tensor idx_out, torch::Tensor out_buf);
+                 torch::Tensor idx_out, torch::Tensor out_buf, c10::optional<torch::Tensor> adv_a,
+                 c10::optional<torch::Tensor> adv_b, c10::optional<torch::Tensor> done);
 void decode_advance(torch::Tensor a, torch::Tensor b, torch::Tensor c);
 // decode_attn.hip
 torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c10::optional<torch::Tensor> k_scale,
@@ -186,7 +187,11 @@ PYBIND11_MODULE(penroz_kernels, m) {
   m.def("adam_rows_step", &adam_rows_step, "row-split Adam/AdamW step of an embedding table (mode 0: untouched rows, 1: touched rows)");
   m.def("multi_tensor_adam", &multi_tensor_adam);
   m.def("sample_tokens", &sample_tokens);
-  m.def("sample_step", &sample_step, "decode-step sampler: device-hashed uniforms, writes idx_out and out_buf[:, *step]");
+  m.def("sample_step", &sample_step, "decode-step sampler: device-hashed uniforms, writes idx_out and out_buf[:, *step]; "
+        "with adv_a / adv_b / done the last row's writer also advances the counters",
+        pybind11::arg("logits"), pybind11::arg("temperature"), pybind11::arg("top_k"), pybind11::arg("seed"),
+        pybind11::arg("step"), pybind11::arg("idx_out"), pybind11::arg("out_buf"), pybind11::arg("adv_a") = pybind11::none(),
+        pybind11::arg("adv_b") = pybind11::none(), pybind11::arg("done") = pybind11::none());
   m.def("decode_advance", &decode_advance, "+1 on three device int64 scalars");
   m.def("decode_attn", &decode_attn, pybind11::arg("q"), pybind11::arg("kc"), pybind11::arg("vc"), pybind11::arg("k_scale"),
         pybind11::arg("v_scale"), pybind11::arg("S"), pybind11::arg("q_offset"), pybind11::arg("scale"),

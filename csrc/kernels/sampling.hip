@@ -29,6 +29,13 @@ struct SampleIO {
   int64_t* out;
   int64_t* out2;
   int64_t out2_stride;
+  // graph decode (sample_step with advance): the writer of the LAST row to finish also advances
+  // the step counters (+1 on *adv_a, *adv_b, *step) — every row has read *step by then — and
+  // re-arms the arrival counter: one launch less per decoded token
+  int64_t* adv_a = nullptr;
+  int64_t* adv_b = nullptr;
+  unsigned* done = nullptr;
+  int nrows = 0;
   __device__ __forceinline__ float uniform(int row) const {
     if (uni) return uni[row];
     uint64_t z = (uint64_t)*seed + 0x9E3779B97F4A7C15ull * (uint64_t)(*step + 1) + 0xD1B54A32D192ED03ull * (uint64_t)(row + 1);
@@ -40,6 +47,16 @@ struct SampleIO {
   __device__ __forceinline__ void write(int row, int64_t tok) const {
     out[row] = tok;
     if (out2) out2[(size_t)row * out2_stride + *step] = tok;
+    if (done) {
+      __threadfence();  // this row's reads of *step and its stores come before its arrival
+      if (atomicAdd(done, 1u) == (unsigned)nrows - 1u) {
+        ++*adv_a;
+        ++*adv_b;
+        ++*const_cast<int64_t*>(step);
+        *done = 0u;
+        __threadfence();
+      }
+    }
   }
 };
 
@@ -836,15 +853,27 @@ torch::Tensor sample_tokens(torch::Tensor logits, c10::optional<torch::Tensor> u
 // Graph-replayed decode: token of row r -> idx_out[r] and out_buf[r, *step]; uniforms hashed
 // from (seed, *step, r) on the device. Then one tiny kernel advances the step counters.
 void sample_step(torch::Tensor logits, double temperature, int64_t top_k, torch::Tensor seed, torch::Tensor step,
-                 torch::Tensor idx_out, torch::Tensor out_buf) {
+                 torch::Tensor idx_out, torch::Tensor out_buf, c10::optional<torch::Tensor> adv_a,
+                 c10::optional<torch::Tensor> adv_b, c10::optional<torch::Tensor> done) {
   TORCH_CHECK(logits.dim() == 2 && step.is_cuda() && step.scalar_type() == torch::kInt64 && step.numel() == 1);
   TORCH_CHECK(seed.is_cuda() && seed.scalar_type() == torch::kInt64 && seed.numel() == 1, "seed: device int64 [1]");
   const int B = logits.size(0);
   TORCH_CHECK(idx_out.scalar_type() == torch::kInt64 && idx_out.numel() == B && idx_out.is_contiguous());
   TORCH_CHECK(out_buf.scalar_type() == torch::kInt64 && out_buf.dim() == 2 && out_buf.size(0) == B &&
               out_buf.stride(1) == 1, "out_buf [B, n] int64");
-  launch_sample(logits, SampleIO{nullptr, seed.data_ptr<int64_t>(), step.data_ptr<int64_t>(), idx_out.data_ptr<int64_t>(),
-                                 out_buf.data_ptr<int64_t>(), out_buf.stride(0)}, temperature, top_k);
+  SampleIO io{nullptr, seed.data_ptr<int64_t>(), step.data_ptr<int64_t>(), idx_out.data_ptr<int64_t>(),
+               out_buf.data_ptr<int64_t>(), out_buf.stride(0)};
+  if (done.has_value() && done->defined()) {  // fused counter advance (see SampleIO)
+    TORCH_CHECK(adv_a.has_value() && adv_b.has_value(), "sample_step: advance needs both counters");
+    for (const torch::Tensor* t : {&*adv_a, &*adv_b})
+      TORCH_CHECK(t->is_cuda() && t->scalar_type() == torch::kInt64 && t->numel() == 1, "advance counters: int64 [1]");
+    TORCH_CHECK(done->is_cuda() && done->scalar_type() == torch::kInt32 && done->numel() == 1, "done: int32 [1] (zero)");
+    io.adv_a = adv_a->data_ptr<int64_t>();
+    io.adv_b = adv_b->data_ptr<int64_t>();
+    io.done = reinterpret_cast<unsigned*>(done->data_ptr<int>());
+    io.nrows = B;
+  }
+  launch_sample(logits, io, temperature, top_k);
 }
 
 __global__ void decode_advance_kernel(int64_t* a, int64_t* b, int64_t* c) {

@@ -83,6 +83,9 @@ BATCHED_BLOCK = os.environ.get("PENROZ_DECODE_BATCHED", "1") != "0"
 # (csrc/kernels/decode_linear.hip decode_gemv: one memory round trip, no LDS, no barrier, no
 # split-K hand-off); "0": decode_ln_linear + skinny GEMMs
 GEMV_MAX_ROWS = int(os.environ.get("PENROZ_DECODE_GEMV_MAX_ROWS", "4"))
+# the sampler's last row advances the step counters itself (sample_step with adv_a / adv_b / done:
+# one launch less per token); "0": the separate decode_advance kernel
+FUSED_ADVANCE = os.environ.get("PENROZ_DECODE_FUSED_ADVANCE", "1") != "0"
 
 
 class _GraphMode:
@@ -596,9 +599,15 @@ class GraphDecoder:
                 # buffer (uniforms hashed on the device), one kernel advances the counters
                 V = last.shape[-1]
                 k = 0 if self.top_k is None or self.top_k >= V else int(self.top_k)
-                _ext.kernels().sample_step(last.contiguous(), self.temperature, k, self.seed_t, self.step_t,
-                                           self.idx, self.out)
-                _ext.kernels().decode_advance(self.cache.pos_t, self.cache.len_t, self.step_t)
+                if FUSED_ADVANCE:  # the sampler's last row advances the counters itself
+                    if getattr(self, "_done_t", None) is None:
+                        self._done_t = torch.zeros(1, dtype=torch.int32, device=last.device)
+                    _ext.kernels().sample_step(last.contiguous(), self.temperature, k, self.seed_t, self.step_t,
+                                               self.idx, self.out, self.cache.pos_t, self.cache.len_t, self._done_t)
+                else:
+                    _ext.kernels().sample_step(last.contiguous(), self.temperature, k, self.seed_t, self.step_t,
+                                               self.idx, self.out)
+                    _ext.kernels().decode_advance(self.cache.pos_t, self.cache.len_t, self.step_t)
             else:
                 nxt = samp_ops.sample(last, self.temperature, self.top_k, device_rng=True)
                 torch.add(nxt, 0, out=self.idx)  # a kernel, not a memcpy node

@@ -899,6 +899,33 @@ def test_sample_step_and_advance(V, dt):
     assert torch.allclose(counts / counts.sum(), torch.softmax(torch.tensor([1.0, 0.5, 0.0]), -1), atol=0.03)
 
 
+@pytest.mark.parametrize("B", [1, 3, 64])
+@pytest.mark.parametrize("topk", [0, 50])
+def test_sample_step_fused_advance(B, topk):
+    """sample_step with the counters: same tokens as without, out_buf written at the OLD step, and
+    the last row's writer bumps (pos, len, step) by one and re-arms the arrival counter, over
+    repeated calls (graph replay)."""
+    K = _ext.kernels()
+    V, n = 50304, 6
+    torch.manual_seed(B + topk)
+    logits = (torch.randn(B, V, device=DEV) * 2).to(torch.bfloat16)
+    seed = torch.tensor([99], device=DEV)
+    temp = 0.0 if topk == 0 else 1.0
+    ref_idx = torch.zeros(B, 1, dtype=torch.long, device=DEV)
+    ref_out = torch.full((B, n), -1, dtype=torch.long, device=DEV)
+    idx = torch.zeros_like(ref_idx)
+    out = torch.full_like(ref_out, -1)
+    pos, ln, step = (torch.tensor([v], device=DEV) for v in (10, 11, 0))
+    done = torch.zeros(1, dtype=torch.int32, device=DEV)
+    for s in range(4):
+        K.sample_step(logits, temp, topk, seed, torch.tensor([s], device=DEV), ref_idx, ref_out)
+        K.sample_step(logits, temp, topk, seed, step, idx, out, pos, ln, done)
+        torch.cuda.synchronize()
+        assert torch.equal(idx, ref_idx), s
+        assert (pos.item(), ln.item(), step.item(), done.item()) == (11 + s, 12 + s, 1 + s, 0)
+    assert torch.equal(out[:, :4], ref_out[:, :4]) and bool((out[:, 4:] == -1).all())
+
+
 @pytest.mark.parametrize("C", [64, 1152, 2304, 5376])
 @pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("with_y", [True, False])
