@@ -52,7 +52,11 @@ __device__ __forceinline__ void dl_tile(int id, int nrb, int nct, int& rb, int& 
   }
 }
 
-// grid = ceil(M/16) * ceil(N/64), block 256. LDS: 16 normalised rows [16][K + 8] bf16.
+// grid = ceil(M/16) * ceil(N/(64/KS)), block 256. LDS: 16 normalised rows [16][K + 8] bf16.
+// KS = 2: 32-column tiles, the two waves of a column block split K in halves and meet in LDS —
+// twice the workgroups (qkv at 64 rows: 288 instead of 144 on 256 CUs), half the weight bytes per
+// workgroup.
+template <int KS>
 __global__ void __launch_bounds__(256) decode_ln_gemm_kernel(const float* __restrict__ resid,
                                                              const float* __restrict__ gamma,
                                                              const float* __restrict__ beta, float eps,
@@ -60,21 +64,24 @@ __global__ void __launch_bounds__(256) decode_ln_gemm_kernel(const float* __rest
                                                              bf16* __restrict__ out, int64_t o_rs, int M, int N, int K,
                                                              int act, int flags) {
   __shared__ __attribute__((aligned(16))) bf16 xs[16 * (1024 + 8)];
+  __shared__ __attribute__((aligned(16))) dl_f32x4 kred[KS > 1 ? (KS - 1) * (4 / KS) * 64 : 1];
+  constexpr int TW = 64 / KS, NCB = 4 / KS, MS = kDlMaxSteps / KS;
   const int LDX = K + 8;  // +16 B per row: a fragment's 16 row reads spread over the banks
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int cb = wid % NCB, kh = wid / NCB;  // column block, K part (KS = 2: halves)
   int rb, ct;
-  dl_tile(blockIdx.x, (M + 15) / 16, (N + 63) / 64, rb, ct);
-  const int steps = K / 32;
+  dl_tile(blockIdx.x, (M + 15) / 16, (N + TW - 1) / TW, rb, ct);
+  const int steps = K / 32 / KS, s0 = kh * steps;  // this wave's k-steps: s0 .. s0 + steps
   const int r16 = lane & 15, kq = 8 * (lane >> 4);
-  const int n0 = ct * 64 + wid * 16;  // this wave's column block
+  const int n0 = ct * TW + cb * 16;  // this wave's column block
   const bool live = n0 < N;
 
-  // 1. the wave's weight fragments for the whole K range, in flight during the prologue
-  dl_u32x4 wa[kDlMaxSteps];
+  // 1. the wave's weight fragments for its K range, in flight during the prologue
+  dl_u32x4 wa[MS];
   {
-    const bf16* wp = w + (size_t)min(n0 + r16, N - 1) * K + kq;
+    const bf16* wp = w + (size_t)min(n0 + r16, N - 1) * K + kq + s0 * 32;
 #pragma unroll
-    for (int s = 0; s < kDlMaxSteps; ++s)
+    for (int s = 0; s < MS; ++s)
       if (s < steps && live && !(flags & 2)) wa[s] = *reinterpret_cast<const dl_u32x4*>(wp + s * 32);
   }
 
@@ -145,22 +152,29 @@ __global__ void __launch_bounds__(256) decode_ln_gemm_kernel(const float* __rest
     }
   }
   __syncthreads();
-  if (!live) return;
+  if (KS == 1 && !live) return;
   if (flags & 2) {
 #pragma unroll
-    for (int s = 0; s < kDlMaxSteps; ++s) wa[s] = dl_u32x4{0u, 0u, 0u, 0u};
+    for (int s = 0; s < MS; ++s) wa[s] = dl_u32x4{0u, 0u, 0u, 0u};
   }
 
-  // 3. MFMA over the full K, x fragments from LDS
+  // 3. MFMA over the wave's K range, x fragments from LDS
   dl_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  const bf16* xl = xs + r16 * LDX + kq;
+  const bf16* xl = xs + r16 * LDX + kq + s0 * 32;
 #pragma unroll
-  for (int s = 0; s < kDlMaxSteps; ++s) {
-    if (s < steps && !(flags & 16)) {
+  for (int s = 0; s < MS; ++s) {
+    if (s < steps && live && !(flags & 16)) {
       const dl_u32x4 xb = *reinterpret_cast<const dl_u32x4*>(xl + s * 32);
       acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(dl_bf16x8, wa[s]),
                                                     __builtin_bit_cast(dl_bf16x8, xb), acc, 0, 0, 0);
     }
+  }
+  if constexpr (KS > 1) {  // the K parts of a column block meet in LDS (every wave reaches the barrier)
+    if (kh > 0) kred[((kh - 1) * NCB + cb) * 64 + lane] = acc;
+    __syncthreads();
+    if (kh > 0 || !live) return;
+#pragma unroll
+    for (int p = 0; p < KS - 1; ++p) acc += kred[(p * NCB + cb) * 64 + lane];
   }
 
   // 4. bias (+ GELU on the bf16-rounded linear output, the unfused pair's rounding point)
@@ -490,11 +504,20 @@ void decode_ln_gemm(torch::Tensor resid, torch::Tensor gamma, torch::Tensor beta
               "decode_ln_gemm: bf16 out [M, N], rows 8-B aligned");
   TORCH_CHECK(act >= 0 && act <= 2, "decode_ln_gemm: act 0 (none), 1 (GELU erf), 2 (GELU tanh)");
   const bf16* bp = dl_bias(bias, N, "decode_ln_gemm");
-  const int grid = ((M + 15) / 16) * ((N + 63) / 64);
-  hipLaunchKernelGGL(decode_ln_gemm_kernel, dim3(grid), dim3(256), 0, at::hip::getCurrentHIPStream(),
-                     resid.data_ptr<float>(), gamma.data_ptr<float>(), beta.data_ptr<float>(), (float)eps,
-                     reinterpret_cast<const bf16*>(w.data_ptr()), bp, reinterpret_cast<bf16*>(out.data_ptr()),
-                     (int64_t)out.stride(0), M, N, K, (int)act, (int)flags);
+  // K halves (KS = 2) by default: GPT-2 decode B = 16 / 32 / 64 0.567 / 0.584 / 0.636 -> 0.532 /
+  // 0.550 / 0.620 ms/step; quarters (KS = 4) lost: 0.55 / 0.74 / 0.96 — every workgroup repeats the
+  // LayerNorm of its 16 rows (profiles/decode_r5.md). PENROZ_DECODE_LN_KSPLIT=1: 64-column tiles.
+  static const int ks_env = [] {
+    const char* e = std::getenv("PENROZ_DECODE_LN_KSPLIT");
+    return e && e[0] == '1' ? 1 : 2;
+  }();
+  const int ks = ks_env == 2 && (K / 32) % 2 == 0 ? 2 : 1;
+  const int tw = 64 / ks;
+  const int grid = ((M + 15) / 16) * ((N + tw - 1) / tw);
+  hipLaunchKernelGGL(ks == 2 ? decode_ln_gemm_kernel<2> : decode_ln_gemm_kernel<1>,
+                     dim3(grid), dim3(256), 0, at::hip::getCurrentHIPStream(), resid.data_ptr<float>(), gamma.data_ptr<float>(),
+                     beta.data_ptr<float>(), (float)eps, reinterpret_cast<const bf16*>(w.data_ptr()), bp,
+                     reinterpret_cast<bf16*>(out.data_ptr()), (int64_t)out.stride(0), M, N, K, (int)act, (int)flags);
 }
 
 // resid[M, N] += x · wᵀ + bias (fp32 residual, in place). flags: timing ablations (1 no x reads,
