@@ -605,9 +605,17 @@ void decode_gemv(c10::optional<torch::Tensor> x, c10::optional<torch::Tensor> ri
   }
   const int cpl = (K / 8 + 31) / 32;
   int rpw = (int)rows_per_wave;
-  // by shape (profiles/decode_gemv_r5.log, batch 1): narrow outputs want more waves (2 rows each),
-  // the vocabulary projection fewer, longer-lived waves (8 rows); K > 2048 keeps 2 rows per wave
-  if (rpw <= 0) rpw = N >= 16384 ? 8 : (cpl > 8 || N <= 1024) ? 2 : 4;
+  // by shape: the vocabulary projection wants fewer, longer-lived waves (8 rows); everything else
+  // 2 rows per wave — the most workgroups in flight. In the replayed step that beat 4 rows for the
+  // wider QKV / fc outputs, which the isolated microbench preferred (GPT-2 B = 1 0.3594 / 0.3608 ->
+  // 0.3563 / 0.3547 ms, Gemma-3 1B neutral; profiles/decode_r5.md). PENROZ_DECODE_GEMV_RPW forces 2 /
+  // 4 / 8 below 16k rows (A/B).
+  static const int rpw_env = [] {
+    const char* e = std::getenv("PENROZ_DECODE_GEMV_RPW");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (rpw <= 0 && rpw_env > 0 && N < 16384) rpw = rpw_env;
+  if (rpw <= 0) rpw = N >= 16384 ? 8 : 2;
   TORCH_CHECK(rpw == 2 || rpw == 4 || rpw == 8, "decode_gemv: rows_per_wave 2, 4 or 8");
   const int RPv = rpw / 2;
   const dim3 grid((N + rpw - 1) / rpw);
