@@ -92,7 +92,9 @@ void decode_ln_gemm(torch::Tensor resid, torch::Tensor gamma, torch::Tensor beta
 void decode_gemv(c10::optional<torch::Tensor> x, c10::optional<torch::Tensor> rin, c10::optional<torch::Tensor> delta,
                  c10::optional<torch::Tensor> dbias, c10::optional<torch::Tensor> rout,
                  c10::optional<torch::Tensor> gamma, c10::optional<torch::Tensor> beta, double eps, torch::Tensor w,
-                 c10::optional<torch::Tensor> bias, torch::Tensor out, int64_t act, int64_t rows_per_wave);
+                 c10::optional<torch::Tensor> bias, torch::Tensor out, int64_t act, int64_t rows_per_wave,
+                 c10::optional<torch::Tensor> emb_idx, c10::optional<torch::Tensor> emb_wte,
+                 c10::optional<torch::Tensor> emb_wpe, c10::optional<torch::Tensor> emb_pos);
 void decode_gemv_pair(torch::Tensor x, torch::Tensor w, torch::Tensor out, int64_t mode, int64_t kind, int64_t D,
                       int64_t nrot, c10::optional<torch::Tensor> cosv, c10::optional<torch::Tensor> sinv,
                       int64_t pairs_per_wave);
@@ -227,8 +229,11 @@ PYBIND11_MODULE(penroz_kernels, m) {
   m.def("decode_gemv", &decode_gemv, pybind11::arg("x"), pybind11::arg("resid_in"), pybind11::arg("delta"),
         pybind11::arg("dbias"), pybind11::arg("resid_out"), pybind11::arg("gamma"), pybind11::arg("beta"),
         pybind11::arg("eps"), pybind11::arg("w"), pybind11::arg("bias"), pybind11::arg("out"), pybind11::arg("act") = 0,
-        pybind11::arg("rows_per_wave") = 0,
-        "decode GEMV for 1..4 rows: act(x · Wᵀ + bias), or act(LN(resid_in + delta + dbias) · Wᵀ + bias)");
+        pybind11::arg("rows_per_wave") = 0, pybind11::arg("emb_idx") = pybind11::none(),
+        pybind11::arg("emb_wte") = pybind11::none(), pybind11::arg("emb_wpe") = pybind11::none(),
+        pybind11::arg("emb_pos") = pybind11::none(),
+        "decode GEMV for 1..4 rows: act(x · Wᵀ + bias), or act(LN(resid_in + delta + dbias) · Wᵀ + bias), or "
+        "act(LN(wte[idx] + wpe[pos]) · Wᵀ + bias) with the embedding rows written to resid_out");
   m.def("decode_gemv_pair", &decode_gemv_pair, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("out"),
         pybind11::arg("mode"), pybind11::arg("kind") = 0, pybind11::arg("D") = 0, pybind11::arg("nrot") = 0,
         pybind11::arg("cos") = pybind11::none(), pybind11::arg("sin") = pybind11::none(),

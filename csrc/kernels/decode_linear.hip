@@ -287,7 +287,9 @@ __global__ void __launch_bounds__(64) decode_gemv_kernel(
     float* __restrict__ rout, const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
     const bf16* __restrict__ x, int64_t x_rs, const bf16* __restrict__ w, const bf16* __restrict__ bias,
     bf16* __restrict__ out, int64_t o_rs, int N, int K, int act, int D = 0, int nrot = 0,
-    const float* __restrict__ cosv = nullptr, const float* __restrict__ sinv = nullptr) {
+    const float* __restrict__ cosv = nullptr, const float* __restrict__ sinv = nullptr,
+    const int64_t* __restrict__ eidx = nullptr, const bf16* __restrict__ ewte = nullptr,
+    const bf16* __restrict__ ewpe = nullptr, const int64_t* __restrict__ epos = nullptr, int eV = 0, int eP = 0) {
   constexpr bool LN = PRO == 1;
   const int lane = threadIdx.x, h = lane >> 5, l32 = lane & 31;
   const int nc = K / 8;  // 16-B chunks per row
@@ -325,12 +327,23 @@ __global__ void __launch_bounds__(64) decode_gemv_kernel(
       }
   } else {
     float v[M][CPL][8];
+    // embedding mode (ewte): the residual row is wte[token] + wpe[position] (the first block of a
+    // decode step, embed_fwd_kernel's arithmetic: clamped token, position min(*epos, P - 1))
+    const int epos_v = ewte ? min((int)*epos, eP - 1) : 0;
 #pragma unroll
     for (int m = 0; m < M; ++m)
 #pragma unroll
       for (int i = 0; i < CPL; ++i) {
         const int c = l32 + 32 * i;
-        if (c < nc) {
+        if (c < nc && ewte) {
+          int64_t tok = eidx[m];
+          tok = tok < 0 ? 0 : (tok >= eV ? eV - 1 : tok);
+          float a[8], b[8];
+          Vec8<bf16>::load(ewte + (size_t)tok * K + 8 * c, a);
+          Vec8<bf16>::load(ewpe + (size_t)epos_v * K + 8 * c, b);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[m][i][k] = a[k] + b[k];
+        } else if (c < nc) {
           const float4_t* rp = reinterpret_cast<const float4_t*>(rin + (size_t)m * K + 8 * c);
           const float4_t a = rp[0], b = rp[1];
           v[m][i][0] = a[0]; v[m][i][1] = a[1]; v[m][i][2] = a[2]; v[m][i][3] = a[3];
@@ -352,7 +365,7 @@ __global__ void __launch_bounds__(64) decode_gemv_kernel(
           for (int k = 0; k < 8; ++k) v[m][i][k] = 0.f;
         }
       }
-    if (delta && rout && blockIdx.x == 0 && h == 0) {
+    if ((delta || ewte) && rout && blockIdx.x == 0 && h == 0) {
 #pragma unroll
       for (int m = 0; m < M; ++m)
 #pragma unroll
@@ -547,8 +560,15 @@ void decode_gemm_acc(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tens
 void decode_gemv(c10::optional<torch::Tensor> x, c10::optional<torch::Tensor> rin, c10::optional<torch::Tensor> delta,
                  c10::optional<torch::Tensor> dbias, c10::optional<torch::Tensor> rout,
                  c10::optional<torch::Tensor> gamma, c10::optional<torch::Tensor> beta, double eps, torch::Tensor w,
-                 c10::optional<torch::Tensor> bias, torch::Tensor out, int64_t act, int64_t rows_per_wave) {
+                 c10::optional<torch::Tensor> bias, torch::Tensor out, int64_t act, int64_t rows_per_wave,
+                 c10::optional<torch::Tensor> emb_idx, c10::optional<torch::Tensor> emb_wte,
+                 c10::optional<torch::Tensor> emb_wpe, c10::optional<torch::Tensor> emb_pos) {
   const bool ln = !(x.has_value() && x->defined());
+  const bool emb = emb_wte.has_value() && emb_wte->defined();
+  const int64_t* eip = nullptr;
+  const bf16 *ewp = nullptr, *epp = nullptr;
+  const int64_t* eps_p = nullptr;
+  int eV = 0, eP = 0;
   const int N = w.size(0), K = w.size(1);
   TORCH_CHECK(w.is_cuda() && w.scalar_type() == torch::kBFloat16 && w.dim() == 2 && w.is_contiguous() &&
                   reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0 && K % 8 == 0,
@@ -568,6 +588,30 @@ void decode_gemv(c10::optional<torch::Tensor> x, c10::optional<torch::Tensor> ri
     M = x->size(0);
     xp = reinterpret_cast<const bf16*>(x->data_ptr());
     x_rs = x->stride(0);
+  } else if (emb) {  // LN mode on the step's embedding rows; resid_out receives them
+    TORCH_CHECK(emb_idx.has_value() && emb_wpe.has_value() && emb_pos.has_value(), "decode_gemv: embedding mode needs idx / wpe / pos");
+    TORCH_CHECK(emb_idx->is_cuda() && emb_idx->scalar_type() == torch::kInt64 && emb_idx->is_contiguous(),
+                "decode_gemv: int64 token ids");
+    for (const torch::Tensor* t : {&*emb_wte, &*emb_wpe})
+      TORCH_CHECK(t->scalar_type() == torch::kBFloat16 && t->dim() == 2 && t->is_contiguous() && t->size(1) == K &&
+                      reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "decode_gemv: bf16 contiguous wte / wpe [*, K]");
+    TORCH_CHECK(emb_pos->is_cuda() && emb_pos->scalar_type() == torch::kInt64 && emb_pos->numel() == 1, "decode_gemv: int64 pos [1]");
+    TORCH_CHECK(K <= 1024, "decode_gemv: LN mode needs K <= 1024");
+    TORCH_CHECK(gamma.has_value() && beta.has_value() && gamma->scalar_type() == torch::kFloat32 &&
+                    beta->scalar_type() == torch::kFloat32 && gamma->numel() == K && beta->numel() == K &&
+                    gamma->is_contiguous() && beta->is_contiguous(), "decode_gemv: fp32 gamma / beta [K]");
+    M = emb_idx->numel();
+    TORCH_CHECK(rout.has_value() && rout->defined() && rout->scalar_type() == torch::kFloat32 && rout->is_contiguous() &&
+                    rout->numel() == (int64_t)M * K, "decode_gemv: fp32 resid_out [M, K] for the embedding rows");
+    rop = rout->data_ptr<float>();
+    gp = gamma->data_ptr<float>();
+    bt = beta->data_ptr<float>();
+    eip = emb_idx->data_ptr<int64_t>();
+    ewp = reinterpret_cast<const bf16*>(emb_wte->data_ptr());
+    epp = reinterpret_cast<const bf16*>(emb_wpe->data_ptr());
+    eps_p = emb_pos->data_ptr<int64_t>();
+    eV = (int)emb_wte->size(0);
+    eP = (int)emb_wpe->size(0);
   } else {
     TORCH_CHECK(rin.has_value() && rin->defined() && rin->scalar_type() == torch::kFloat32 && rin->dim() == 2 &&
                     rin->is_contiguous() && rin->size(1) == K, "decode_gemv: fp32 contiguous resid_in [M, K]");
@@ -627,7 +671,8 @@ void decode_gemv(c10::optional<torch::Tensor> x, c10::optional<torch::Tensor> ri
     constexpr int MM = decltype(mt)::value, RR = decltype(rpt)::value, CC = decltype(cplt)::value;
     constexpr int LL = decltype(lnt)::value ? 1 : 0;
     hipLaunchKernelGGL((decode_gemv_kernel<MM, LL, RR, CC>), grid, dim3(64), 0, stream, rp, dp, dbp, rop, gp, bt,
-                       (float)eps, xp, x_rs, wp, bp, op, o_rs, N, K, (int)act);
+                       (float)eps, xp, x_rs, wp, bp, op, o_rs, N, K, (int)act, 0, 0, (const float*)nullptr,
+                       (const float*)nullptr, eip, ewp, epp, eps_p, eV, eP);
   };
   auto by_cpl = [&](auto mt, auto lnt, auto rpt) {
     using I = std::integral_constant<int, 0>;

@@ -202,6 +202,13 @@ class GPTDecodeProgram:
         """idx [rows, 1] -> logits [rows, V] (bf16); appends this step's K/V at cache.pos_t."""
         sp = self.spec
         rows, C, H, D = idx.shape[0], sp.C, sp.H, sp.D
+        if (rows == 1 and self._gemv_ok(rows) and sp.wte.weight.dtype == torch.bfloat16
+                and sp.wpe.weight.dtype == torch.bfloat16):
+            # the first block's LN + QKV GEMV reads the embedding row itself (no embedding kernel):
+            # B = 1 0.3548 / 0.3564 -> 0.3520 / 0.3544 ms; at 4 rows every workgroup's four-row
+            # gather cost more than the launch it saves (0.535 -> 0.551), profiles/decode_r5.md
+            x = torch.empty(rows, C, dtype=torch.float32, device=idx.device)
+            return self._forward_gemv(x, torch.empty_like(x), rows, cache, emb=(idx.reshape(-1).contiguous(), cache.pos_t))
         x = fused_ops.embedding_fwd(idx, sp.wte.weight, sp.wpe.weight, 0, pos_dev=cache.pos_t)  # fp32 [rows, C]
         if self._batched_ok(rows):
             return self._forward_batched(x, rows, cache)
@@ -270,10 +277,12 @@ class GPTDecodeProgram:
         return self._linear(y, sp.head)
 
 
-    def _forward_gemv(self, x: Tensor, x2: Tensor, rows: int, cache) -> Tensor:
+    def _forward_gemv(self, x: Tensor, x2: Tensor, rows: int, cache, emb=None) -> Tensor:
         """Batch 1-4, per block: [add + LN1 + QKV GEMV + bias] → decode attention (K/V append fused)
         → proj GEMV → [add + proj bias + LN2 + fc GEMV + bias + GELU] → fc2 GEMV; then the final
-        add + LN and the lm_head GEMV — every linear one decode_gemv launch."""
+        add + LN and the lm_head GEMV — every linear one decode_gemv launch. ``emb`` = (token ids,
+        device position): the first GEMV builds the residual rows wte[tok] + wpe[pos] itself and
+        writes them to ``x`` (one kernel less per token)."""
         sp = self.spec
         K = _ext.kernels()
         C, H, D = sp.C, sp.H, sp.D
@@ -283,7 +292,10 @@ class GPTDecodeProgram:
             w1, b1, e1, w2, b2, e2 = self.ln[l]
             pb, fb = self.out_bias[l]
             qkv = torch.empty(rows, 3 * C, dtype=torch.bfloat16, device=x.device)
-            if delta is None:
+            if delta is None and emb is not None:
+                K.decode_gemv(None, None, None, None, x, w1, b1, e1, blk.qkv.weight, blk.qkv.bias, qkv, 0,
+                              emb_idx=emb[0], emb_wte=sp.wte.weight, emb_wpe=sp.wpe.weight, emb_pos=emb[1])
+            elif delta is None:
                 K.decode_gemv(None, x, None, None, None, w1, b1, e1, blk.qkv.weight, blk.qkv.bias, qkv, 0)
             else:
                 K.decode_gemv(None, x, delta, dbias, x2, w1, b1, e1, blk.qkv.weight, blk.qkv.bias, qkv, 0)
