@@ -291,12 +291,20 @@ __global__ void __launch_bounds__(64) decode_gemv_kernel(
     const int64_t* __restrict__ eidx = nullptr, const bf16* __restrict__ ewte = nullptr,
     const bf16* __restrict__ ewpe = nullptr, const int64_t* __restrict__ epos = nullptr, int eV = 0, int eP = 0) {
   constexpr bool LN = PRO == 1;
+  // EPI 3 (PRO 0 only): the whole wave on each of its RP rows — lane l reads chunks l, l + 64, …
+  // — twice the workgroups of the half-wave form for the same rows per wave
+  constexpr bool WR = EPI == 3;
+  constexpr int CS = WR ? 64 : 32;  // lanes striding over a row's chunks
+  static_assert(!WR || PRO == 0, "wave-per-row mode reads a bf16 x");
   const int lane = threadIdx.x, h = lane >> 5, l32 = lane & 31;
+  const int cl = WR ? lane : l32;
   const int nc = K / 8;  // 16-B chunks per row
   const int n0 = blockIdx.x * (EPI == 0 ? 2 * RP : RP);
   const int npair = N / 2;  // modes 1 / 2: output pairs
   auto row_of = [&](int rp) -> int {  // this half's weight row for its rp-th row (pair)
-    if constexpr (EPI == 0) {
+    if constexpr (WR) {
+      return min(n0 + rp, N - 1);
+    } else if constexpr (EPI == 0) {
       return min(n0 + 2 * rp + h, N - 1);
     } else if constexpr (EPI == 1) {
       return min(n0 + rp, npair - 1) + h * npair;
@@ -312,7 +320,7 @@ __global__ void __launch_bounds__(64) decode_gemv_kernel(
     const bf16* wr = w + (size_t)row_of(rp) * K;
 #pragma unroll
     for (int i = 0; i < CPL; ++i) {
-      const int c = l32 + 32 * i;
+      const int c = cl + CS * i;
       wv[rp][i] = c < nc ? *reinterpret_cast<const uint4*>(wr + 8 * c) : uint4{0u, 0u, 0u, 0u};
     }
   }
@@ -322,7 +330,7 @@ __global__ void __launch_bounds__(64) decode_gemv_kernel(
     for (int m = 0; m < M; ++m)
 #pragma unroll
       for (int i = 0; i < CPL; ++i) {
-        const int c = l32 + 32 * i;
+        const int c = cl + CS * i;
         xb[m][i] = c < nc ? *reinterpret_cast<const uint4*>(x + (size_t)m * x_rs + 8 * c) : uint4{0u, 0u, 0u, 0u};
       }
   } else {
@@ -433,10 +441,27 @@ __global__ void __launch_bounds__(64) decode_gemv_kernel(
       float a = 0.f;
 #pragma unroll
       for (int i = 0; i < CPL; ++i) a = dot8_bf16(wv[rp][i], xb[m][i], a);
-      acc[rp][m] = half_sum(a);
+      a = half_sum(a);
+      if constexpr (WR) a += __shfl_xor(a, 32, 64);
+      acc[rp][m] = a;
     }
   // 3. epilogue: lane 0 of each half stores its rows
-  if constexpr (EPI != 0) {
+  if constexpr (WR) {
+    if (lane != 0) return;
+#pragma unroll
+    for (int rp = 0; rp < RP; ++rp) {
+      const int n = n0 + rp;
+      if (n >= N) continue;
+      const float bv = bias ? bf2f(bias[n]) : 0.f;
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        float y = acc[rp][m] + bv;
+        if (act) y = gelu_f(bf2f(from_f<bf16>(y)), act - 1);
+        out[(size_t)m * o_rs + n] = from_f<bf16>(y);
+      }
+    }
+    return;
+  } else if constexpr (EPI != 0) {
     float other[RP][M];  // the partner half's sums (lane 0 <-> lane 32)
 #pragma unroll
     for (int rp = 0; rp < RP; ++rp)
@@ -662,7 +687,17 @@ void decode_gemv(c10::optional<torch::Tensor> x, c10::optional<torch::Tensor> ri
   if (rpw <= 0) rpw = N >= 16384 ? 8 : 2;
   TORCH_CHECK(rpw == 2 || rpw == 4 || rpw == 8, "decode_gemv: rows_per_wave 2, 4 or 8");
   const int RPv = rpw / 2;
-  const dim3 grid((N + rpw - 1) / rpw);
+  // wave-per-row form for the bf16-x GEMVs (proj, fc2, Gemma o / down): one row per wave, the
+  // whole wave striding over K — twice the workgroups. Same box: Gemma-3 1B B = 1 1.2626 / 1.2621 ->
+  // 1.2577 / 1.2555 ms, GPT-2 B = 4 0.549 / 0.544 -> 0.544 / 0.542, GPT-2 B = 1 even
+  // (profiles/decode_r5.md). PENROZ_DECODE_GEMV_WAVE_ROW=0: the half-wave form.
+  static const bool wave_row_env = [] {
+    const char* e = std::getenv("PENROZ_DECODE_GEMV_WAVE_ROW");
+    return !(e && e[0] == '0');
+  }();
+  const bool wave_row = wave_row_env && !ln && rows_per_wave <= 0 && N < 16384;
+  const int cpl64 = (K / 8 + 63) / 64;
+  const dim3 grid(wave_row ? N : (N + rpw - 1) / rpw);
   auto stream = at::hip::getCurrentHIPStream();
   auto wp = reinterpret_cast<const bf16*>(w.data_ptr());
   auto op = reinterpret_cast<bf16*>(out.data_ptr());
@@ -694,6 +729,19 @@ void decode_gemv(c10::optional<torch::Tensor> x, c10::optional<torch::Tensor> ri
     else by_cpl(mt, lnt, std::integral_constant<int, 4>{});
   };
   auto by_ln = [&](auto mt) {
+    if (wave_row) {  // one row per wave (RP = 1), chunks per lane over 64 lanes
+      auto go = [&](auto cplt) {
+        constexpr int MM = decltype(mt)::value, CC = decltype(cplt)::value;
+        hipLaunchKernelGGL((decode_gemv_kernel<MM, 0, 1, CC, 3>), grid, dim3(64), 0, stream, rp, dp, dbp, rop, gp, bt,
+                           (float)eps, xp, x_rs, wp, bp, op, o_rs, N, K, (int)act);
+      };
+      if (cpl64 <= 2) go(std::integral_constant<int, 2>{});
+      else if (cpl64 <= 4) go(std::integral_constant<int, 4>{});
+      else if (cpl64 <= 7) go(std::integral_constant<int, 7>{});
+      else if (cpl64 <= 16) go(std::integral_constant<int, 16>{});
+      else go(std::integral_constant<int, 16>{});  // K <= 8192 (checked above)
+      return;
+    }
     if (ln) {
       TORCH_CHECK(cpl <= 4, "decode_gemv: LN mode needs K <= 1024");
       // LN mode instantiates only the small chunk counts (K <= 1024)
