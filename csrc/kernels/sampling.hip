@@ -520,6 +520,7 @@ __global__ void __launch_bounds__(kRT) sample_reg_kernel(const T* __restrict__ l
 //   stage 2 (one workgroup per row): argmax merge; radix select over the candidates; the kept
 //     ones are ranked by token index (the draw order of the one-stage kernels), softmax(v/T),
 //     inverse-CDF draw with the row's uniform.
+constexpr int kMergeBatch = 8;  // sample_merge_kernel: candidate slots per thread loaded together
 constexpr int kPartN = 4096, kPartK = 64, kPartC = 128, kPartKeep = 1024, kPartMaxP = 64,
               kPartLds = kPartMaxP * kPartC;  // every part's candidates fit: none dropped in the merge
 
@@ -632,9 +633,11 @@ __global__ void __launch_bounds__(256) sample_merge_kernel(const SampleIO io, in
   extern __shared__ __attribute__((aligned(16))) uint32_t dyn_lds[];  // kPartLds keys + indices (64 KB)
   uint32_t* lkey = dyn_lds;
   int* lidx = reinterpret_cast<int*>(dyn_lds + kPartLds);
-  __shared__ int coff[256];
+  __shared__ int coff[256], ccnt[256];
   __shared__ int ctot;
   const int row = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  // this thread's part candidate count, fetched with the argmax operands (one memory round trip)
+  const int c_own = (cnt != nullptr && t < P) ? cnt[(size_t)row * P + t] : 0;
   float bm = -INFINITY;
   int bi = 0x7fffffff;
   for (int p = t; p < P; p += 256) {
@@ -660,10 +663,8 @@ __global__ void __launch_bounds__(256) sample_merge_kernel(const SampleIO io, in
   }
   __syncthreads();  // fred / ired are reused below
   // compact the valid candidates of all parts into LDS (part order), then work from there
-  const int* nr = cnt + (size_t)row * P;
-  int c = 0, incl = 0;
-  if (t < P) c = nr[t];
-  incl = c;
+  const int c = c_own;
+  int incl = c;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const int y = __shfl_up(incl, o, 64);
@@ -672,15 +673,35 @@ __global__ void __launch_bounds__(256) sample_merge_kernel(const SampleIO io, in
   if (lane == 63) ired[w] = incl;
   __syncthreads();
   for (int i = 0; i < w; ++i) incl += ired[i];
-  if (t < P) coff[t] = incl - c;
+  if (t < P) {
+    coff[t] = incl - c;
+    ccnt[t] = c;
+  }
   if (t == 255) ctot = min(incl, kPartLds);
   __syncthreads();
+  // all of a thread's candidate slots are read before any is kept (slots past a part's count
+  // hold stale values and are dropped): one memory round trip per kMergeBatch slots
   const int NCg = P * kPartC;
-  for (int f = t; f < NCg; f += 256) {
-    const int p = f / kPartC, j = f - p * kPartC;
-    if (j < nr[p] && coff[p] + j < kPartLds) {
-      lkey[coff[p] + j] = ckey[(size_t)row * NCg + f];
-      lidx[coff[p] + j] = cidx[(size_t)row * NCg + f];
+  for (int f0 = t; f0 < NCg; f0 += 256 * kMergeBatch) {
+    uint32_t kb[kMergeBatch];
+    int ib[kMergeBatch];
+#pragma unroll
+    for (int u = 0; u < kMergeBatch; ++u) {
+      const int f = f0 + 256 * u;
+      if (f < NCg) {
+        kb[u] = ckey[(size_t)row * NCg + f];
+        ib[u] = cidx[(size_t)row * NCg + f];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kMergeBatch; ++u) {
+      const int f = f0 + 256 * u;
+      if (f >= NCg) break;
+      const int p = f / kPartC, j = f - p * kPartC;
+      if (j < ccnt[p] && coff[p] + j < kPartLds) {
+        lkey[coff[p] + j] = kb[u];
+        lidx[coff[p] + j] = ib[u];
+      }
     }
   }
   const int NC = ctot;
