@@ -648,8 +648,11 @@ torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c
   }();
   const int G0 = H / Hkv;
   // (GQA or wide heads only: at G = 1, D = 64 — GPT-2 batch 1 — the general kernel is ~1 µs faster
-  // per layer, profiles/decode_r5.md)
-  if (!quant && q.scalar_type() == torch::kBFloat16 && Tq == 1 && items <= small_items && (G0 >= 2 || D >= 128 || small_any) &&
+  // per layer, profiles/decode_r5.md). It runs ONE workgroup per (batch, KV head) over the whole
+  // cache, so it only takes contexts the general kernel would not split either (S <= split_keys,
+  // S = the capacity under graph capture); longer contexts keep the key-split grid
+  if (!quant && q.scalar_type() == torch::kBFloat16 && Tq == 1 && items <= small_items && splits == 1 &&
+      (G0 >= 2 || D >= 128 || small_any) &&
       (G0 == 1 || G0 == 2 || G0 == 4 || G0 == 8 || G0 == 16) && (D == 64 || D == 128 || D == 256 || D == 512) &&
       G0 * D <= 4096 && (!fuse || kv_rs % 8 == 0)) {
     const bf16* qp = reinterpret_cast<const bf16*>(q.data_ptr());

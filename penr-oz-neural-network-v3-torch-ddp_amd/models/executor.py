@@ -309,6 +309,10 @@ class GPTExecutor:
 
     def refresh_shadow(self):
         self.shadow.copy_(self.flat)
+        # a shadow rebuilt outside the fused optimizer (a new session, weights loaded) makes every
+        # transposed dgrad copy stale, including those rebuilt after the last segment AdamW pass
+        if getattr(self, "_t_fresh", None):
+            self._t_fresh.clear()
 
     # ---- transposed bf16 weight copies for the data-gradient GEMMs ----------------------------
     # dx = dy·W with W [out, in] as stored reaches 0.94-1.32 PF on hipBLASLt at GPT-2 shapes; with

@@ -83,6 +83,9 @@ BATCHED_BLOCK = os.environ.get("PENROZ_DECODE_BATCHED", "1") != "0"
 # (csrc/kernels/decode_linear.hip decode_gemv: one memory round trip, no LDS, no barrier, no
 # split-K hand-off); "0": decode_ln_linear + skinny GEMMs
 GEMV_MAX_ROWS = int(os.environ.get("PENROZ_DECODE_GEMV_MAX_ROWS", "4"))
+# decode_gemv's reduction limit (256 lanes × 32 values, decode_linear.hip); wider linears take the
+# skinny GEMM
+GEMV_MAX_K = 8192
 # the sampler's last row advances the step counters itself (sample_step with adv_a / adv_b / done:
 # one launch less per token); "0": the separate decode_advance kernel
 FUSED_ADVANCE = os.environ.get("PENROZ_DECODE_FUSED_ADVANCE", "1") != "0"
@@ -428,7 +431,10 @@ class GemmaDecodeProgram:
         """Batch 1-4: every projection as one decode GEMV (decode_gemv / decode_gemv_pair:
         one wave per workgroup, one memory round trip; RoPE and the gated activation in the
         paired-row epilogues)."""
-        return 1 <= rows <= min(4, GEMV_MAX_ROWS) and C % 8 == 0 and C <= 1792 and _ext.available()
+        # decode_gemv reads K <= 8192 (decode_linear.hip); the O and down projections read K = H·D
+        # and the intermediate size (12288 on Gemma-4 e2b's KV-shared double-wide MLPs)
+        return (1 <= rows <= min(4, GEMV_MAX_ROWS) and C % 8 == 0 and C <= 1792 and _ext.available()
+                and all(b["o"].shape[1] <= GEMV_MAX_K and b["down"].shape[1] <= GEMV_MAX_K for b in self.blocks))
 
     def forward(self, idx: Tensor, cache) -> Tensor:
         """idx [rows, 1] -> logits [rows, V] (bf16); appends this step's K/V at cache.pos_t."""
@@ -437,7 +443,7 @@ class GemmaDecodeProgram:
         gemv = self._gemv_ok(rows, self.emb.embedding_dim)
 
         def lin(x: Tensor, w: Tensor) -> Tensor:
-            if gemv and w.shape[1] % 8 == 0:
+            if gemv and w.shape[1] % 8 == 0 and w.shape[1] <= GEMV_MAX_K:
                 out = torch.empty(rows, w.shape[0], device=x.device, dtype=torch.bfloat16)
                 K.decode_gemv(x.contiguous(), None, None, None, None, None, None, 0.0, w, None, out, 0)
                 return out

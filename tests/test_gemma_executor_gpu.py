@@ -356,3 +356,36 @@ def test_capture_returns_activation_and_gradient_pairs():
     for act, grad in pairs:
         assert act.shape[:2] == (2, 32) and act.shape == grad.shape
         assert torch.isfinite(act).all() and torch.isfinite(grad).all()
+
+
+def test_new_session_after_segment_transposes_uses_fresh_weights(monkeypatch):
+    """the transposed dgrad copies rebuilt after each segment's AdamW pass are marked
+    fresh; a new session that rebuilds the shadow from other weights (loaded after training) must
+    rebuild them too, or its first step's data gradients use the old weights. Gradients of the
+    first step after the reload == an executor without transposed copies (PENROZ_DGRAD_T=0)."""
+    from penroz.models.model import _FusedRunner
+    m = _gemma("gemma3_text", seed=6).to(DEV)
+    assert GemmaExecutor.SEGMENT_TRANSPOSE
+    _train(m, 2, True)
+    ex = m._get_executor(torch.device(DEV))
+    other = _gemma("gemma3_text", seed=7).to(DEV)
+    with torch.no_grad():
+        for p, q in zip(m.parameters(), other.parameters()):
+            p.data.copy_(q.data)  # fp32 parameters are views of the executor's flat masters
+    runner = _FusedRunner(m, torch.device(DEV), False)  # new session: shadow rebuilt from flat
+    assert runner.exec is ex
+    g = torch.Generator(device=DEV).manual_seed(8)
+    x = torch.randint(0, 512, (2, 64), device=DEV, generator=g)
+    y = torch.randint(0, 512, (2, 64), device=DEV, generator=g)
+    ex.zero_grad()
+    ex.train_micro_step(x, y, 1.0)
+    monkeypatch.setenv("PENROZ_DGRAD_T", "0")
+    ref = GemmaExecutor(other, torch.device(DEV))
+    ref.setup_training(False)
+    ref.zero_grad()
+    ref.train_micro_step(x, y, 1.0)
+    torch.cuda.synchronize()
+    for (n, p), (_, q) in zip(m.named_parameters(), other.named_parameters()):
+        a, b = ex.grad(p), ref.grad(q)
+        rel = ((a - b).norm() / (b.norm() + 1e-12)).item()
+        assert rel < 1e-2, f"{n}: rel grad err {rel}"

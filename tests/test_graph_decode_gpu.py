@@ -129,11 +129,12 @@ def test_decode_program_step_matches_module_step(rows):
     assert rel < 2e-2, rel
 
 
-def _gemma_model(head_dim, model_type="gemma3_text"):
+def _gemma_model(head_dim, model_type="gemma3_text", intermediate_size=128):
     """Tiny Gemma style model (RoPE, GQA 4:1, RMSNorm, gated MLP) from the HF config builder."""
     from types import SimpleNamespace
     tc = SimpleNamespace(vocab_size=256, hidden_size=64, num_attention_heads=4, num_key_value_heads=1,
-                         head_dim=head_dim, num_hidden_layers=2, intermediate_size=128, rms_norm_eps=1e-6,
+                         head_dim=head_dim, num_hidden_layers=2, intermediate_size=intermediate_size,
+                         rms_norm_eps=1e-6,
                          rope_theta=10000.0, attention_dropout=0.0, hidden_activation="gelu_pytorch_tanh",
                          model_type=model_type)
     torch.manual_seed(5)
@@ -176,6 +177,34 @@ def test_gemma_program_step_matches_module_step(model_type, rows):
             ref = acts[-1][:, -1, :].float()
             dec.cache.begin_step()
             got = dec.program.forward(tok, dec.cache).float()  # rewrites the same cache slot
+        finally:
+            dec.cache.graph_mode = False
+            dec.detach()
+    rel = (got - ref).norm() / ref.norm()
+    assert rel < 2e-2, rel
+
+
+@pytest.mark.parametrize("rows", [1, 3])
+def test_gemma_program_wide_mlp_falls_back_from_gemv(rows):
+    """An intermediate size above decode_gemv's K <= 8192 (Gemma-4 e2b's double-wide MLPs are
+    12288): the program must not take the GEMV path for the down projection."""
+    m = _gemma_model(64, intermediate_size=8192 + 256)
+    dec = gd.GraphDecoder(m, rows, 32, 0.0, None)
+    assert isinstance(dec.program, gd.GemmaDecodeProgram)
+    assert not dec.program._gemv_ok(rows, 64)
+    idx = torch.randint(0, 256, (rows, 7), device="cuda", generator=torch.Generator("cuda").manual_seed(3))
+    with torch.inference_mode():
+        dec.attach()
+        try:
+            m(idx[:, :6], skip_softmax=True)
+            tok = idx[:, 6:]
+            dec._set_state(tok, 6)
+            dec.cache.graph_mode = True
+            dec.cache.begin_step()
+            acts, _ = m(tok, skip_softmax=True)
+            ref = acts[-1][:, -1, :].float()
+            dec.cache.begin_step()
+            got = dec.program.forward(tok, dec.cache).float()
         finally:
             dec.cache.graph_mode = False
             dec.detach()
