@@ -182,6 +182,10 @@ def parse_args(argv=None):
     ap.add_argument("--via-runtime", action="store_true",
                     help="also time the same config through NeuralNetworkModel.train_model (Loader over synthetic "
                          "shards, per-epoch diagnostics, checkpoints) and report its tokensPerSec progress figure")
+    ap.add_argument("--data-ranks", type=int, default=1,
+                    help="single process only: each step's batch is the concatenation of the synthetic batches "
+                         "that ranks 0..N-1 of a --gpus N run would draw (with --batch B·N), so its losses and "
+                         "parameters must match that N-rank data-parallel run (rehearsal check)")
     ap.add_argument("--profile", default=None, metavar="DIR",
                     help="after the timed steps, profile 3 more under torch.profiler into DIR "
                          "(Chrome trace + per-kernel table); set PENROZ_ROCTX=1 for roctx phase ranges")
@@ -273,6 +277,8 @@ def _comm_info(runner, world: int) -> dict:
         info["rccl_version"] = ".".join(map(str, v)) if isinstance(v, tuple) else str(v)
     except Exception:  # no RCCL in this build
         info["rccl_version"] = None
+    if ex is not None and hasattr(ex, "opt_overlap_mode"):
+        info["optimizer_overlap"] = ex.opt_overlap_mode()
     if red is not None:
         sizes = [(e - s) * red.flat_grad.element_size() / 2**20 for s, e in red.buckets]
         info.update({"buckets": len(sizes), "bucket_mb": [round(x, 2) for x in sizes],
@@ -280,6 +286,14 @@ def _comm_info(runner, world: int) -> dict:
                      "transport": "native-rccl" if red._native is not None else red.backend,
                      "grad_mb": round(sum(sizes), 2)})
     return info
+
+
+def _reducer_of(runner):
+    ex = getattr(runner, "exec", None)
+    if ex is not None:
+        return ex.reducer
+    r = getattr(runner, "reducer", None)
+    return r.reducer if r is not None else None
 
 
 def _allreduce_probe(device, world: int, iters: int) -> dict:
@@ -533,8 +547,15 @@ def run_rank(args):
     if T > cfg["P"]:
         raise SystemExit(f"--seq {T} exceeds the {args.model} position table ({cfg['P']})")
     model, runner = _build(args, cfg, device, args.engine, world)
-    g = torch.Generator().manual_seed(rank)
-    pool = [torch.randint(0, V, (B, T + 1), generator=g) for _ in range(4)]
+    if args.data_ranks > 1:
+        if world > 1 or B % args.data_ranks:
+            raise SystemExit("--data-ranks N: one process, --batch a multiple of N")
+        gens = [torch.Generator().manual_seed(r) for r in range(args.data_ranks)]
+        b = B // args.data_ranks
+        pool = [torch.cat([torch.randint(0, V, (b, T + 1), generator=gr) for gr in gens]) for _ in range(4)]
+    else:
+        g = torch.Generator().manual_seed(rank)
+        pool = [torch.randint(0, V, (B, T + 1), generator=g) for _ in range(4)]
     if device.type == "cuda":
         pool = [p.pin_memory() for p in pool]
     step = _make_step(runner, pool, device)
@@ -553,6 +574,25 @@ def run_rank(args):
 
     comm = _comm_info(runner, world)
     comm.update(first_contact)
+    # the loss averaged over ranks (= the single-process loss of the concatenated batch) and a
+    # parameter checksum: what the multi-rank rehearsal tests compare against a --data-ranks run
+    gl = loss.detach().float().reshape(1).clone()
+    if world > 1:
+        gl = gl.to(device) if device.type == "cuda" else gl
+        dist.all_reduce(gl, op=dist.ReduceOp.SUM)
+        gl /= world
+        # every rank must have built the same gradient buckets (boundaries decide which
+        # elements each collective sums): gathered and compared, not assumed
+        red = _reducer_of(runner)
+        plan_b = [list(b) for b in red.buckets] if red is not None else None
+        plans = [None] * world
+        dist.all_gather_object(plans, plan_b)
+        if any(p_ != plan_b for p_ in plans):
+            raise SystemExit(f"bench.py: ranks built different gradient buckets: {plans}")
+        comm["bucket_plans_agree"] = world
+    global_loss = float(gl.item())
+    with torch.no_grad():
+        param_checksum = float(sum(p.detach().double().abs().sum() for p in model.parameters()))
     if world > 1 and args.nocomm_steps > 0:  # outside the timed region
         dt0, _ = _timed(_make_step(runner, pool, device, sync_grads=False), args.nocomm_steps, world, device)
         comm["ms_per_step_without_allreduce"] = dt0 / args.nocomm_steps * 1e3
@@ -606,7 +646,8 @@ def run_rank(args):
             "vs_reference_eager_same_gpu": (tok_s / ref_tok_s) if ref_tok_s else None,
             "reference_eager_tok_s": ref_tok_s,
             "mfu_bf16_dense": tok_s / world * flops_per_tok / 2.5e15 if device.type == "cuda" else None,
-            "final_loss": final_loss, "engine": args.engine, "device": args.device,
+            "final_loss": final_loss, "final_loss_global": global_loss, "param_checksum": param_checksum,
+            "engine": args.engine, "device": args.device,
             "dtype": "bf16" if device.type == "cuda" else "fp32",
             "data": "synthetic uniform tokens, random-init weights",
             "comm": comm,

@@ -100,6 +100,10 @@ void decode_gemv_pair(torch::Tensor x, torch::Tensor w, torch::Tensor out, int64
                       int64_t pairs_per_wave);
 void decode_gemm_acc(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> bias, torch::Tensor resid,
                      int64_t flags);
+// gemm_nt.hip
+bool gemm_nt_supported(int64_t M, int64_t N, int64_t K);
+void gemm_nt(torch::Tensor a, torch::Tensor b, c10::optional<torch::Tensor> bias, torch::Tensor out,
+             c10::optional<torch::Tensor> act, int64_t approx, int64_t group_m, int64_t grid, int64_t ablate);
 // gemm_wgrad.hip
 void wgrad_gemm(torch::Tensor dy, torch::Tensor x, torch::Tensor grad, int64_t tile, int64_t variant, bool accumulate);
 // flash_attn.hip
@@ -242,6 +246,11 @@ PYBIND11_MODULE(penroz_kernels, m) {
   m.def("decode_gemm_acc", &decode_gemm_acc, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("bias"),
         pybind11::arg("resid"), pybind11::arg("flags") = 0,
         "batched decode: resid += x·wᵀ + bias (fp32 residual, in place)");
+  m.def("gemm_nt_supported", &gemm_nt_supported, "shapes the native NT GEMM takes (M % 256, N % 128, K % 32, K >= 160)");
+  m.def("gemm_nt", &gemm_nt, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("bias"), pybind11::arg("out"),
+        pybind11::arg("act") = pybind11::none(), pybind11::arg("approx") = 0, pybind11::arg("group_m") = 0,
+        pybind11::arg("grid") = 0, pybind11::arg("ablate") = 0,
+        "out = a·bᵀ (+ bias) (bf16, both operands reduction-contiguous); with act: act = GELU(out)");
   m.def("wgrad_gemm", &wgrad_gemm, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("grad"),
         pybind11::arg("tile") = 256, pybind11::arg("variant") = 8, pybind11::arg("accumulate") = true,
         "grad (+)= dyᵀ·x (fp32 gradient, bf16 operands); accumulate=False overwrites grad");

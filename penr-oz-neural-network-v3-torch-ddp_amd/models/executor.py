@@ -379,7 +379,7 @@ class GPTExecutor:
         k = _ext.kernels()
         for key, ent in self._tw.items():
             off = self.offsets.get(key)
-            if off is not None and s <= off < e:
+            if off is not None and s <= off and off + ent[1].numel() <= e:  # the whole weight is final
                 k.transpose_bf16(self._tw_source(ent), ent[1])
                 self._t_fresh.add(key)
 
@@ -533,20 +533,40 @@ class GPTExecutor:
         self._forward(idx, training=False)
         return self._full_logits().view(idx.shape[0], idx.shape[1], -1)
 
+    # the last bucket (wpe + wte: 157 MB fp32 at GPT-2 124M, produced by the backward's final
+    # kernel) is cut into this many pieces so its all-reduce pipelines with the optimizer passes of
+    # the pieces already landed (PENROZ_TAIL_PIECES)
+    TAIL_PIECES = 4
+
     def setup_training(self, distributed: bool):
-        from penroz.parallel.reducer import GradReducer, plan_buckets, default_bucket_mb
+        from penroz.parallel.reducer import GradReducer, plan_buckets, default_bucket_mb, ready_map, split_last_bucket
+        import os
         import torch.distributed as dist
         self.refresh_shadow()
         self.reducer = None
         if distributed and dist.is_initialized() and dist.get_world_size() > 1:
             buckets = plan_buckets(self.segments, default_bucket_mb(dist.get_backend()) * 2**20)
+            buckets = split_last_bucket(buckets, int(os.environ.get("PENROZ_TAIL_PIECES", self.TAIL_PIECES)))
             self.reducer = GradReducer(self.flat_grad, buckets)
             self.reducer.broadcast_params(self.flat)
             self.refresh_shadow()
-            self._seg_bucket = [self.reducer.bucket_of(s) for s, _ in self.segments]
-            self._bucket_last_seg = {}
-            for i, bkt in enumerate(self._seg_bucket):
-                self._bucket_last_seg[bkt] = i
+            self._ready_at = ready_map(buckets, self.segments)
+
+    def _per_bucket_opt_ok(self) -> bool:
+        """World > 1: apply the fused AdamW to each gradient bucket inside the backward, on its own
+        stream, as soon as that bucket's all-reduce has landed (PENROZ_OPT_PER_BUCKET=1 forces it on
+        a host-blocking transport such as gloo, 0 disables it)."""
+        import os
+        env = os.environ.get("PENROZ_OPT_PER_BUCKET")
+        if env == "0" or self.device.type != "cuda" or not self._buckets_tile_flat():
+            return False
+        return env == "1" or self.reducer.stream_waits()
+
+    def opt_overlap_mode(self) -> str:
+        """How the optimizer step overlaps the backward (reported by bench.py in ``comm``)."""
+        if getattr(self, "_opt_mode", None):
+            return self._opt_mode
+        return "none"
 
     def end_training(self):
         if self.reducer is not None:
@@ -597,7 +617,7 @@ class GPTExecutor:
         self._zero_gaps = gaps
 
     def _segment_done(self, seg_index: int, sync: bool):
-        if self._opt_apply is not None and sync:
+        if self._opt_apply is not None and sync and self.reducer is None:
             # optimizer inside the backward: this segment's gradients are final once the side
             # stream (its weight gradients, deferred dγ / bias reductions) has caught up with the
             # main stream (its other gradients); nothing later in this backward reads its weights
@@ -614,18 +634,41 @@ class GPTExecutor:
             return
         if self.reducer is None or not sync:
             return
-        bkt = self._seg_bucket[seg_index]
-        if self._bucket_last_seg[bkt] == seg_index:
-            if getattr(self, "_side", None) is None:
-                self.reducer.bucket_ready(bkt)
-                return
+        ready = self._ready_at.get(seg_index, ())
+        if not ready:
+            return
+        if getattr(self, "_side", None) is None:
+            for i in ready:
+                self.reducer.bucket_ready(i)
+        else:
             # the bucket's weight gradients come from the side stream, its bias / LayerNorm
             # gradients from the main stream: launch the collective from the side stream after
             # it has caught up with the main stream
             main = torch.cuda.current_stream(self.device)
             with torch.cuda.stream(self._side):
                 self._side.wait_stream(main)
-                self.reducer.bucket_ready(bkt)
+                for i in ready:
+                    self.reducer.bucket_ready(i)
+        if self._opt_bucketed:
+            self._opt_buckets(ready)
+
+    def _opt_buckets(self, ids):
+        """Per-bucket optimizer (world > 1): on the optimizer stream, wait for each bucket's
+        all-reduce (a stream wait, not a host wait) and apply the fused AdamW to its range, then
+        rebuild the transposed dgrad copies of the weights wholly inside it (Gemma). Nothing later
+        in the backward reads the parameters of a finished segment; the main stream joins this
+        stream before the step returns (the next forward reads the new weights)."""
+        ost = getattr(self, "_opt_stream", None)
+        if ost is None:
+            ost = self._opt_stream = torch.cuda.Stream(device=self.device)
+        with torch.cuda.stream(ost):
+            for i in ids:
+                if i in self._opt_buckets_done:
+                    continue
+                s, e = self.reducer.wait_bucket(i)
+                self._opt_apply(s, e)
+                self._transpose_segment(s, e)
+                self._opt_buckets_done.add(i)
 
     # ---- weight gradients on a side HIP stream -------------------------------------------------
     # The weight-gradient GEMMs and the finishing kernels of every dγ / dβ / bias column reduction
@@ -756,9 +799,17 @@ class GPTExecutor:
         to do). ``PENROZ_OPT_IN_BWD=0`` keeps the separate step."""
         import os
         self._opt_apply = None
-        if (fuse_optimizer and sync and not capture and self.reducer is None and self._opt_flat
+        self._opt_bucketed = False
+        if (fuse_optimizer and sync and not capture and self._opt_flat
                 and os.environ.get("PENROZ_OPT_IN_BWD", "1") != "0"):
-            self._opt_apply = self.model.optimizer.begin_flat_ranges()
+            if self.reducer is None:
+                self._opt_apply = self.model.optimizer.begin_flat_ranges()
+                self._opt_mode = "per-segment-in-backward" if self._opt_apply is not None else None
+            elif self._per_bucket_opt_ok():
+                self._opt_apply = self.model.optimizer.begin_flat_ranges()
+                self._opt_bucketed = self._opt_apply is not None
+                self._opt_buckets_done = set()
+                self._opt_mode = "per-bucket-in-backward" if self._opt_bucketed else None
         hp = self._main_stream() if not capture else None
         try:
             if hp is None:
@@ -890,7 +941,11 @@ class GPTExecutor:
             # next, it updates each bucket's slice as soon as that bucket's all-reduce has landed
             # (optimizer_step), instead of waiting for all of them here.
             self.reducer.launch_remaining()
-            if self._overlap_opt and not cap and self.reducer.per_bucket_waits():
+            if self._opt_bucketed:  # every bucket's AdamW is queued on the optimizer stream
+                self._opt_buckets(range(len(self.reducer.buckets)))
+                torch.cuda.current_stream(self.device).wait_stream(self._opt_stream)
+                self.reducer.reset()
+            elif self._overlap_opt and not cap and self.reducer.per_bucket_waits():
                 self._reduce_pending = True
             else:
                 with trace_range("grad_allreduce.wait"):
@@ -923,6 +978,7 @@ class GPTExecutor:
                 ranges = [(lambda i=i: red.wait_bucket(i)) for i in range(len(red.buckets))]
                 if self._buckets_tile_flat() and self._opt_flat and opt.flat_step_ranges(ranges):
                     red.reset()
+                    self._opt_mode = "per-bucket-after-backward"
                     return
                 red.finish()
             opt.step()

@@ -368,7 +368,10 @@ class GemmaExecutor(GPTExecutor):
         app = self._opt_apply
         side = getattr(self, "_side", None)
         C = self.spec.C
+        # (world > 1: a row untouched here may be touched on another rank — the averaged table
+        # gradient is dense, so the per-bucket optimizer updates the table as a whole)
         if (app is None or not hasattr(app, "rows") or side is None or self._micro_since_zero != 1
+                or self.reducer is not None
                 or C % 4 or os.environ.get("PENROZ_EMB_ROW_ADAM", "1") == "0"):
             return
         es, ee = self.segments[self.L + 1]
@@ -562,7 +565,11 @@ class GemmaExecutor(GPTExecutor):
         self._join_side()
         if sync and self.reducer is not None:
             self.reducer.launch_remaining()
-            if self._overlap_opt and not cap and self.reducer.per_bucket_waits():
+            if self._opt_bucketed:  # every bucket's AdamW is queued on the optimizer stream
+                self._opt_buckets(range(len(self.reducer.buckets)))
+                torch.cuda.current_stream(self.device).wait_stream(self._opt_stream)
+                self.reducer.reset()
+            elif self._overlap_opt and not cap and self.reducer.per_bucket_waits():
                 self._reduce_pending = True
             else:
                 with trace_range("grad_allreduce.wait"):

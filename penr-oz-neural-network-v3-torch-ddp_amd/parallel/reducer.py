@@ -72,6 +72,30 @@ def plan_buckets(segments: list[tuple[int, int]], bucket_bytes: float, elem_size
     return buckets
 
 
+def split_last_bucket(buckets: list[tuple[int, int]], pieces: int, align: int = 64) -> list[tuple[int, int]]:
+    """The last bucket (the token / position embeddings, produced by the final kernel of the
+    backward, so its all-reduce cannot overlap anything) cut into ``pieces`` consecutive pieces
+    (boundaries on ``align``-element multiples): the pieces' all-reduces pipeline with the
+    optimizer passes of the pieces that have already landed."""
+    if pieces <= 1 or not buckets:
+        return list(buckets)
+    s, e = buckets[-1]
+    n = e - s
+    step = max(align, -(-(-(-n // pieces)) // align) * align)  # ceil(ceil(n / pieces) / align) · align
+    cuts = list(range(s, e, step)) + [e]
+    return list(buckets[:-1]) + [(a, b) for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
+
+
+def ready_map(buckets: list[tuple[int, int]], segments: list[tuple[int, int]]) -> dict[int, list[int]]:
+    """segment index -> the buckets whose last element lies in that segment (a bucket may be
+    all-reduced once the segment that completes it is done; every bucket appears once)."""
+    out: dict[int, list[int]] = {}
+    for i, (_, be) in enumerate(buckets):
+        seg = next(j for j, (s, e) in enumerate(segments) if s <= be - 1 < e)
+        out.setdefault(seg, []).append(i)
+    return out
+
+
 class GradReducer:
     def __init__(self, flat_grad: torch.Tensor, buckets: list[tuple[int, int]], group=None,
                  wire: str | None = None):
@@ -129,6 +153,12 @@ class GradReducer:
         """True when :meth:`wait_bucket` can wait for one bucket at a time (every bucket launched,
         in bucket order; c10d work objects or native RCCL completion events)."""
         return len(self._works) == len(self.buckets)
+
+    def stream_waits(self) -> bool:
+        """True when :meth:`wait_bucket` only makes the CURRENT STREAM wait (RCCL through c10d or
+        the native communicator), so the host can enqueue a bucket's optimizer pass right after
+        launching it; gloo waits block the host."""
+        return self.world > 1 and (self._native is not None or self.backend == "nccl")
 
     def wait_bucket(self, i: int) -> tuple[int, int]:
         """Current stream waits for bucket ``i``'s all-reduce (launch order = bucket order);

@@ -48,8 +48,11 @@ def _batch(rank):
 
 
 def _worker(rank, world, port, out, bucket_mb, overlap):
+    per_bucket = overlap == "per_bucket"
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK="0", PENROZ_BUCKET_MB=str(bucket_mb), PENROZ_OVERLAP_OPT=str(overlap))
+                      LOCAL_RANK="0", PENROZ_BUCKET_MB=str(bucket_mb),
+                      PENROZ_OVERLAP_OPT=str(1 if per_bucket else overlap),
+                      PENROZ_OPT_PER_BUCKET="1" if per_bucket else "0")
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import penroz.parallel.reducer as R
@@ -66,6 +69,20 @@ def _worker(rank, world, port, out, bucket_mb, overlap):
     assert ex.reducer is not None and len(ex.reducer.buckets) > 1
     x, y = _batch(rank)
     ex.zero_grad()
+    if per_bucket:
+        # the fused AdamW of each bucket runs inside the backward, on the optimizer stream, as soon
+        # as the bucket's all-reduce has landed; the embedding bucket is cut into pieces
+        assert len(ex.reducer.buckets) >= 4
+        ex.train_micro_step(x.to(dev), y.to(dev), 1.0, sync=True, fuse_optimizer=True)
+        assert ex.opt_overlap_mode() == "per-bucket-in-backward" and ex._opt_done
+        assert ex._opt_buckets_done == set(range(len(ex.reducer.buckets)))
+        ex.optimizer_step()  # nothing left to do
+        torch.cuda.synchronize()
+        torch.save(ex.flat_grad.cpu(), f"{out}/grad{rank}.pt")
+        torch.save(ex.flat.cpu(), f"{out}/param{rank}.pt")
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     ex.train_micro_step(x.to(dev), y.to(dev), 1.0, sync=True)
     assert ex._reduce_pending == bool(overlap)  # overlap: the last buckets are still reducing
     if rank == 0:  # the optimizer consumes the in-flight buckets one by one
@@ -82,7 +99,7 @@ def _worker(rank, world, port, out, bucket_mb, overlap):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("overlap", [0, 1])
+@pytest.mark.parametrize("overlap", [0, 1, "per_bucket"])
 def test_fused_executor_two_ranks_match_single_process(tmp_path, overlap):
     mp.spawn(_worker, args=(2, _port(), str(tmp_path), 0.05, overlap), nprocs=2, join=True)
     from penroz.models.executor import GPTExecutor

@@ -384,3 +384,44 @@ def test_gemm_table_guard_keeps_only_a_faster_table(monkeypatch):
     assert not r["table_kept"] and state["on"] is False
     monkeypatch.setattr(G, "_tuned_state", {})
     assert G.guard_tuned_gemms(lambda n: 1.0) == {}
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("world", [4, 8])
+def test_bench_multi_rank_cpu_matches_single_process(world):
+    """the data-parallel bench at 4 and 8 ranks (gloo on the CPU, tiny model).
+    Every rank agrees on the first-contact plan and builds the same gradient buckets, and the
+    rank-averaged loss and the parameters after the run equal one process training on the
+    concatenated batches (``--data-ranks``)."""
+    common = ["--device", "cpu", "--model", "tiny", "--steps", "3", "--warmup", "1", "--nocomm-steps", "0",
+              "--comm-probe-iters", "2"]
+    r = _run_bench(["--gpus", str(world)] + common, env_extra={"OMP_NUM_THREADS": "1"}, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == world and d["comm"]["nranks"] == world
+    assert d["comm"]["plan"]["agreed_ranks"] == world and d["comm"]["bucket_plans_agree"] == world
+    assert len(d["comm"]["devices"]) == world
+    s = _run_bench(["--gpus", "1", "--batch", str(4 * world), "--data-ranks", str(world)] + common,
+                   env_extra={"OMP_NUM_THREADS": "4"}, timeout=600)
+    assert s.returncode == 0, s.stderr[-3000:]
+    one = _json_line(s.stdout)
+    assert one["config"]["global_batch"] == d["config"]["global_batch"]
+    assert abs(d["final_loss_global"] - one["final_loss"]) <= 1e-4 * abs(one["final_loss"]), (d, one)
+    assert abs(d["param_checksum"] - one["param_checksum"]) <= 1e-4 * one["param_checksum"]
+
+
+def test_split_last_bucket_and_ready_map():
+    """The embedding bucket (produced by the backward's last kernel) is cut into pieces that all
+    become ready with the last segment; every bucket is launched exactly once."""
+    from penroz.parallel.reducer import plan_buckets, ready_map, split_last_bucket
+    segs = [(0, 1000), (1000, 1300), (1300, 1600), (1600, 1900), (1900, 6000)]
+    b = plan_buckets(segs, 600 * 4)
+    assert b == [(0, 1000), (1000, 1600), (1600, 6000)]
+    s4 = split_last_bucket(b, 4, align=64)
+    assert s4[:2] == b[:2] and s4[2][0] == 1600 and s4[-1][1] == 6000 and len(s4) == 2 + 4
+    assert all(x[1] == y[0] for x, y in zip(s4, s4[1:]))
+    assert all((e - s) % 64 == 0 for s, e in s4[2:-1])
+    rm = ready_map(s4, segs)
+    assert rm == {0: [0], 2: [1], 4: [2, 3, 4, 5]}
+    assert sorted(i for v in rm.values() for i in v) == list(range(len(s4)))
+    assert split_last_bucket(b, 1) == b
