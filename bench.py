@@ -146,7 +146,10 @@ def gemma_layer_shapes(cfg: dict) -> list[tuple[int, int, int]]:
             + ((2 * cfg["F"]) if i >= first_shared else cfg["F"],) for i, t in enumerate(g.layer_types)]
 
 
-def hf_gpt2_layers(V, C, L, H, P, pdrop=0.1):
+def hf_gpt2_layers(V, C, L, H, P, pdrop=None):
+    # PENROZ_BENCH_HF_PDROP: A/B of the import layout's dropout (HF gpt2: 0.1 at all three sites)
+    if pdrop is None:
+        pdrop = float(os.environ.get("PENROZ_BENCH_HF_PDROP", "0.1"))
     from types import SimpleNamespace
     from penroz.models import hf
     cfg = SimpleNamespace(vocab_size=V, n_embd=C, n_head=H, n_layer=L, n_positions=P, activation_function="gelu_new",

@@ -69,6 +69,7 @@ class RcclComm {
 
   ~RcclComm() {
     if (comm_) ncclCommDestroy(comm_);
+    comm_ = nullptr;
     for (auto e : events_) hipEventDestroy(e);
     for (auto e : done_) hipEventDestroy(e);
     if (stream_) hipStreamDestroy(stream_);
@@ -126,6 +127,15 @@ class RcclComm {
   }
 
   void synchronize() { HIP_OK(hipStreamSynchronize(stream_)); }
+
+  // tear the communicator down WITHOUT waiting for collectives in flight (a peer that never
+  // enqueued its side would leave them hanging forever); the object is unusable afterwards
+  void abort() {
+    if (comm_) ncclCommAbort(comm_);
+    comm_ = nullptr;
+    pending_ = 0;
+    n_done_ = 0;
+  }
   int rank() const { return rank_; }
   int world() const { return world_; }
   int channels() const { return channels_; }
@@ -200,6 +210,7 @@ PYBIND11_MODULE(penroz_comm, m) {
       .def("reset_handles", &RcclComm::reset_handles)
       .def("wait_all", &RcclComm::wait_all)
       .def("synchronize", &RcclComm::synchronize)
+      .def("abort", &RcclComm::abort)
       .def_property_readonly("rank", &RcclComm::rank)
       .def_property_readonly("world", &RcclComm::world)
       .def_property_readonly("channels", &RcclComm::channels)

@@ -273,7 +273,11 @@ class GPTExecutor:
         params = [p for seg in segs for p in seg]
         if len({id(p) for p in params}) != len(params) or len(params) != len(list(self.model.parameters())):
             raise ValueError("executor needs every parameter exactly once (no tying)")
-        total = sum(p.numel() for p in params)
+        # zero rows after the lm_head weight (V rounded up to HEAD_PAD): the head GEMMs run at the
+        # padded width (the logit rows are padded anyway), the pad rows stay zero (zero gradient,
+        # zero update) and the state_dict sees only the first V rows
+        pad = {id(self.spec.head.weight): self.head_pad_rows() * self.spec.C} if self.head_pad_rows() else {}
+        total = sum(p.numel() + pad.get(id(p), 0) for p in params)
         dev = self.device
         self.flat = torch.empty(total, dtype=torch.float32, device=dev)
         self.flat_grad = torch.zeros(total, dtype=torch.float32, device=dev)
@@ -296,6 +300,9 @@ class GPTExecutor:
                     p.grad = self.flat_grad[off:off + n].view_as(p)
                 self.offsets[id(p)] = off
                 off += n
+                if pad.get(id(p)):
+                    self.flat[off:off + pad[id(p)]].zero_()
+                    off += pad[id(p)]
             self.segments.append((start, off))
         self.params_in_order = params
         self.refresh_shadow()
@@ -306,6 +313,30 @@ class GPTExecutor:
             self._opt_flat = True
         else:
             self._opt_flat = False
+
+    # the lm_head weight's rows are padded to a multiple of this (HF GPT-2 V = 50257 -> 50304, the
+    # headline's width: hipBLASLt ran the 50257-wide lm_head forward 1.7 ms slower per step, and the
+    # transposed dgrad copy needs widths % 64; profiles/notes_r6.md). PENROZ_HEAD_PAD=0: off
+    HEAD_PAD = 128
+
+    def head_pad_rows(self) -> int:
+        import os
+        m = int(os.environ.get("PENROZ_HEAD_PAD", self.HEAD_PAD))
+        return (-self.spec.V) % m if m > 0 and self.device.type == "cuda" else 0
+
+    @property
+    def Vp(self) -> int:
+        """Rows of the padded lm_head weight (= logit columns the head GEMMs produce)."""
+        return self.spec.V + self.head_pad_rows()
+
+    def head_w(self) -> Tensor:
+        """The bf16 lm_head weight with its zero pad rows, [Vp, C]."""
+        off = self.offsets[id(self.spec.head.weight)]
+        return self.shadow[off:off + self.Vp * self.spec.C].view(self.Vp, self.spec.C)
+
+    def head_grad(self) -> Tensor:
+        off = self.offsets[id(self.spec.head.weight)]
+        return self.flat_grad[off:off + self.Vp * self.spec.C].view(self.Vp, self.spec.C)
 
     def refresh_shadow(self):
         self.shadow.copy_(self.flat)
@@ -330,13 +361,16 @@ class GPTExecutor:
             return
         s = self.spec
         lins = [s.head] + [l for b in s.blocks for l in (b.qkv, b.proj, b.fc, b.fc2)]
-        ws = [l.weight for l in lins if l.weight.shape[0] % 64 == 0 and l.weight.shape[1] % 64 == 0]
-        self.shadow_t = torch.empty(sum(w.numel() for w in ws), dtype=torch.bfloat16, device=self.device)
+        shape = {id(s.head.weight): (self.Vp, s.C)}  # the head's copy covers its pad rows
+        ws = [l.weight for l in lins]
+        ws = [w for w in ws if shape.get(id(w), w.shape)[0] % 64 == 0 and shape.get(id(w), w.shape)[1] % 64 == 0]
+        self.shadow_t = torch.empty(sum(math.prod(shape.get(id(w), w.shape)) for w in ws), dtype=torch.bfloat16,
+                                    device=self.device)
         off = 0
         for w in ws:
-            n = w.numel()
-            self._tw[id(w)] = (w, self.shadow_t[off:off + n].view(w.shape[1], w.shape[0]))
-            off += n
+            r, c = shape.get(id(w), w.shape)
+            self._tw[id(w)] = (w, self.shadow_t[off:off + r * c].view(c, r))
+            off += r * c
 
     def _refresh_transposed(self):
         if not self._tw:
@@ -364,7 +398,7 @@ class GPTExecutor:
             self._t_ready.record(side)
 
     def _tw_source(self, entry) -> Tensor:
-        return self.bf16(entry[0])
+        return self.head_w() if entry[0] is self.spec.head.weight else self.bf16(entry[0])
 
     # rebuild a segment's transposed copies right after its optimizer pass: Gemma-3 1B B=8 −0.2 to
     # −0.3 ms, Gemma-4 e2b −0.4 ms; GPT-2 +0.16 / +0.19 ms (its start-of-step transposes already
@@ -384,10 +418,11 @@ class GPTExecutor:
                 self._t_fresh.add(key)
 
     def _dgrad_w(self, w: Tensor) -> Tensor:
-        """The weight operand of dx = dy·W: the transposed copy (viewed back as [out, in]) or the shadow."""
+        """The weight operand of dx = dy·W: the transposed copy (viewed back as [out, in]) or the shadow
+        (the lm_head's with its pad rows)."""
         tw = self._tw.get(id(w)) if self._tw else None
         if tw is None:
-            return self.bf16(w)
+            return self.head_w() if w is self.spec.head.weight else self.bf16(w)
         if self._t_ready is not None:
             torch.cuda.current_stream(self.device).wait_event(self._t_ready)
             self._t_ready = None
@@ -430,7 +465,7 @@ class GPTExecutor:
         # training: two rotating [chunk, ld] buffers (lm_head → CE → dgrad/wgrad per token chunk);
         # the full [N, ld] logits only exist transiently for logits_for / diagnostics captures
         self.head_chunk = _head_chunk_rows(N, V)
-        self._head_bufs = [torch.empty(self.head_chunk, (V + 7) // 8 * 8, dtype=bf, device=dev)
+        self._head_bufs = [torch.empty(self.head_chunk, self._logit_ld(), dtype=bf, device=dev)
                            for _ in range(2 if self.head_chunk < N else 1)]
         self.tmp_c = torch.empty(N, C, dtype=bf, device=dev)
         self.dresid = torch.empty(N, C, dtype=f32, device=dev)
@@ -505,16 +540,23 @@ class GPTExecutor:
         norm_ops.add_ln_fwd(self.resid_mid[Lc - 1], self.tmp_c, self.resid[Lc], f(s.lnf.weight), f(s.lnf.bias),
                             s.lnf.eps, y=self.lnf_out, mean=meanf, rstd=rstdf, dropout_p=dp, dropout_seed=ds)
 
+    def _logit_ld(self) -> int:
+        """Row stride of the logits buffers: the padded head width, and a multiple of 8 elements
+        (16 B: the GEMMs take the stride, the CE kernel's 16-B chunks stay inside the row)."""
+        return (self.Vp + 7) // 8 * 8
+
     def _head_logits(self, r0: int, r1: int, buf: Tensor) -> Tensor:
-        """lm_head GEMM of token rows [r0, r1) into ``buf`` ([rows, ld]); returns the [rows, V] view."""
-        lg = buf[: r1 - r0, : self.spec.V]
-        torch.mm(self.lnf_out[r0:r1], self.bf16(self.spec.head.weight).t(), out=lg)
+        """lm_head GEMM of token rows [r0, r1) into ``buf`` ([rows, ld]); returns the [rows, Vp]
+        view (columns V..Vp-1 are the pad rows' exact zeros; slice [:, :V] for the logits)."""
+        lg = buf[: r1 - r0, : self.Vp]
+        torch.mm(self.lnf_out[r0:r1], self.head_w().t(), out=lg)
         return lg
 
-    def _full_logits(self) -> Tensor:
-        N, V = self.lnf_out.shape[0], self.spec.V
-        buf = torch.empty(N, (V + 7) // 8 * 8, dtype=torch.bfloat16, device=self.device)
-        return self._head_logits(0, N, buf)
+    def _full_logits(self, padded: bool = False) -> Tensor:
+        N = self.lnf_out.shape[0]
+        buf = torch.empty(N, self._logit_ld(), dtype=torch.bfloat16, device=self.device)
+        lg = self._head_logits(0, N, buf)
+        return lg if padded else lg[:, : self.spec.V]
 
     # ------------------------------------------------------------------ public API
     @torch.no_grad()
@@ -524,8 +566,8 @@ class GPTExecutor:
         total = torch.zeros((), dtype=torch.float32, device=self.device)
         for r0 in range(0, N, self.head_chunk):
             r1 = min(N, r0 + self.head_chunk)
-            total += fused_ops.cross_entropy_fwd_bwd(self._head_logits(r0, r1, self._head_bufs[0]), tg[r0:r1],
-                                                     0.0).sum()
+            total += fused_ops.cross_entropy_fwd_bwd(self._head_logits(r0, r1, self._head_bufs[0])[:, : self.spec.V],
+                                                     tg[r0:r1], 0.0).sum()
         return total / N
 
     @torch.no_grad()
@@ -859,10 +901,11 @@ class GPTExecutor:
         head_range.__enter__()
         self._defer_reductions(True)
         tg = targets.reshape(-1)
+        V = s.V
         if cap:  # diagnostics want the whole logits / dlogits tensors: one transient chunk
-            full = self._full_logits()
+            full = self._full_logits(padded=True)
             acts = [self.resid[0].view(B, T, C).clone()] * 2 + [r.view(B, T, C).clone() for r in self.resid[1:]] + \
-                   [self.lnf_out.view(B, T, C).float().clone(), full.view(B, T, -1).clone()]
+                   [self.lnf_out.view(B, T, C).float().clone(), full[:, :V].reshape(B, T, V).clone()]
             chunks = [(0, N, full)]
         else:
             chunks = [(r0, min(N, r0 + self.head_chunk), None) for r0 in range(0, N, self.head_chunk)]
@@ -871,9 +914,11 @@ class GPTExecutor:
         for i, (r0, r1, lg) in enumerate(chunks):
             if lg is None:  # the side stream may still be reading this buffer (wgrad two chunks back)
                 lg = self._head_logits(r0, r1, self._reuse(self._head_bufs[i % len(self._head_bufs)]))
-            loss += fused_ops.cross_entropy_fwd_bwd(lg, tg[r0:r1], scale / N).sum()
-            torch.mm(lg, w_dgrad, out=self.d_c[r0:r1])
-            self._wgrad(lg, self.lnf_out[r0:r1], s.head.weight)
+            # CE rewrites the V real columns with dlogits; the pad columns stay the exact zeros of
+            # the pad rows, so the padded dgrad / wgrad equal the unpadded ones (pad rows get 0)
+            loss += fused_ops.cross_entropy_fwd_bwd(lg[:, :V], tg[r0:r1], scale / N).sum()
+            torch.mm(lg[:, : w_dgrad.shape[0]], w_dgrad, out=self.d_c[r0:r1])
+            self._wgrad_into(id(s.head.weight), lg, self.lnf_out[r0:r1], self.head_grad())
         loss *= scale / N
         mean, rstd = self.statsf
         last = s.blocks[-1]
@@ -884,7 +929,7 @@ class GPTExecutor:
                         self.grad(last.fc2.bias), dropout_p=dp, dropout_seed=ds)
         grads_cap = []
         if cap:
-            grads_cap = [full.view(B, T, -1).clone(), self.d_c.view(B, T, C).float().clone(),
+            grads_cap = [full[:, :V].reshape(B, T, V).clone(), self.d_c.view(B, T, C).float().clone(),
                          self.dresid.view(B, T, C).clone()]
         self._segment_done(0, sync)
         head_range.__exit__(None, None, None)

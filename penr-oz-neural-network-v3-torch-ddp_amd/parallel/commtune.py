@@ -180,23 +180,36 @@ def _native_or_none(device, channels: int = 0, proto: str = "", algo: str = ""):
 
 def _probe_native(device, native, channels, proto, algo):
     """One small AVG all-reduce on a freshly built communicator before any timing: a forced
-    protocol / algorithm that RCCL cannot serve fails at ENQUEUE time, not at init. Every rank must
-    agree (MIN over the c10d group) or the arm is dropped on every rank."""
+    protocol / algorithm that RCCL cannot serve fails at ENQUEUE time, not at init. The ranks first
+    agree (MIN over the c10d group) that EVERY rank enqueued it — a rank whose enqueue failed leaves
+    its peers' collective hanging, so they abort the communicator instead of waiting on it
+     — then wait, check the average and agree again; a failed arm is dropped on every
+    rank."""
+    from penroz.parallel import rccl
+    arm = (f"native RCCL arm ({channels or 'default'} channels, protocol {proto or 'default'}, "
+           f"algorithm {algo or 'default'})")
+    enq = torch.zeros(1, device=device)
+    t = torch.full((4096,), float(dist.get_rank() + 1), device=device)
+    try:
+        native.all_reduce_avg_async(t)
+        enq += 1
+    except RuntimeError as e:
+        log.warning(f"{arm} failed to enqueue its probe all-reduce: {e}")
+    dist.all_reduce(enq, op=dist.ReduceOp.MIN)
+    if enq.item() == 0:
+        rccl.NativeComm.drop(channels=channels, proto=proto, algo=algo, abort=True)
+        return None
     ok = torch.zeros(1, device=device)
     try:
-        t = torch.full((4096,), float(dist.get_rank() + 1), device=device)
-        native.all_reduce_avg_async(t)
         native.wait_all()
         _sync(device)
         if bool((t == (dist.get_world_size() + 1) / 2.0).all()):
             ok += 1
     except RuntimeError as e:
-        log.warning(f"native RCCL arm ({channels or 'default'} channels, protocol {proto or 'default'}, "
-                    f"algorithm {algo or 'default'}) failed its probe all-reduce: {e}")
+        log.warning(f"{arm} failed its probe all-reduce: {e}")
     dist.all_reduce(ok, op=dist.ReduceOp.MIN)
     if ok.item() > 0:
         return native
-    from penroz.parallel import rccl
     rccl.NativeComm.drop(channels=channels, proto=proto, algo=algo)
     return None
 

@@ -93,9 +93,12 @@ class NativeComm:
             del cls._instances[k]
 
     @classmethod
-    def drop(cls, group=None, channels: int = 0, proto: str = "", algo: str = ""):
-        """Destroy the one communicator of this group with that (channels, protocol, algorithm)."""
-        cls._instances.pop((id(group), channels, proto, algo), None)
+    def drop(cls, group=None, channels: int = 0, proto: str = "", algo: str = "", abort: bool = False):
+        """Destroy the one communicator of this group with that (channels, protocol, algorithm);
+        ``abort``: ncclCommAbort first (a collective may be in flight that will never complete)."""
+        c = cls._instances.pop((id(group), channels, proto, algo), None)
+        if c is not None and abort:
+            c.abort()
 
     @property
     def nranks(self) -> int:
@@ -126,6 +129,10 @@ class NativeComm:
 
     def wait_all(self):
         self.comm.wait_all()
+
+    def abort(self):
+        """ncclCommAbort: drop the communicator without waiting for collectives in flight."""
+        self.comm.abort()
 
     def broadcast(self, t: torch.Tensor, root: int = 0):
         self.comm.broadcast(t, root)

@@ -176,3 +176,43 @@ def test_launcher_fault_marks_error(sandbox):
     assert code == launcher.FAULT_EXIT_CODE and failures == [(1, launcher.FAULT_EXIT_CODE)]
     st = NeuralNetworkModel.read_progress("flt")["status"]
     assert st["code"] == "Error" and "rank 1" in st["message"]
+
+
+class _FakeNative:
+    """Stands in for the native RCCL communicator in the probe: rank 1's enqueue fails."""
+
+    def __init__(self, rank, log):
+        self.rank, self.log = rank, log
+        self.enqueued = False
+
+    def all_reduce_avg_async(self, t):
+        if self.rank == 1:
+            raise RuntimeError("forced protocol refused at enqueue")
+        self.enqueued = True
+        return 0
+
+    def wait_all(self):
+        # the real communicator would hang here: rank 1 never enqueued its half
+        raise AssertionError("waited on a collective a peer never enqueued")
+
+
+def _probe_worker(rank, world, port, out):
+    _init(rank, world, port)
+    from penroz.parallel import commtune, rccl
+    calls = []
+    rccl.NativeComm.drop = classmethod(lambda cls, **kw: calls.append(kw))
+    fake = _FakeNative(rank, calls)
+    res = commtune._probe_native(torch.device("cpu"), fake, 0, "LL128", "")
+    torch.save({"res": res is None, "calls": calls, "enq": fake.enqueued}, f"{out}/p{rank}.pt")
+    dist.destroy_process_group()
+
+
+def test_native_probe_agrees_on_enqueue_before_waiting(tmp_path):
+    """when one rank's enqueue fails, no rank waits on the probe collective; every rank
+    drops the arm, aborting (not destroying) the communicator."""
+    mp.spawn(_probe_worker, args=(2, _port(), str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        d = torch.load(tmp_path / f"p{r}.pt")
+        assert d["res"], "the arm must be dropped on every rank"
+        assert d["calls"] == [{"channels": 0, "proto": "LL128", "algo": "", "abort": True}]
+    assert torch.load(tmp_path / "p0.pt")["enq"] and not torch.load(tmp_path / "p1.pt")["enq"]
