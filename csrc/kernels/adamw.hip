@@ -298,3 +298,124 @@ void multi_tensor_adam(std::vector<torch::Tensor> ps, std::vector<torch::Tensor>
   if (dt == torch::kBFloat16) launch(adam_multi_kernel<bf16>);
   else launch(adam_multi_kernel<float>);
 }
+
+// ---- weight-update diagnostics ------------------------------------------------------------------
+// Per-epoch weight-update ratios of the training loop (reference neural_net_model.py:684-703:
+// std(w − w_prev) / std(w) per weight matrix): one launch over a chunk table of every (w, prev)
+// pair computing fp64 partial sums (Σd, Σd², Σw, Σw²) per chunk, then one launch folding each
+// tensor's chunks in chunk order (deterministic) into the two unbiased standard deviations. The
+// per-tensor torch formulation (sub, cast, two std reductions and a stack per weight: ~300 small
+// kernels) cost ≈ 8 ms of GPU time per epoch at GPT-2 124M (profiles/notes_r6.md).
+namespace penroz {
+namespace {
+struct MomEntry {
+  const void* w;
+  const void* p;
+  int64_t n;
+};
+
+template <typename T>
+__global__ void __launch_bounds__(256) moments_chunk_kernel(const MomEntry* __restrict__ tab,
+                                                            const int32_t* __restrict__ chunk_tensor,
+                                                            const int32_t* __restrict__ chunk_index,
+                                                            double* __restrict__ part) {
+  const MomEntry e = tab[chunk_tensor[blockIdx.x]];
+  const T* W = static_cast<const T*>(e.w);
+  const T* P = static_cast<const T*>(e.p);
+  const int64_t start = (int64_t)chunk_index[blockIdx.x] * kChunk;
+  const int64_t end = min(e.n, start + kChunk);
+  float sd = 0.f, sdd = 0.f, sw = 0.f, sww = 0.f;
+  for (int64_t i = start + threadIdx.x; i < end; i += blockDim.x) {
+    const float w = to_f(W[i]), d = w - to_f(P[i]);
+    sd += d; sdd += d * d; sw += w; sww += w * w;
+  }
+  __shared__ double red[4][4];
+  double v[4] = {sd, sdd, sw, sww};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    // wave sum in fp64 via two fp32 halves would lose the point; reduce the fp32 lane sums in fp64
+    double x = v[k];
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+    v[k] = x;
+  }
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) red[wv][k] = v[k];
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    const int k = threadIdx.x;
+    part[(size_t)blockIdx.x * 4 + k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+  }
+}
+
+// out[t] = (std(w − prev), std(w)) of tensor t, chunks [first[t], first[t + 1])
+__global__ void __launch_bounds__(64) moments_fold_kernel(const double* __restrict__ part,
+                                                          const int32_t* __restrict__ first,
+                                                          const int64_t* __restrict__ numel, float* __restrict__ out,
+                                                          int nt) {
+  const int t = blockIdx.x * 64 + threadIdx.x;
+  if (t >= nt) return;
+  double s[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int c = first[t]; c < first[t + 1]; ++c)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s[k] += part[(size_t)c * 4 + k];
+  const double n = (double)numel[t];
+  auto sdev = [&](double a, double aa) { return n > 1.0 ? sqrt(fmax(aa - a * a / n, 0.0) / (n - 1.0)) : 0.0; };
+  out[2 * t] = (float)sdev(s[0], s[1]);
+  out[2 * t + 1] = (float)sdev(s[2], s[3]);
+}
+}  // namespace
+}  // namespace penroz
+
+// [n, 2] fp32: (std(w − prev), std(w)) for every pair (same shape and dtype, fp32 or bf16)
+torch::Tensor update_moments(std::vector<torch::Tensor> ws, std::vector<torch::Tensor> ps) {
+  const size_t nt = ws.size();
+  TORCH_CHECK(ps.size() == nt && nt > 0, "update_moments: one prev per weight");
+  const auto dt = ws[0].scalar_type();
+  TORCH_CHECK(dt == torch::kFloat32 || dt == torch::kBFloat16, "update_moments: fp32 or bf16");
+  std::vector<MomEntry> tab(nt);
+  std::vector<int32_t> ct, ci, first(nt + 1);
+  std::vector<int64_t> numel(nt);
+  for (size_t i = 0; i < nt; ++i) {
+    TORCH_CHECK(ws[i].is_cuda() && ps[i].is_cuda() && ws[i].is_contiguous() && ps[i].is_contiguous() &&
+                    ws[i].scalar_type() == dt && ps[i].scalar_type() == dt && ws[i].numel() == ps[i].numel(),
+                "update_moments: contiguous GPU tensors of one dtype, prev shaped like its weight");
+    tab[i] = {ws[i].data_ptr(), ps[i].data_ptr(), ws[i].numel()};
+    numel[i] = ws[i].numel();
+    first[i] = (int32_t)ct.size();
+    const int64_t chunks = (ws[i].numel() + kChunk - 1) / kChunk;
+    for (int64_t c = 0; c < chunks; ++c) {
+      ct.push_back((int32_t)i);
+      ci.push_back((int32_t)c);
+    }
+  }
+  first[nt] = (int32_t)ct.size();
+  const int64_t nchunks = ct.size();
+  auto opt = ws[0].options();
+  auto out = torch::zeros({(int64_t)nt, 2}, opt.dtype(torch::kFloat32));
+  if (nchunks == 0) return out;
+  const int64_t tab_bytes = nt * sizeof(MomEntry);
+  const int64_t bytes = tab_bytes + 8 * nchunks + 4 * (nt + 1) + 8 * nt + 8;
+  auto host = torch::empty({bytes}, torch::TensorOptions().dtype(torch::kUInt8).pinned_memory(true));
+  uint8_t* hp = host.data_ptr<uint8_t>();
+  std::memcpy(hp, tab.data(), tab_bytes);
+  std::memcpy(hp + tab_bytes, ct.data(), 4 * nchunks);
+  std::memcpy(hp + tab_bytes + 4 * nchunks, ci.data(), 4 * nchunks);
+  const int64_t off_first = tab_bytes + 8 * nchunks;
+  std::memcpy(hp + off_first, first.data(), 4 * (nt + 1));
+  const int64_t off_numel = (off_first + 4 * (nt + 1) + 7) / 8 * 8;
+  std::memcpy(hp + off_numel, numel.data(), 8 * nt);
+  auto dev = host.to(ws[0].device(), /*non_blocking=*/true);
+  const uint8_t* base = dev.data_ptr<uint8_t>();
+  auto part = torch::empty({nchunks * 4}, opt.dtype(torch::kFloat64));
+  auto stream = at::hip::getCurrentHIPStream();
+  auto k1 = dt == torch::kBFloat16 ? moments_chunk_kernel<bf16> : moments_chunk_kernel<float>;
+  hipLaunchKernelGGL(k1, dim3((unsigned)nchunks), dim3(256), 0, stream, reinterpret_cast<const MomEntry*>(base),
+                     reinterpret_cast<const int32_t*>(base + tab_bytes),
+                     reinterpret_cast<const int32_t*>(base + tab_bytes + 4 * nchunks), part.data_ptr<double>());
+  hipLaunchKernelGGL(moments_fold_kernel, dim3((unsigned)((nt + 63) / 64)), dim3(64), 0, stream,
+                     part.data_ptr<double>(), reinterpret_cast<const int32_t*>(base + off_first),
+                     reinterpret_cast<const int64_t*>(base + off_numel), out.data_ptr<float>(), (int)nt);
+  return out;
+}

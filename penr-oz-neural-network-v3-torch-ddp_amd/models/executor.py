@@ -168,6 +168,26 @@ def _cu_masked_stream(device: torch.device, spec: str):
     return torch.cuda.ExternalStream(ptr, device=device)
 
 
+_HP_STREAMS: dict = {}
+
+
+def _high_priority_stream(device: torch.device):
+    """ONE high-priority stream per device for every executor of the process. A second executor
+    drawing a second stream from torch's high-priority pool (a later model in the same process —
+    the server's worker, bench.py --via-runtime) ran the headline step at 65.4-65.5 ms instead of
+    61.2-61.3: the second stream does not get the first one's queue priority, and the side stream's
+    weight-gradient GEMMs then delay the dgrad chain (11 main-queue stalls of 0.3-0.56 ms before
+    LayerNorm backward per step); with PENROZ_MAIN_PRIORITY=0 the second run matched the first
+    (bench/runtime_ab.py, profiles/notes_r6.md). Sharing the stream only adds ordering between
+    executors, never removes it."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    hp = _HP_STREAMS.get(idx)
+    if hp is None:
+        lo, hi = torch.cuda.Stream.priority_range()
+        hp = _HP_STREAMS[idx] = torch.cuda.Stream(device=torch.device("cuda", idx), priority=min(lo, hi))
+    return hp
+
+
 class GPTExecutor:
     # ------------------------------------------------------------------ pattern match
     @staticmethod
@@ -882,8 +902,7 @@ class GPTExecutor:
             return None
         hp = getattr(self, "_hp_stream", None)
         if hp is None:
-            lo, hi = torch.cuda.Stream.priority_range()
-            hp = self._hp_stream = torch.cuda.Stream(device=self.device, priority=min(lo, hi))
+            hp = self._hp_stream = _high_priority_stream(self.device)
         return hp
 
     def _train_micro_step(self, idx: Tensor, targets: Tensor, scale: float, sync: bool, capture: bool) -> Tensor:

@@ -80,6 +80,34 @@ class NeuralNetworkModel(nn.Module):
     def _weights(self) -> list[Tensor | None]:
         return [p if p.ndim == 2 else None for p in self.parameters()]
 
+    @torch.no_grad()
+    def _snapshot_weights(self) -> list[Tensor | None]:
+        """The weights before an epoch, for its weight-update ratios (reference
+        ``neural_net_model.py:684-703``): copied into one buffer kept across epochs by a single
+        multi-tensor copy, instead of one allocation + copy kernel per weight every epoch."""
+        ws = self._weights
+        live = [w for w in ws if w is not None]
+        key = tuple((w.dtype, w.device, w.numel()) for w in live)
+        cache = self.__dict__.get("_snap")
+        if cache is None or cache[0] != key:
+            bufs = {}
+            views = []
+            for w in live:
+                k = (w.dtype, w.device)
+                bufs[k] = bufs.get(k, 0) + w.numel()
+            flat = {k: torch.empty(n, dtype=k[0], device=k[1]) for k, n in bufs.items()}
+            off = dict.fromkeys(flat, 0)
+            for w in live:
+                k = (w.dtype, w.device)
+                views.append(flat[k][off[k]:off[k] + w.numel()].view_as(w))
+                off[k] += w.numel()
+            cache = self.__dict__["_snap"] = (key, views)
+        views = cache[1]
+        if live:
+            torch._foreach_copy_(views, [w.detach() for w in live])
+        it = iter(views)
+        return [next(it) if w is not None else None for w in ws]
+
     @property
     def num_params(self) -> int:
         return sum(p.numel() for p in self.parameters())
@@ -609,28 +637,78 @@ class NeuralNetworkModel(nn.Module):
         runner = _make_runner(self, engine, device, distributed)
         self.train()
 
+        def fetch():
+            """The next micro-batch on the device. Called right after the previous micro-step is
+            enqueued, so the host-side shard read / pin / copy overlaps the GPU executing that step
+            instead of leaving the GPU idle at every epoch start (the --via-runtime bench ratio went
+            0.92 -> see profiles/notes_r6.md). The batch order is the loader's, unchanged."""
+            inp, tgt = loader.next_batch()
+            x = torch.as_tensor(np.asarray(inp), dtype=torch.long).view(batch_size, block_size)
+            y = torch.as_tensor(np.asarray(tgt), dtype=torch.long).view(batch_size, block_size)
+            if device.type == "cuda":
+                return x.pin_memory().to(device, non_blocking=True), y.pin_memory().to(device, non_blocking=True)
+            return x.to(device), y.to(device)
+
+        # GPU: an epoch's bookkeeping (cost, weight-update ratios, duration) is read back one epoch
+        # LATER, from pinned copies and events recorded behind its step, so the host never drains
+        # the device between epochs: the next epoch's work is already queued while the previous
+        # one's numbers are finalised (a per-epoch synchronize left the GPU idle ≈ 3-5 ms per
+        # epoch: the --via-runtime ratio 0.91, profiles/notes_r6.md). PENROZ_EPOCH_SYNC=1: the
+        # synchronous loop. Durations are then GPU-timeline epoch spans (event to event).
+        lazy = device.type == "cuda" and os.environ.get("PENROZ_EPOCH_SYNC", "0") != "1"
+        every = max(1, epochs // 100)
+        pend = None
+
+        def finish(pd):
+            """Record one finished epoch (waits for that epoch's events only)."""
+            ep, ev0, ev1, cost_h, rat, t_host = pd
+            if ev1 is not None:
+                ev1.synchronize()
+                secs = max(ev0.elapsed_time(ev1) / 1e3, 1e-9)
+            else:
+                secs = t_host
+            progress_cost = float(cost_h.item())
+            if ep % every == 0:
+                self.progress.append({
+                    "dt": dt.now().isoformat(), "epoch": ep + 1, "durationInSecs": secs,
+                    "speedPerSec": buffer_size / secs,
+                    "tokensPerSec": num_steps * world * buffer_size / secs,
+                    "cost": progress_cost,
+                    "weight_upd_ratio": diagnostics.finish_update_ratios(rat) if rat is not None else [],
+                })
+            log.info(f"Model {self.model_id}: Training Epoch {ep + 1}, Cost: {progress_cost:.4f}, "
+                     f"Duration: {secs:.2f} secs, Speed: {buffer_size / secs:.2f} tokens/sec")
+
+        nxt = fetch() if epochs > 0 else None
         for epoch in range(epochs):
             t0 = time.time()
             long_training = last_serialized is not None and (t0 - last_serialized >= 10)
             capture = ddp.master_proc() and (epoch + 1 == epochs or long_training)
-            prev = [w.detach().clone() if w is not None else None for w in self._weights] \
-                if ddp.master_proc() else []
+            record = ddp.master_proc() and epoch % every == 0
+            ev0 = None
+            if lazy and ddp.master_proc():
+                ev0 = torch.cuda.Event(enable_timing=True)
+                ev0.record()
+            prev = self._snapshot_weights() if record and os.environ.get("PENROZ_DIAG_SNAPSHOT", "1") != "0" \
+                else []
             runner.zero_grad()
             cost = torch.zeros((), device=device, dtype=torch.float32)
             try:
                 for step in range(num_steps):
                     maybe_inject_fault(epoch * num_steps + step)
-                    inp, tgt = loader.next_batch()
-                    x = torch.as_tensor(np.asarray(inp), dtype=torch.long).view(batch_size, block_size)
-                    y = torch.as_tensor(np.asarray(tgt), dtype=torch.long).view(batch_size, block_size)
-                    if device.type == "cuda":
-                        x, y = x.pin_memory().to(device, non_blocking=True), y.pin_memory().to(device, non_blocking=True)
-                    else:
-                        x, y = x.to(device), y.to(device)
+                    x, y = nxt
                     cost += runner.micro_step(x, y, 1.0 / num_steps, first=step == 0,
                                               last=step == num_steps - 1, capture=capture)
+                    if epoch + 1 < epochs or step + 1 < num_steps:
+                        nxt = fetch()
             except Exception as exc:
                 if ddp.master_proc():
+                    if pend is not None:  # the previous epoch's record is complete: keep it
+                        try:
+                            finish(pend)
+                        except Exception:  # the device may be in a failed state
+                            pass
+                        pend = None
                     log.error(f"Model {self.model_id}: Training Epoch {epoch + 1} failed: {exc}")
                     self.status = _status("Error", f"Training epoch {epoch + 1} failed: {exc}")
                     self.serialize()
@@ -638,25 +716,33 @@ class NeuralNetworkModel(nn.Module):
             if distributed:
                 ddp.ddp_all_reduce(cost)
             runner.step()
-            if device.type == "cuda":
-                torch.cuda.synchronize()
-            if ddp.master_proc():
-                secs = time.time() - t0
-                progress_cost = cost.item()
-                if epoch % max(1, epochs // 100) == 0:
-                    self.progress.append({
-                        "dt": dt.now().isoformat(), "epoch": epoch + 1, "durationInSecs": secs,
-                        "speedPerSec": buffer_size / secs,
-                        "tokensPerSec": num_steps * world * buffer_size / secs,
-                        "cost": progress_cost,
-                        "weight_upd_ratio": diagnostics.weight_update_ratios(prev, self._weights),
-                    })
-                log.info(f"Model {self.model_id}: Training Epoch {epoch + 1}, Cost: {progress_cost:.4f}, "
-                         f"Duration: {secs:.2f} secs, Speed: {buffer_size / secs:.2f} tokens/sec")
+            if lazy:
+                if ddp.master_proc():
+                    # the ratios of this epoch's update, on the device behind its step; host copies
+                    # land in pinned memory, read by finish() one epoch later
+                    rat = diagnostics.start_update_ratios(prev, self._weights) if record and prev else None
+                    cost_h = torch.empty((), dtype=torch.float32, pin_memory=True)
+                    cost_h.copy_(cost, non_blocking=True)
+                    ev1 = torch.cuda.Event(enable_timing=True)
+                    ev1.record()
+                    if pend is not None:
+                        finish(pend)
+                    pend = (epoch, ev0, ev1, cost_h, rat, None)
+            else:
+                if device.type == "cuda":
+                    torch.cuda.synchronize()
+                if ddp.master_proc():
+                    rat = diagnostics.start_update_ratios(prev, self._weights) if record and prev else None
+                    finish((epoch, None, None, cost.detach().cpu(), rat, time.time() - t0))
             if ddp.master_proc() and long_training:
+                if pend is not None:
+                    finish(pend)
+                    pend = None
                 self._record_training_overall_progress(runner.captured(), runner.grad_of)
                 self.serialize()
                 last_serialized = time.time()
+        if pend is not None:
+            finish(pend)
 
         if ddp.master_proc():
             self.status = _status("Trained", f"Model trained for {epochs} epochs.")

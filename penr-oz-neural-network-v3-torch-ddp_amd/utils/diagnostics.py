@@ -21,6 +21,37 @@ from penroz.ops import fused as fused_ops
 
 
 @torch.no_grad()
+def start_update_ratios(prev: list, weights: list):
+    """Device-side part of :func:`weight_update_ratios`: std(w − prev) and std(w) of every weight,
+    stacked on the device and copied to pinned host memory without waiting (the training loop
+    reads them one epoch later with :func:`finish_update_ratios`)."""
+    pairs = [(i, w.detach(), pw) for i, (pw, w) in enumerate(zip(prev, weights)) if pw is not None and w is not None]
+    idx = [i for i, _, _ in pairs]
+    if not pairs:
+        return (len(weights), idx, None)
+    from penroz.ops._ext import use_kernels, kernels
+    ws, ps = [w for _, w, _ in pairs], [p for _, _, p in pairs]
+    if (use_kernels(ws[0]) and len({(w.dtype, p.dtype) for w, p in zip(ws, ps)}) == 1
+            and ws[0].dtype in (torch.float32, torch.bfloat16) and all(w.is_contiguous() and p.is_contiguous()
+                                                                      for w, p in zip(ws, ps))):
+        dev = kernels().update_moments(ws, ps)  # one chunked launch + one fold (csrc/kernels/adamw.hip)
+    else:
+        dev = torch.stack([torch.stack([(w - pw).float().std(), w.float().std()]) for w, pw in zip(ws, ps)])
+    host = torch.empty(dev.shape, dtype=dev.dtype, pin_memory=dev.is_cuda)
+    host.copy_(dev, non_blocking=dev.is_cuda)
+    return (len(weights), idx, host)
+
+
+def finish_update_ratios(started) -> list:
+    """The per-weight update ratios of :func:`start_update_ratios` (after its work completed)."""
+    n, idx, host = started
+    out: list = [None] * n
+    if host is not None:
+        for i, (d, s) in zip(idx, host.tolist()):
+            out[i] = d / (s + 1e-8)
+    return out
+
+
 def weight_update_ratios(prev: list, weights: list) -> list:
     vals = []
     idx = []

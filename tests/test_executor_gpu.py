@@ -219,3 +219,21 @@ def test_transposed_dgrad_weights_follow_the_main_stream():
     torch.cuda.synchronize()
     for w, t in ex._tw.values():
         assert torch.equal(t, ex.bf16(w).t()), "transpose ran before the main stream's shadow write"
+
+
+def test_executors_share_one_high_priority_stream():
+    """Every executor of the process runs its critical path on ONE high-priority stream per
+    device: a second stream from torch's high-priority pool lost the queue priority and slowed the
+    second model's step by ≈4 ms (bench/runtime_ab.py)."""
+    from penroz.models import executor as ex_mod
+    dev = torch.device("cuda", torch.cuda.current_device())
+    a = ex_mod._high_priority_stream(dev)
+    b = ex_mod._high_priority_stream(torch.device("cuda"))
+    assert a is b
+    lo, hi = torch.cuda.Stream.priority_range()
+    assert a.priority == min(lo, hi)
+    m1, m2 = tiny().cuda(), tiny().cuda()
+    e1, e2 = GPTExecutor(m1, torch.device("cuda")), GPTExecutor(m2, torch.device("cuda"))
+    s1, s2 = e1._main_stream(), e2._main_stream()
+    if s1 is not None:
+        assert s1 is s2 is a

@@ -51,7 +51,9 @@ def test_headline_shape_one_step_matches_fp32():
     for (n, p), (_, r) in zip(m.named_parameters(), ref.named_parameters()):
         rel = ((ex.grad(p) - r.grad).norm() / (r.grad.norm() + 1e-12)).item()
         worst = max(worst, rel)
-        assert rel < 5e-2, f"{n}: rel grad err {rel}"
+        # measured worst over all parameters: 0.0104 (round 6, profiles/bench_r6_configs_final.log);
+        # 2 % is that plus a margin — a regression to the former 5 % bound would now fail
+        assert rel < 2e-2, f"{n}: rel grad err {rel}"
     print(f"headline-shape parity: loss {loss.item():.5f} vs {loss_ref.item():.5f}, worst rel grad err {worst:.4f}")
 
 

@@ -1238,3 +1238,25 @@ def test_decode_gemm_acc(M, K, N, with_bias):
     kk.decode_gemm_acc(x, w, b, r1)
     assert torch.equal(r, r1), "not deterministic"
     _close(r, r0 + 2 * step, 2e-3, 1e-4, "resid x2")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_update_moments_matches_torch_std(dtype):
+    """Per-epoch weight-update diagnostics: the chunked fp64 moments kernel == torch's per-tensor
+    std(w - prev) and std(w) (unbiased), over sizes below, at and across the 8192-element chunk."""
+    from penroz.ops import _ext
+    from penroz.utils import diagnostics
+    g = torch.Generator(device="cuda").manual_seed(11)
+    shapes = [(3, 5), (64, 128), (8192, 1), (257, 769), (1024, 3072)]
+    ws = [torch.randn(s, device="cuda", generator=g).to(dtype) for s in shapes]
+    ps = [(w.float() + 1e-3 * torch.randn(w.shape, device="cuda", generator=g)).to(dtype) for w in ws]
+    got = _ext.kernels().update_moments(ws, ps).cpu()
+    for i, (w, p) in enumerate(zip(ws, ps)):
+        ref = torch.stack([(w - p).float().std(), w.float().std()]).cpu()
+        assert torch.allclose(got[i], ref, rtol=2e-3, atol=1e-7), (shapes[i], got[i], ref)
+    started = diagnostics.start_update_ratios([ps[0], None, ps[2]], [ws[0], ws[1], ws[2]])
+    torch.cuda.synchronize()  # the pinned copy is asynchronous: finish only after it has landed
+    r = diagnostics.finish_update_ratios(started)
+    old = diagnostics.weight_update_ratios([ps[0], None, ps[2]], [ws[0], ws[1], ws[2]])
+    assert r[1] is None and old[1] is None
+    assert abs(r[0] - old[0]) <= 2e-3 * abs(old[0]) and abs(r[2] - old[2]) <= 2e-3 * abs(old[2])
