@@ -20,6 +20,9 @@ ap.add_argument("--new", type=int, default=128)
 ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
 ap.add_argument("--turbo", action="store_true")
 ap.add_argument("--model", default="gpt2", choices=["gpt2", "gemma3-1b"])
+# the generation window (block_size): a context longer than it is cropped and re-prefilled every
+# token, so long-context rows need --block >= prompt + new
+ap.add_argument("--block", type=int, default=1024)
 a = ap.parse_args()
 if a.turbo:
     M.create_kv_cache = lambda n, cap=None: KV.TurboQuantKVCache(n, cap)
@@ -38,12 +41,12 @@ m = NeuralNetworkModel("dec", Mapper(layers, {"adamw": {"lr": 6e-4}})).to("cuda"
 if a.dtype == "bf16":
     m.to(dtype=torch.bfloat16)
 ctx = torch.randint(0, V, (a.batch, a.prompt)).tolist()
-m.generate_batch(ctx, 1024, 4, temperature=1.0, top_k=50)  # warmup
+m.generate_batch(ctx, a.block, 4, temperature=1.0, top_k=50)  # warmup
 torch.cuda.synchronize()
 t0 = time.perf_counter()
-out = m.generate_batch(ctx, 1024, a.new, temperature=1.0, top_k=50)
+out = m.generate_batch(ctx, a.block, a.new, temperature=1.0, top_k=50)
 torch.cuda.synchronize()
 dt = time.perf_counter() - t0
 print(json.dumps({"metric": "decode tokens/sec (all rows)", "value": a.batch * a.new / dt, "batch": a.batch,
-                  "prompt": a.prompt, "new_tokens": a.new, "ms_per_step": dt / a.new * 1e3, "dtype": a.dtype,
+                  "prompt": a.prompt, "new_tokens": a.new, "block": a.block, "ms_per_step": dt / a.new * 1e3, "dtype": a.dtype,
                   "kv_cache": "int8-turboquant" if a.turbo else a.dtype, "model": "gpt2-124m" if a.model == "gpt2" else "gemma3-1b-shape", "data": "random weights"}))

@@ -68,7 +68,8 @@ void decode_advance(torch::Tensor a, torch::Tensor b, torch::Tensor c);
 torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c10::optional<torch::Tensor> k_scale,
                           c10::optional<torch::Tensor> v_scale, int64_t S, int64_t q_offset, double scale,
                           c10::optional<torch::Tensor> seq_len_dev,
-                          c10::optional<torch::Tensor> k_new, c10::optional<torch::Tensor> v_new);
+                          c10::optional<torch::Tensor> k_new, c10::optional<torch::Tensor> v_new,
+                          c10::optional<torch::Tensor> counters);
 // elementwise.hip (deferred.h)
 void set_deferred_reduce_stream(int64_t stream, int64_t device);
 // decode_attn.hip
@@ -203,7 +204,7 @@ PYBIND11_MODULE(penroz_kernels, m) {
   m.def("decode_attn", &decode_attn, pybind11::arg("q"), pybind11::arg("kc"), pybind11::arg("vc"), pybind11::arg("k_scale"),
         pybind11::arg("v_scale"), pybind11::arg("S"), pybind11::arg("q_offset"), pybind11::arg("scale"),
         pybind11::arg("seq_len_dev") = pybind11::none(), pybind11::arg("k_new") = pybind11::none(),
-        pybind11::arg("v_new") = pybind11::none());
+        pybind11::arg("v_new") = pybind11::none(), pybind11::arg("counters") = pybind11::none());
   m.def("set_deferred_reduce_stream", &set_deferred_reduce_stream);
   m.def("kv_append", &kv_append, pybind11::arg("k"), pybind11::arg("v"), pybind11::arg("kc"), pybind11::arg("vc"),
         pybind11::arg("ks") = pybind11::none(), pybind11::arg("vs") = pybind11::none(),

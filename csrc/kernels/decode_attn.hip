@@ -14,7 +14,8 @@
 // int8 caches (TurboQuant) carry per-token fp32 scales that are folded into the score and
 // the P·V weight, so the int8 cache is never dequantised to memory.
 // The key groups merge through LDS; with several splits the partial (m, l, O) go to a workspace
-// and a second kernel combines them. Enough splits are used to put ≥ 512 workgroups in
+// and the last split workgroup of the item to arrive combines them (or, without arrival
+// counters, a second kernel). Enough splits are used to put ≥ 512 workgroups in
 // flight (256 CUs) even at batch 1.
 #include "common.h"
 #include <cstdlib>
@@ -25,6 +26,8 @@
 namespace penroz {
 
 constexpr int kMaxGroup = 16;
+constexpr int kMaxMergeSplits = 16;
+constexpr int64_t kMergeMaxKeys = 8192;
 
 template <typename TK> struct KRow;
 template <> struct KRow<bf16> {
@@ -98,7 +101,8 @@ __global__ void __launch_bounds__(256) decode_kernel(const TQ* __restrict__ q, c
                                                      int Tq, int H, int Hkv, int cap, int S, int q_offset,
                                                      int splits, float scale, const int64_t* __restrict__ S_dev,
                                                      int64_t q_rs, const TQ* __restrict__ k_new,
-                                                     const TQ* __restrict__ v_new, int64_t kv_rs) {
+                                                     const TQ* __restrict__ v_new, int64_t kv_rs,
+                                                     int* __restrict__ cnt, int min_keys) {
   constexpr int GMAX = GC ? GC : kMaxGroup;
   constexpr int RB = D * (int)sizeof(TK);                 // cache row bytes
   constexpr int KC = RB * 256 <= 32768 ? 256 : 32768 / RB;  // keys per chunk (V chunk <= 32 KB of LDS)
@@ -140,7 +144,13 @@ __global__ void __launch_bounds__(256) decode_kernel(const TQ* __restrict__ q, c
     q_offset = S - Tq;
   }
   const int kend_causal = min(S, q_offset + tq + 1);
-  const int per_split = (kend_causal + splits - 1) / splits;
+  // With the in-launch merge (cnt) the grid is sized for the capacity, but only the splits the
+  // actual context needs (>= min_keys keys each) run: a short context is one workgroup writing the
+  // output directly, the other split workgroups of the item leave at once (every workgroup of the
+  // item derives the same count from the device-side length).
+  const int nsplit = cnt != nullptr ? max(1, min(splits, (kend_causal + min_keys - 1) / min_keys)) : splits;
+  if (split >= nsplit) return;
+  const int per_split = (kend_causal + nsplit - 1) / nsplit;
   const int k0 = split * per_split, k1 = min(kend_causal, k0 + per_split);
   const size_t head_base = ((size_t)b * Hkv + g) * cap;
   const int kk = t / TPK, part = t % TPK;     // score phase: key kk of the chunk, pieces part*CPT..
@@ -331,7 +341,7 @@ __global__ void __launch_bounds__(256) decode_kernel(const TQ* __restrict__ q, c
     for (int x = 0; x < NG; ++x) O += ro[(x * GMAX + i) * D + d];
     const float Mi = fin[i][0], Li = fin[i][1];
     const int h = g * G + i;
-    if (splits == 1) {
+    if (nsplit == 1) {
       out[(((size_t)b * Tq + tq) * H + h) * D + d] = from_f<TQ>(Li > 0.f ? O / Li : 0.f);
     } else {
       const size_t r = (((size_t)split * B + b) * Tq + tq) * H + h;
@@ -341,6 +351,56 @@ __global__ void __launch_bounds__(256) decode_kernel(const TQ* __restrict__ q, c
         ws_ml[2 * r + 1] = Li;
       }
     }
+  }
+  if (nsplit == 1 || cnt == nullptr) return;
+  // In-launch merge: the last of the item's split workgroups to arrive combines all splits' (m, l, O)
+  // in split order — the same arithmetic, in the same order, as decode_combine_kernel (so the
+  // result does not depend on which workgroup arrives last), without a second launch. The counter
+  // is left at zero for the next launch (a replayed graph reuses it).
+  __syncthreads();
+  __shared__ int last;
+  const int item = blockIdx.x / splits;
+  if (t == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int prev = __hip_atomic_fetch_add(&cnt[item], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = prev == nsplit - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  if (t == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(&cnt[item], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  const int64_t rows = (int64_t)B * Tq * H;
+  for (int idx = t; idx < G * D; idx += 256) {
+    const int i = idx / D, d = idx % D;
+    const int64_t r = ((int64_t)b * Tq + tq) * H + g * G + i;
+    // every split's (m, l, o) loads issue together (one memory round trip, not 3 per split: the
+    // serial form cost ~0.1 ms per layer at 16 splits)
+    float mv[kMaxMergeSplits], lv[kMaxMergeSplits], ov[kMaxMergeSplits];
+#pragma unroll
+    for (int sp = 0; sp < kMaxMergeSplits; ++sp) {
+      const int64_t rr = sp * rows + r;
+      const bool on = sp < nsplit;
+      mv[sp] = on ? ws_ml[2 * rr] : -INFINITY;
+      lv[sp] = on ? ws_ml[2 * rr + 1] : 0.f;
+      ov[sp] = on ? ws_o[rr * D + d] : 0.f;
+    }
+    float Mx = -INFINITY;
+#pragma unroll
+    for (int sp = 0; sp < kMaxMergeSplits; ++sp) Mx = fmaxf(Mx, mv[sp]);
+    float Lx = 0.f, Ox = 0.f;
+#pragma unroll
+    for (int sp = 0; sp < kMaxMergeSplits; ++sp) {
+      if (sp >= nsplit) break;
+      const float f = mv[sp] == -INFINITY ? 0.f : __expf(mv[sp] - Mx);
+      Lx += lv[sp] * f;
+      Ox += ov[sp] * f;
+    }
+    out[r * D + d] = from_f<TQ>(Lx > 0.f ? Ox / Lx : 0.f);
   }
 }
 
@@ -585,7 +645,7 @@ using namespace penroz;
 torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c10::optional<torch::Tensor> k_scale,
                           c10::optional<torch::Tensor> v_scale, int64_t S, int64_t q_offset, double scale,
                           c10::optional<torch::Tensor> seq_len_dev, c10::optional<torch::Tensor> k_new,
-                          c10::optional<torch::Tensor> v_new) {
+                          c10::optional<torch::Tensor> v_new, c10::optional<torch::Tensor> counters) {
   TORCH_CHECK(q.is_cuda() && q.dim() == 4, "q must be [B, Tq, H, D]");
   // q may be a view into the fused QKV rows: unit dim stride, packed heads, uniform row stride
   // (a size-1 Tq dim may carry any stride: the row stride is then stride(0))
@@ -604,16 +664,34 @@ torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c
   auto out = torch::empty({B, Tq, H * D}, q.options());
   const int64_t q_rs = Tq == 1 ? q.stride(0) : q.stride(1);
   const int items = B * Hkv * Tq;
-  // keys per split: a split costs a second (combine) launch, ~4.6 µs in a replayed decode step, so
-  // only contexts longer than this are split (each workgroup sweeps its keys in chunks of 256; a
-  // graph captures S = the cache capacity and the kernel stops at the device-side length).
-  // PENROZ_DECODE_SPLIT_KEYS overrides (256: the round-4 rule)
-  static const int split_keys = [] {
+  // keys per split (each workgroup sweeps its keys in chunks of 256; a graph captures S = the cache
+  // capacity and the kernel stops at the device-side length). With zeroed arrival counters
+  // (`counters`, int32 >= items) the last split workgroup of an item merges the partials itself,
+  // so a split costs no second launch and contexts beyond 256 keys are split; without them a split
+  // costs the combine launch (~4.6 µs in a replayed step) and only contexts beyond 1024 keys are.
+  // GPT-2 B = 1 at a 1024-key context: 0.489 ms/token unsplit vs 0.418 split four ways
+  // (profiles/decode_longctx_r6.log). PENROZ_DECODE_SPLIT_KEYS overrides both.
+  static const int split_keys_env = [] {
     const char* e = std::getenv("PENROZ_DECODE_SPLIT_KEYS");
     const int v = e ? std::atoi(e) : 0;
-    return v >= 64 ? v : 1024;
+    return v >= 64 ? v : 0;
   }();
+  int* cnt = nullptr;
+  if (counters.has_value() && counters->defined()) {
+    TORCH_CHECK(counters->is_cuda() && counters->scalar_type() == torch::kInt32 && counters->is_contiguous(),
+                "counters: contiguous int32 on the device");
+    // beyond 8192 keys the combine launch wins again: every merging item costs its split
+    // workgroups a device-scope release (Gemma-3 1B batch 1 at 16k keys, 16 splits either way:
+    // 10.89-10.91 ms/token merged in launch vs 10.54-10.56 with the combine kernel)
+    if (counters->numel() >= items && S <= kMergeMaxKeys) cnt = counters->data_ptr<int>();
+  }
+  const int split_keys = split_keys_env ? split_keys_env : (cnt ? 256 : 1024);
   int splits = std::max(1, std::min<int>((512 + items - 1) / items, (int)((S + split_keys - 1) / split_keys)));
+  // the merging workgroup reads every split's partials: at most 16
+  if (cnt) splits = std::min(splits, kMaxMergeSplits);
+  // the one-workgroup-per-item kernel below takes contexts up to 1024 keys (GQA batch 1: Gemma-3
+  // 1B 1.57 -> 1.26 ms/token at a 1024-slot cache, profiles/decode_r5.md)
+  const int small_keys = split_keys_env ? split_keys_env : 1024;
   const int64_t* sdev = nullptr;
   if (seq_len_dev.has_value() && seq_len_dev->defined()) {
     TORCH_CHECK(seq_len_dev->is_cuda() && seq_len_dev->scalar_type() == torch::kInt64 && seq_len_dev->numel() == 1,
@@ -649,9 +727,9 @@ torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c
   const int G0 = H / Hkv;
   // (GQA or wide heads only: at G = 1, D = 64 — GPT-2 batch 1 — the general kernel is ~1 µs faster
   // per layer, profiles/decode_r5.md). It runs ONE workgroup per (batch, KV head) over the whole
-  // cache, so it only takes contexts the general kernel would not split either (S <= split_keys,
-  // S = the capacity under graph capture); longer contexts keep the key-split grid
-  if (!quant && q.scalar_type() == torch::kBFloat16 && Tq == 1 && items <= small_items && splits == 1 &&
+  // cache, so it only takes contexts up to small_keys (S = the capacity under graph capture);
+  // longer contexts keep the key-split grid
+  if (!quant && q.scalar_type() == torch::kBFloat16 && Tq == 1 && items <= small_items && S <= small_keys &&
       (G0 >= 2 || D >= 128 || small_any) &&
       (G0 == 1 || G0 == 2 || G0 == 4 || G0 == 8 || G0 == 16) && (D == 64 || D == 128 || D == 256 || D == 512) &&
       G0 * D <= 4096 && (!fuse || kv_rs % 8 == 0)) {
@@ -705,7 +783,8 @@ torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c
     const int G = H / Hkv;
 #define PENROZ_DECODE(DD, GC)                                                                                   \
   hipLaunchKernelGGL((decode_kernel<DD, GC, TQ, TK>), grid, dim3(256), 0, stream, qp, kp, vp, ksp, vsp, op, wo, wm, \
-                     B, Tq, H, Hkv, cap, (int)S, (int)q_offset, splits, (float)scale, sdev, q_rs, knp, vnp, kv_rs)
+                     B, Tq, H, Hkv, cap, (int)S, (int)q_offset, splits, (float)scale, sdev, q_rs, knp, vnp, kv_rs, cnt, \
+                     split_keys)
 #define PENROZ_DECODE_G(DD)              \
   switch (G) {                           \
     case 1: PENROZ_DECODE(DD, 1); break; \
@@ -720,7 +799,7 @@ torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c
     else PENROZ_DECODE(512, 0);              // Gemma-4 full-attention layers (global_head_dim)
 #undef PENROZ_DECODE_G
 #undef PENROZ_DECODE
-    if (splits > 1) {
+    if (splits > 1 && cnt == nullptr) {
       const int rows = B * Tq * H;
       hipLaunchKernelGGL(decode_combine_kernel<TQ>, dim3(std::min(2048, (rows * D + 255) / 256)), dim3(256), 0, stream,
                          wo, wm, op, rows, D, splits);

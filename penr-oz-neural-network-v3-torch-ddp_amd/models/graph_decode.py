@@ -582,6 +582,7 @@ class GraphDecoder:
         self.seed_t = torch.zeros(1, dtype=torch.long, device=self.device)  # per-run sampling salt
         self.graph: torch.cuda.CUDAGraph | None = None
         gemm_ops.skinny_workspace(self.device)  # zeroed counters exist before any capture
+        attn_ops.decode_counters(self.device)  # (the decode attention's split-merge counters too)
         gemm_ops.load_tuned_gemms()  # measured hipBLASLt solutions for the decode-shaped GEMMs too
         self.program = GPTDecodeProgram.build(model) or GemmaDecodeProgram.build(model)
 

@@ -198,6 +198,25 @@ def reference_cache_attention(q: Tensor, k: Tensor, v: Tensor, q_offset: int) ->
     return o.transpose(1, 2).reshape(B, Tq, H * D).to(q.dtype)
 
 
+# arrival counters of the decode kernel's in-launch split merge (csrc/kernels/decode_attn.hip):
+# zeroed once per device, outside any graph capture (every launch leaves them zero again), so a
+# captured step reuses them. PENROZ_DECODE_MERGE=0: no counters — the separate combine launch.
+DECODE_COUNTERS = 1 << 13
+_decode_counters: dict = {}
+
+
+def decode_counters(device: torch.device) -> Tensor | None:
+    """The device's split-merge counters, created on first use — unless that use is inside a
+    stream capture (the zeroing would become part of the graph): then None, the combine launch."""
+    if os.environ.get("PENROZ_DECODE_MERGE", "1") == "0" or device.type != "cuda":
+        return None
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    cnt = _decode_counters.get(idx)
+    if cnt is None and not torch.cuda.is_current_stream_capturing():
+        cnt = _decode_counters[idx] = torch.zeros(DECODE_COUNTERS, dtype=torch.int32, device=torch.device("cuda", idx))
+    return cnt
+
+
 def decode_attention(q: Tensor, k_cache: Tensor, v_cache: Tensor, seq_len: int,
                      k_scale: Tensor | None = None, v_scale: Tensor | None = None,
                      seq_len_dev: Tensor | None = None, k_new: Tensor | None = None,
@@ -219,7 +238,8 @@ def decode_attention(q: Tensor, k_cache: Tensor, v_cache: Tensor, seq_len: int,
                 and (Tq == 1 or q.stride(0) == q.shape[1] * q.stride(1))):
             q = q.contiguous()
         return kernels().decode_attn(q, k_cache, v_cache, k_scale, v_scale, int(seq_len),
-                                     int(seq_len - Tq), 1.0 / math.sqrt(q.shape[-1]), seq_len_dev, k_new, v_new)
+                                     int(seq_len - Tq), 1.0 / math.sqrt(q.shape[-1]), seq_len_dev, k_new, v_new,
+                                     decode_counters(q.device))
     if k_new is not None:
         raise ValueError("fused KV append needs the decode kernel")
     if seq_len_dev is not None:

@@ -596,6 +596,34 @@ def test_decode_attention(dtype, D, B, H, Hkv, S, Tq):
         _close(A.decode_attention(qv, kc, vc, S), out, 0.0)
 
 
+@pytest.mark.parametrize("B,H,Hkv,S,D", [(1, 12, 12, 1000, 64), (2, 8, 2, 3000, 128), (1, 4, 1, 5000, 256),
+                                         (3, 4, 4, 257, 64), (16, 8, 4, 8000, 64)])
+def test_decode_split_merge_in_launch_matches_combine_kernel(B, H, Hkv, S, D):
+    """Split decode attention: the last split workgroup's in-launch merge (arrival counters) matches
+    the fp32 reference, leaves every counter at zero, and repeated launches on the same counters
+    (a replayed graph) give the same result. Where both rules pick the same split count (64 items:
+    8 splits either way at 8000 keys) it is bitwise the combine kernel's output."""
+    from penroz.ops import _ext
+    k = _ext.kernels()
+    cap = S + 64
+    q = torch.randn(B, 1, H, D, device=DEV).to(torch.bfloat16)
+    kc = torch.randn(B, Hkv, cap, D, device=DEV).to(torch.bfloat16)
+    vc = torch.randn(B, Hkv, cap, D, device=DEV).to(torch.bfloat16)
+    cnt = torch.zeros(4096, dtype=torch.int32, device=DEV)
+    scale = 1.0 / math.sqrt(D)
+    merged = [k.decode_attn(q, kc, vc, None, None, S, S - 1, scale, None, None, None, cnt) for _ in range(3)]
+    combined = k.decode_attn(q, kc, vc, None, None, S, S - 1, scale, None, None, None, None)
+    for m in merged:
+        assert torch.equal(m, merged[0])
+    ref = A.reference_cache_attention(q.float(), kc[:, :, :S].float(), vc[:, :, :S].float(), S - 1)
+    _close(merged[0], ref, 0.02, 0.01)
+    _close(combined, ref, 0.02, 0.01)
+    torch.cuda.synchronize()
+    assert int(cnt.abs().sum()) == 0
+    if B * Hkv == 64:
+        assert torch.equal(merged[0], combined)
+
+
 def test_decode_attention_int8():
     B, H, S, D, cap = 2, 4, 200, 64, 256
     q = torch.randn(B, 1, H, D, device=DEV).to(torch.bfloat16)
