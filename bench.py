@@ -443,12 +443,41 @@ def _build(args, cfg, device, engine, world):
 
 
 def _make_step(runner, pool, device, sync_grads=True):
+    """One training step on pool batch i. On the GPU each step copies the NEXT step's batch on a
+    copy stream after enqueuing its own work (the runtime's Loader path prefetches the same way,
+    models/model.py): the host-to-device copy on the compute stream put the host behind the GPU
+    at every step boundary (PENROZ_COPY_STREAM=0: the copy inline, A/B; the copy stream is the
+    process-wide one the runtime's Loader path uses too, models/executor.py shared_stream)."""
+    cuda = device.type == "cuda" and os.environ.get("PENROZ_COPY_STREAM", "1") != "0"
+    if cuda:
+        from penroz.models.executor import shared_stream
+        cs = shared_stream(device, "copy")
+    pending = {}
+
+    def fetch(slot):
+        with torch.cuda.stream(cs):
+            buf = pool[slot].to(device, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(cs)
+        return buf, ev
+
     def step(i):
-        buf = pool[i % len(pool)].to(device, non_blocking=True)
+        slot = i % len(pool)
+        if cuda:
+            buf, ev = pending.pop(slot, None) or fetch(slot)
+            pending.clear()
+            cur = torch.cuda.current_stream(device)
+            cur.wait_event(ev)
+            buf.record_stream(cur)
+        else:
+            buf = pool[slot].to(device, non_blocking=True)
         x, y = buf[:, :-1], buf[:, 1:]
         runner.zero_grad()
         loss = runner.micro_step(x.contiguous(), y.contiguous(), 1.0, first=True, last=sync_grads, capture=False)
         runner.step()
+        if cuda:
+            nxt = (i + 1) % len(pool)
+            pending[nxt] = fetch(nxt)
         return loss
     return step
 

@@ -169,6 +169,22 @@ def _cu_masked_stream(device: torch.device, spec: str):
 
 
 _HP_STREAMS: dict = {}
+_SHARED_STREAMS: dict = {}
+
+
+def shared_stream(device: torch.device, role: str):
+    """ONE stream per (device, role) for the whole process — the executors' weight-gradient side
+    stream ("side"), the per-bucket optimizer stream ("opt") and the input-copy stream ("copy").
+    Every extra stream drawn from torch's pool is mapped onto one of the device's few hardware
+    queues (GPU_MAX_HW_QUEUES = 4), and which streams end up sharing a queue depends on how many
+    were drawn before: a copy stream created before a second model's executor cut that model's
+    step from 0.98 to 0.88 of the first's (bench.py --via-runtime, profiles/notes_r6.md). Shared
+    streams keep a later executor on the first one's queues; sharing only adds ordering."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    st = _SHARED_STREAMS.get((idx, role))
+    if st is None:
+        st = _SHARED_STREAMS[(idx, role)] = torch.cuda.Stream(device=torch.device("cuda", idx))
+    return st
 
 
 def _high_priority_stream(device: torch.device):
@@ -722,7 +738,7 @@ class GPTExecutor:
         stream before the step returns (the next forward reads the new weights)."""
         ost = getattr(self, "_opt_stream", None)
         if ost is None:
-            ost = self._opt_stream = torch.cuda.Stream(device=self.device)
+            ost = self._opt_stream = shared_stream(self.device, "opt")
         with torch.cuda.stream(ost):
             for i in ids:
                 if i in self._opt_buckets_done:
@@ -748,7 +764,7 @@ class GPTExecutor:
         self._side = None
         if self.device.type == "cuda" and os.environ.get("PENROZ_WGRAD_STREAM", "1") != "0":
             cus = os.environ.get("PENROZ_SIDE_CUS", "")
-            self._side = _cu_masked_stream(self.device, cus) if cus else torch.cuda.Stream(device=self.device)
+            self._side = _cu_masked_stream(self.device, cus) if cus else shared_stream(self.device, "side")
         self._buf_free = {}
 
     def _side_call(self, operand: Tensor, fn):

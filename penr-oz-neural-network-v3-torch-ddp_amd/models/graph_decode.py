@@ -668,7 +668,8 @@ class GraphDecoder:
         # warm-up really executes a step, so it must start from the true state: it then writes
         # exactly the cache slot the first real step rewrites.
         self._set_state(last_tok, cache_len, start)
-        side = torch.cuda.Stream(device=self.device)
+        from penroz.models.executor import shared_stream
+        side = shared_stream(self.device, "side")  # (no new pool stream per capture)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):
             self._step()
