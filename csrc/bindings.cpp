@@ -101,6 +101,7 @@ void decode_gemv_pair(torch::Tensor x, torch::Tensor w, torch::Tensor out, int64
                       int64_t pairs_per_wave);
 void decode_gemm_acc(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> bias, torch::Tensor resid,
                      int64_t flags);
+void decode_gemm(torch::Tensor x, torch::Tensor w, torch::Tensor out, int64_t kind);
 torch::Tensor update_moments(std::vector<torch::Tensor> ws, std::vector<torch::Tensor> ps);
 // gemm_nt.hip
 bool gemm_nt_supported(int64_t M, int64_t N, int64_t K);
@@ -248,6 +249,9 @@ PYBIND11_MODULE(penroz_kernels, m) {
   m.def("decode_gemm_acc", &decode_gemm_acc, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("bias"),
         pybind11::arg("resid"), pybind11::arg("flags") = 0,
         "batched decode: resid += x·wᵀ + bias (fp32 residual, in place)");
+  m.def("decode_gemm", &decode_gemm, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("out"),
+        pybind11::arg("kind") = -1,
+        "batched decode (16-64 rows): out = x·wᵀ, or the gated MLP act(x·Wgᵀ)·(x·Wuᵀ) of a packed [gate; up] weight");
   m.def("update_moments", &update_moments, "per-epoch weight-update diagnostics: [n, 2] (std(w - prev), std(w))");
   m.def("gemm_nt_supported", &gemm_nt_supported, "shapes the native NT GEMM takes (M % 256, N % 128, K % 32, K >= 160)");
   m.def("gemm_nt", &gemm_nt, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("bias"), pybind11::arg("out"),

@@ -243,6 +243,94 @@ __global__ void __launch_bounds__(256) decode_gemm_acc_kernel(const bf16* __rest
   *rp = cur;
 }
 
+// out[M, N] = x · Wᵀ (bf16) — decode_gemm_acc's tiling (16 rows × 16 columns per workgroup, the 4
+// waves split K, partial tiles reduced through LDS; every load of a wave's k-range in flight at
+// once) with a plain store, or with GATED the packed [gate; up] weight [2I, K]: a workgroup takes
+// gate columns n0..n0+15 and the matching up columns I + n0.., out[m, n] = bf16(act(bf16(g)) ·
+// bf16(u)) — the rounding of GEMM -> gated_act_packed. For the Gemma decode program's 17-64-row
+// steps, where hipBLASLt's picks for these skinny shapes ran 36-216 workgroups (gate|up at 64
+// rows: 72 workgroups, 1.6 TB/s of weights; profiles/notes_r6.md).
+// RB row blocks of 16 per workgroup share each weight fragment (RB = 4 at 33-64 rows and wide N:
+// the weights are read once instead of once per row block).
+template <bool GATED, int RB>
+__global__ void __launch_bounds__(256) decode_gemm_kernel(const bf16* __restrict__ x, int64_t x_rs,
+                                                          const bf16* __restrict__ w, bf16* __restrict__ out,
+                                                          int64_t o_rs, int M, int N, int K, int kind) {
+  constexpr int GROUP = (GATED ? 16 : kDlGroup) / RB;
+  __shared__ __attribute__((aligned(16))) dl_f32x4 red[2][RB][3 * 64];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  int rbg, ct;
+  dl_tile(blockIdx.x, (M + 16 * RB - 1) / (16 * RB), N / 16, rbg, ct);
+  const int steps = K / 32;
+  const int s0 = steps * wid / 4, s1 = steps * (wid + 1) / 4;
+  const int r16 = lane & 15, kq = 8 * (lane >> 4);
+  const int n0 = ct * 16;
+  const bf16* wp = w + (size_t)(n0 + r16) * K + kq;
+  const bf16* up = wp + (size_t)N * K;  // GATED: the up row of the same column
+  const bf16* xp[RB];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) {
+    const int mx = (rbg * RB + r) * 16 + r16;
+    xp[r] = x + (size_t)(mx < M ? mx : 0) * x_rs + kq;  // rows past M feed unstored outputs
+  }
+  dl_f32x4 acc0[RB], acc1[RB];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) acc0[r] = acc1[r] = dl_f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int s = s0; s < s1; s += GROUP) {
+    dl_u32x4 wg[GROUP], wu[GROUP], xb[RB * GROUP];  // (flat: a 2-D array of these miscompiled)
+#pragma unroll
+    for (int u = 0; u < GROUP; ++u) {
+      if (s + u < s1) {
+        const size_t ko = (size_t)(s + u) * 32;
+        wg[u] = *reinterpret_cast<const dl_u32x4*>(wp + ko);
+        if constexpr (GATED) wu[u] = *reinterpret_cast<const dl_u32x4*>(up + ko);
+#pragma unroll
+        for (int r = 0; r < RB; ++r) xb[r * GROUP + u] = *reinterpret_cast<const dl_u32x4*>(xp[r] + ko);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < GROUP; ++u) {
+      if (s + u < s1) {
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          acc0[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(dl_bf16x8, wg[u]),
+                                                            __builtin_bit_cast(dl_bf16x8, xb[r * GROUP + u]), acc0[r], 0, 0, 0);
+          if constexpr (GATED)
+            acc1[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(dl_bf16x8, wu[u]),
+                                                              __builtin_bit_cast(dl_bf16x8, xb[r * GROUP + u]), acc1[r], 0, 0, 0);
+        }
+      }
+    }
+  }
+  if (wid) {
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      red[0][r][(wid - 1) * 64 + lane] = acc0[r];
+      if constexpr (GATED) red[1][r][(wid - 1) * 64 + lane] = acc1[r];
+    }
+  }
+  __syncthreads();
+  if (wid) return;
+  const int n = n0 + 4 * (lane >> 4);
+#pragma unroll
+  for (int r = 0; r < RB; ++r) {
+    const int m = (rbg * RB + r) * 16 + r16;
+    if (m >= M) continue;
+    dl_f32x4 a0 = acc0[r] + red[0][r][lane] + red[0][r][64 + lane] + red[0][r][128 + lane];
+    dl_f32x4 a1 = acc1[r];
+    if constexpr (GATED) a1 += red[1][r][lane] + red[1][r][64 + lane] + red[1][r][128 + lane];
+    float y[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if constexpr (GATED)
+        y[i] = act_f(bf2f(from_f<bf16>(a0[i])), kind) * bf2f(from_f<bf16>(a1[i]));
+      else
+        y[i] = a0[i];
+    }
+    *reinterpret_cast<uint2*>(out + (size_t)m * o_rs + n) = uint2{pack_bf16x2(y[0], y[1]), pack_bf16x2(y[2], y[3])};
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // Decode GEMV for M <= 4 rows (batch-1..4 decode): out[M, N] = act(x · Wᵀ + bias), x either a
 // bf16 matrix or — LN mode — LayerNorm(resid_in + delta + dbias) computed in the kernel (the
@@ -577,6 +665,34 @@ void decode_gemm_acc(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tens
   hipLaunchKernelGGL(decode_gemm_acc_kernel, dim3(grid), dim3(256), 0, at::hip::getCurrentHIPStream(),
                      reinterpret_cast<const bf16*>(x.data_ptr()), (int64_t)x.stride(0),
                      reinterpret_cast<const bf16*>(w.data_ptr()), bp, resid.data_ptr<float>(), M, N, K, (int)flags);
+}
+
+// out[M, N] = x · Wᵀ (kind < 0), or with the packed [gate; up] weight [2I, K] out[M, I] =
+// act(x·Wgᵀ) ⊙ (x·Wuᵀ) (kind 0 gelu, 1 gelu_tanh, 2 silu) — decode_gemm_kernel
+void decode_gemm(torch::Tensor x, torch::Tensor w, torch::Tensor out, int64_t kind) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kBFloat16 && x.dim() == 2 && x.stride(1) == 1 &&
+                  x.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "decode_gemm: bf16 x [M, K], rows 16-B aligned");
+  const int M = x.size(0), K = x.size(1);
+  TORCH_CHECK(M >= 1 && K % 32 == 0, "decode_gemm: K % 32 == 0");
+  dl_check_w(w, K, "decode_gemm");
+  const bool gated = kind >= 0;
+  TORCH_CHECK(kind <= 2, "decode_gemm: kind -1 (plain), 0 gelu, 1 gelu_tanh, 2 silu");
+  const int N = gated ? w.size(0) / 2 : w.size(0);
+  TORCH_CHECK(N % 16 == 0 && (!gated || w.size(0) == 2 * N), "decode_gemm: N (gated: I) % 16 == 0");
+  TORCH_CHECK(out.scalar_type() == torch::kBFloat16 && out.dim() == 2 && out.size(0) == M && out.size(1) == N &&
+                  out.stride(1) == 1 && out.stride(0) % 4 == 0 && reinterpret_cast<uintptr_t>(out.data_ptr()) % 8 == 0,
+              "decode_gemm: bf16 out [M, N], rows 8-B aligned");
+  // 4 row blocks per workgroup once there are more than two and the columns alone give >= 256
+  // workgroups (weights read once); otherwise one row block per workgroup (more workgroups)
+  const int rb = (M > 32 && N / 16 >= 256) ? 4 : 1;
+  const int grid = ((M + 16 * rb - 1) / (16 * rb)) * (N / 16);
+  auto kern = gated ? (rb == 4 ? decode_gemm_kernel<true, 4> : decode_gemm_kernel<true, 1>)
+                    : (rb == 4 ? decode_gemm_kernel<false, 4> : decode_gemm_kernel<false, 1>);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, at::hip::getCurrentHIPStream(),
+                     reinterpret_cast<const bf16*>(x.data_ptr()), (int64_t)x.stride(0),
+                     reinterpret_cast<const bf16*>(w.data_ptr()), reinterpret_cast<bf16*>(out.data_ptr()),
+                     (int64_t)out.stride(0), M, N, K, (int)(gated ? kind : 0));
 }
 
 // out[M, N] = act(x · Wᵀ + bias) for M <= 4 decode rows (decode_gemv_kernel). LN mode (x

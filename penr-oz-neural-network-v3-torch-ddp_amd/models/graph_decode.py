@@ -520,18 +520,48 @@ class GemmaDecodeProgram:
         return logits
 
 
+# 17-32 rows: decode_linear.hip decode_gemm (16 rows × 16 columns per workgroup, K split over its
+# waves) instead of hipBLASLt, whose picks for these skinny shapes ran 36-216 workgroups
+# (profiles/notes_r6.md §13); up to this many output columns (the lm_head keeps hipBLASLt).
+# PENROZ_DECODE_GEMM=0: hipBLASLt (A/B)
+DECODE_GEMM = os.environ.get("PENROZ_DECODE_GEMM", "1") != "0"
+DECODE_GEMM_MAX_ROWS, DECODE_GEMM_MAX_N = 32, 32768
+
+
+def _decode_gemm_ok(x: Tensor, w: Tensor, gated: bool = False) -> bool:
+    """decode_gemm takes 17-32 rows (Gemma-3 1B B = 17 / 32: 2.20 -> 1.92 / 2.22 -> 2.07
+    ms/step). At 64 rows every mix measured slower than hipBLASLt's step (2.42 ms: 2.60-2.88;
+    the narrow O / down projections ran 19 vs 8-12 µs), so those keep hipBLASLt
+    (profiles/notes_r6.md §13)."""
+    n = w.shape[0] // 2 if gated else w.shape[0]
+    return (DECODE_GEMM and SKINNY_MAX_ROWS < x.shape[0] <= DECODE_GEMM_MAX_ROWS and x.is_cuda
+            and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 2 and x.stride(1) == 1
+            and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0 and w.is_contiguous() and w.data_ptr() % 16 == 0
+            and w.shape[1] == x.shape[1] and x.shape[1] % 32 == 0 and n % 16 == 0 and n <= DECODE_GEMM_MAX_N
+            and _ext.available())
+
+
 def _gated(x: Tensor, gu: Tensor, kind: int) -> Tensor:
-    """act(x·Wgᵀ) ⊙ (x·Wuᵀ) from the packed gate|up weight: one fused skinny launch up to
-    SKINNY_MAX_ROWS rows (activation in the GEMM epilogue), else GEMM + packed activation."""
+    """act(x·Wgᵀ) ⊙ (x·Wuᵀ) from the packed gate|up weight: one fused launch with the activation
+    in the GEMM epilogue (the skinny kernel up to SKINNY_MAX_ROWS rows, decode_gemm up to 64), else
+    GEMM + packed activation."""
     if DECODE_EPILOGUES and x.shape[0] <= SKINNY_MAX_ROWS and gemm_ops.skinny_ok(x, gu):
         return gemm_ops.skinny_gated(x, gu, kind)
+    if DECODE_EPILOGUES and _decode_gemm_ok(x, gu, gated=True):
+        out = torch.empty(x.shape[0], gu.shape[0] // 2, device=x.device, dtype=torch.bfloat16)
+        _ext.kernels().decode_gemm(x, gu, out, kind)
+        return out
     return _ext.kernels().gated_act_packed(_linear(x, gu), kind)
 
 
 def _linear(x: Tensor, w: Tensor) -> Tensor:
-    """x [M, K] · wᵀ without bias: the decode-shaped MFMA kernel up to SKINNY_MAX_ROWS rows."""
+    """x [M, K] · wᵀ without bias: the decode-shaped MFMA kernels up to 64 rows."""
     if x.shape[0] <= SKINNY_MAX_ROWS and gemm_ops.skinny_ok(x, w):
         return gemm_ops.skinny_linear(x, w, None)
+    if _decode_gemm_ok(x, w):
+        out = torch.empty(x.shape[0], w.shape[0], device=x.device, dtype=torch.bfloat16)
+        _ext.kernels().decode_gemm(x, w, out, -1)
+        return out
     return torch.mm(x, w.t())
 
 
