@@ -1,3 +1,9 @@
+"""Host time per step of the headline executor loop (bench.py's step), with the GPU idle and
+with the GPU busy ahead of the host: shows whether the host's enqueue rate can keep up with the
+GPU (profiles/notes_r6.md §1: 10-13 ms of host time against a 61 ms GPU step).
+
+    python bench/host_time.py
+"""
 import os, sys, time, torch
 sys.path.insert(0, os.getcwd())
 import bench
