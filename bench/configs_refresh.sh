@@ -1,4 +1,4 @@
-# Round-6 refresh of every secondary config (one box, one after the other) -> gpurun_out/bench_r6_configs.log
+# Refresh of every secondary config (one box, one after the other) -> gpurun_out/bench_r6_configs.log
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
