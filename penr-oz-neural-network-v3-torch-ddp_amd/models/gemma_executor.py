@@ -96,7 +96,10 @@ class GemmaSpec:
 
 
 class GemmaExecutor(GPTExecutor):
-    MAIN_PRIORITY_DEFAULT = False  # measured slightly slower at B = 8 (GPTExecutor._main_stream)
+    # the critical path on the high-priority stream: round 5 measured it slightly slower at B = 8;
+    # with one stream per role per process (round 6) it is faster: Gemma-3 1B B = 8 66.85 / 66.87
+    # -> 66.30 / 66.29 ms (same box, profiles/notes_r6.md §15)
+    MAIN_PRIORITY_DEFAULT = True
     SEGMENT_TRANSPOSE = True  # see GPTExecutor._transpose_segment
 
     # ------------------------------------------------------------------ pattern match
