@@ -444,7 +444,9 @@ class GPTExecutor:
     def _transpose_segment(self, s: int, e: int):
         """Rebuild the transposed dgrad copies of the parameters in flat range [s, e) on the current
         stream, right after that range's optimizer pass (their shadow is final for the next step)."""
-        if not getattr(self, "_tw", None) or not self.SEGMENT_TRANSPOSE:
+        import os
+        env = os.environ.get("PENROZ_SEGMENT_TRANSPOSE")  # (A/B: 1 / 0 overrides the class default)
+        if not getattr(self, "_tw", None) or not (self.SEGMENT_TRANSPOSE if env is None else env == "1"):
             return
         k = _ext.kernels()
         for key, ent in self._tw.items():

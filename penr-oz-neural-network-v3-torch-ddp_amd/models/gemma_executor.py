@@ -100,7 +100,12 @@ class GemmaExecutor(GPTExecutor):
     # with one stream per role per process (round 6) it is faster: Gemma-3 1B B = 8 66.85 / 66.87
     # -> 66.30 / 66.29 ms (same box, profiles/notes_r6.md §15)
     MAIN_PRIORITY_DEFAULT = True
-    SEGMENT_TRANSPOSE = True  # see GPTExecutor._transpose_segment
+    # transposed dgrad copies rebuilt at the step start (as GPT) instead of after each segment's
+    # AdamW: round 5 measured the segment rebuild −0.2 to −0.3 ms; with the high-priority critical
+    # path and the shared streams (round 6) the step-start rebuild is faster: Gemma-3 1B B = 8
+    # 65.86 / 65.86 -> 65.14 / 65.32 and 65.82 / 65.72 -> 65.09 / 65.06 ms on two boxes, Gemma-4 e2b
+    # neutral (profiles/notes_r6.md §16; PENROZ_SEGMENT_TRANSPOSE=1 / 0 overrides)
+    SEGMENT_TRANSPOSE = False
 
     # ------------------------------------------------------------------ pattern match
     @staticmethod
