@@ -63,7 +63,8 @@ def _worker(rank, world, port, out, bucket_mb, overlap, model_type):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK="0", PENROZ_BUCKET_MB=str(bucket_mb),
                       PENROZ_OVERLAP_OPT=str(1 if per_bucket else overlap),
-                      PENROZ_OPT_PER_BUCKET="1" if per_bucket else "0")
+                      PENROZ_OPT_PER_BUCKET="1" if per_bucket else "0",
+                      PENROZ_SEGMENT_TRANSPOSE="1" if per_bucket else "0")
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import penroz.parallel.reducer as R
@@ -83,7 +84,7 @@ def _worker(rank, world, port, out, bucket_mb, overlap, model_type):
     if per_bucket:
         # the fused AdamW of each bucket inside the backward (optimizer stream, after the bucket's
         # all-reduce), then the transposed dgrad copies of the weights wholly inside the bucket
-        # (SEGMENT_TRANSPOSE): a SECOND step runs its dgrads on them, so two steps are compared
+        # (PENROZ_SEGMENT_TRANSPOSE=1): a SECOND step runs its dgrads on them, so two steps are compared
         for step in range(2):
             xs, ys = _batch(rank + 10 * step)
             ex.zero_grad()

@@ -371,8 +371,8 @@ def test_new_session_after_segment_transposes_uses_fresh_weights(monkeypatch):
     rebuild them too, or its first step's data gradients use the old weights. Gradients of the
     first step after the reload == an executor without transposed copies (PENROZ_DGRAD_T=0)."""
     from penroz.models.model import _FusedRunner
+    monkeypatch.setenv("PENROZ_SEGMENT_TRANSPOSE", "1")  # (the default rebuilds at the step start)
     m = _gemma("gemma3_text", seed=6).to(DEV)
-    assert GemmaExecutor.SEGMENT_TRANSPOSE
     _train(m, 2, True)
     ex = m._get_executor(torch.device(DEV))
     other = _gemma("gemma3_text", seed=7).to(DEV)
