@@ -905,9 +905,12 @@ class GPTExecutor:
             self._opt_apply = None
         return loss
 
-    # the critical path on a high-priority stream: GPT-2 headline 61.63 / 61.63 -> 61.19 / 61.19
-    # ms/step; Gemma-3 1B B=8 66.42 / 66.71 -> 66.68 / 66.84 (same box, profiles/notes_r5.md)
-    MAIN_PRIORITY_DEFAULT = True
+    # the critical path on a high-priority stream. Round 5: GPT-2 headline 61.63 / 61.63 -> 61.19 /
+    # 61.19 ms/step. Round 6, with one stream per role per process and the batch copy on its own
+    # stream, the headline is faster WITHOUT it: 61.83 / 61.76 / 61.79 (high) vs 61.55 / 61.60 /
+    # 61.63 (normal) and 60.45 / 60.54 vs 60.40 / 60.29 on a second box; the Gemma executors keep
+    # it (faster there, profiles/notes_r6.md §15, §17)
+    MAIN_PRIORITY_DEFAULT = False
 
     def _main_stream(self):
         """A high-priority stream for the forward / backward critical path, so the side stream's
