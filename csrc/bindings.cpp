@@ -69,7 +69,9 @@ torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c
                           c10::optional<torch::Tensor> v_scale, int64_t S, int64_t q_offset, double scale,
                           c10::optional<torch::Tensor> seq_len_dev,
                           c10::optional<torch::Tensor> k_new, c10::optional<torch::Tensor> v_new,
-                          c10::optional<torch::Tensor> counters);
+                          c10::optional<torch::Tensor> counters, c10::optional<torch::Tensor> rope_cos,
+                          c10::optional<torch::Tensor> rope_sin);
+bool decode_small_applies(int64_t B, int64_t Tq, int64_t H, int64_t Hkv, int64_t D, int64_t S);
 // elementwise.hip (deferred.h)
 void set_deferred_reduce_stream(int64_t stream, int64_t device);
 // decode_attn.hip
@@ -205,7 +207,9 @@ PYBIND11_MODULE(penroz_kernels, m) {
   m.def("decode_attn", &decode_attn, pybind11::arg("q"), pybind11::arg("kc"), pybind11::arg("vc"), pybind11::arg("k_scale"),
         pybind11::arg("v_scale"), pybind11::arg("S"), pybind11::arg("q_offset"), pybind11::arg("scale"),
         pybind11::arg("seq_len_dev") = pybind11::none(), pybind11::arg("k_new") = pybind11::none(),
-        pybind11::arg("v_new") = pybind11::none(), pybind11::arg("counters") = pybind11::none());
+        pybind11::arg("v_new") = pybind11::none(), pybind11::arg("counters") = pybind11::none(),
+        pybind11::arg("rope_cos") = pybind11::none(), pybind11::arg("rope_sin") = pybind11::none());
+  m.def("decode_small_applies", &decode_small_applies, "decode_attn takes the one-workgroup-per-item kernel");
   m.def("set_deferred_reduce_stream", &set_deferred_reduce_stream);
   m.def("kv_append", &kv_append, pybind11::arg("k"), pybind11::arg("v"), pybind11::arg("kc"), pybind11::arg("vc"),
         pybind11::arg("ks") = pybind11::none(), pybind11::arg("vs") = pybind11::none(),

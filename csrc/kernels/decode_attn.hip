@@ -414,13 +414,19 @@ __global__ void __launch_bounds__(256) decode_kernel(const TQ* __restrict__ q, c
 // The 4 waves' (m, l, O) merge through LDS at the end. Made for the batch-1 GQA shapes where the
 // general kernel's thread-per-key loop is serial (Gemma-3 1B: G = 4, D = 256 — 19 µs per layer).
 // Fused append as in decode_kernel: key S-1 comes from k_new / v_new and is written to the cache.
+// rc / rs (optional, fp32 [D/2]: this step's RoPE cos / sin): the query and the new key arrive
+// unrotated and are rotated here (rotate-half pairs d, d + D/2, rope_vec_kernel's arithmetic), so the
+// decode step needs no separate RoPE pass. Column chunk s2 of a lane pairs with chunk s2 + KS/2 of
+// the same lane, so the rotation stays in registers.
 template <int D, int GMAX>  // GMAX: the exact query-group size H / Hkv
 __global__ void __launch_bounds__(256) decode_small_kernel(const bf16* __restrict__ q, bf16* __restrict__ kc,
                                                            bf16* __restrict__ vc, bf16* __restrict__ out, int H,
                                                            int Hkv, int cap, int S, float scale,
                                                            const int64_t* __restrict__ S_dev, int64_t q_rs,
                                                            const bf16* __restrict__ k_new,
-                                                           const bf16* __restrict__ v_new, int64_t kv_rs) {
+                                                           const bf16* __restrict__ v_new, int64_t kv_rs,
+                                                           const float* __restrict__ rc,
+                                                           const float* __restrict__ rs) {
   constexpr int KS = D / 32;   // MFMA k-steps per score block
   constexpr int EPL = D / 64;  // P·V output columns per lane
   static_assert(EPL >= 1 && (EPL & (EPL - 1)) == 0 && GMAX <= 16, "decode_small geometry");
@@ -447,6 +453,33 @@ __global__ void __launch_bounds__(256) decode_small_kernel(const bf16* __restric
 #pragma unroll
     for (int s2 = 0; s2 < KS; ++s2) qf[s2] = ok ? *reinterpret_cast<const uint4*>(qp + 32 * s2) : uint4{0u, 0u, 0u, 0u};
   }
+  // rotate a lane's KS chunks (columns 32 s2 + 8 qd .. +8) of one head row in place
+  auto rotate = [&](uint4* f) {
+#pragma unroll
+    for (int s2 = 0; s2 < KS / 2; ++s2) {
+      const int j0 = 32 * s2 + 8 * qd;
+      const float4 c0 = *reinterpret_cast<const float4*>(rc + j0), c1 = *reinterpret_cast<const float4*>(rc + j0 + 4);
+      const float4 n0 = *reinterpret_cast<const float4*>(rs + j0), n1 = *reinterpret_cast<const float4*>(rs + j0 + 4);
+      const float cs[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+      const float sn[8] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w};
+      const uint32_t a[4] = {f[s2].x, f[s2].y, f[s2].z, f[s2].w};
+      const uint32_t bb[4] = {f[s2 + KS / 2].x, f[s2 + KS / 2].y, f[s2 + KS / 2].z, f[s2 + KS / 2].w};
+      uint32_t o1[4], o2[4];
+#pragma unroll
+      for (int e2 = 0; e2 < 4; ++e2) {
+        const float x1l = __uint_as_float(a[e2] << 16), x1h = __uint_as_float(a[e2] & 0xffff0000u);
+        const float x2l = __uint_as_float(bb[e2] << 16), x2h = __uint_as_float(bb[e2] & 0xffff0000u);
+        const int e = 2 * e2;
+        const float y1l = x1l * cs[e] - x2l * sn[e], y1h = x1h * cs[e + 1] - x2h * sn[e + 1];
+        const float y2l = x2l * cs[e] + x1l * sn[e], y2h = x2h * cs[e + 1] + x1h * sn[e + 1];
+        o1[e2] = pack_bf16x2(y1l, y1h);
+        o2[e2] = pack_bf16x2(y2l, y2h);
+      }
+      f[s2] = uint4{o1[0], o1[1], o1[2], o1[3]};
+      f[s2 + KS / 2] = uint4{o2[0], o2[1], o2[2], o2[3]};
+    }
+  };
+  if (rc != nullptr) rotate(qf);
   // keys of this wave
   const int per = ((S + 63) / 64) * 16;  // 16-key blocks, a quarter each
   const int k0 = w * per, k1 = min(S, k0 + per);
@@ -465,6 +498,7 @@ __global__ void __launch_bounds__(256) decode_small_kernel(const bf16* __restric
     const bf16* kr = fresh ? k_new + new_off : kc + (head_base + key) * D;
 #pragma unroll
     for (int s2 = 0; s2 < KS; ++s2) kf[s2] = *reinterpret_cast<const uint4*>(kr + 32 * s2 + 8 * qd);
+    if (rc != nullptr && fresh) rotate(kf);
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const int kj = min(kb + j, S - 1);
@@ -489,7 +523,19 @@ __global__ void __launch_bounds__(256) decode_small_kernel(const bf16* __restric
     bf16* kd = kc + (head_base + S - 1) * D;
     bf16* vd = vc + (head_base + S - 1) * D;
     for (int d = 8 * lane; d < D; d += 512) {
-      *reinterpret_cast<uint4*>(kd + d) = *reinterpret_cast<const uint4*>(ks + d);
+      if (rc != nullptr) {
+        constexpr int half = D / 2;
+        const int j0 = d < half ? d : d - half;
+        float x1[8], x2[8], y[8];
+        Vec8<bf16>::load(ks + j0, x1);
+        Vec8<bf16>::load(ks + j0 + half, x2);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          y[e] = d < half ? x1[e] * rc[j0 + e] - x2[e] * rs[j0 + e] : x2[e] * rc[j0 + e] + x1[e] * rs[j0 + e];
+        Vec8<bf16>::store(kd + d, y);
+      } else {
+        *reinterpret_cast<uint4*>(kd + d) = *reinterpret_cast<const uint4*>(ks + d);
+      }
       *reinterpret_cast<uint4*>(vd + d) = *reinterpret_cast<const uint4*>(vs + d);
     }
   }
@@ -637,6 +683,37 @@ __global__ void __launch_bounds__(256) kv_append_kernel(const T* __restrict__ k,
 
 using namespace penroz;
 
+// Whether decode_attn takes the one-workgroup-per-(batch, KV head) kernel (decode_small_kernel) for
+// a bf16 cache of S slots (the capacity under graph capture). Callers fusing RoPE into the decode
+// step ask this first: only that kernel rotates in place.
+bool decode_small_applies(int64_t B, int64_t Tq, int64_t H, int64_t Hkv, int64_t D, int64_t S) {
+  // PENROZ_DECODE_SMALL_ITEMS: the largest B·Hkv it takes (0 disables)
+  static const int small_items = [] {
+    const char* e = std::getenv("PENROZ_DECODE_SMALL_ITEMS");
+    return e ? std::atoi(e) : 64;
+  }();
+  static const bool small_any = [] {  // (A/B switch: also MHA head_dim 64 — GPT-2)
+    const char* e = std::getenv("PENROZ_DECODE_SMALL_ANY");
+    return e && e[0] == '1';
+  }();
+  static const int split_keys_env = [] {
+    const char* e = std::getenv("PENROZ_DECODE_SPLIT_KEYS");
+    const int v = e ? std::atoi(e) : 0;
+    return v >= 64 ? v : 0;
+  }();
+  if (Hkv <= 0 || H % Hkv) return false;
+  const int64_t G0 = H / Hkv;
+  // the one-workgroup-per-item kernel takes contexts up to 1024 keys (GQA batch 1: Gemma-3 1B
+  // 1.57 -> 1.26 ms/token at a 1024-slot cache, profiles/decode_r5.md); GQA or wide heads only: at
+  // G = 1, D = 64 (GPT-2 batch 1) the general kernel is ~1 µs faster per layer. It runs ONE
+  // workgroup per (batch, KV head) over the whole cache, so longer contexts keep the key-split
+  // grid
+  const int64_t small_keys = split_keys_env ? split_keys_env : 1024;
+  return Tq == 1 && B * Hkv <= small_items && S <= small_keys && (G0 >= 2 || D >= 128 || small_any) &&
+         (G0 == 1 || G0 == 2 || G0 == 4 || G0 == 8 || G0 == 16) && (D == 64 || D == 128 || D == 256 || D == 512) &&
+         G0 * D <= 4096;
+}
+
 // seq_len_dev (optional int64 [1] on the device): the cache length is read by the kernel at run
 // time (S / q_offset are then only upper bounds used to size the launch) — lets a captured HIP
 // graph replay the same decode step at every position.
@@ -645,7 +722,8 @@ using namespace penroz;
 torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c10::optional<torch::Tensor> k_scale,
                           c10::optional<torch::Tensor> v_scale, int64_t S, int64_t q_offset, double scale,
                           c10::optional<torch::Tensor> seq_len_dev, c10::optional<torch::Tensor> k_new,
-                          c10::optional<torch::Tensor> v_new, c10::optional<torch::Tensor> counters) {
+                          c10::optional<torch::Tensor> v_new, c10::optional<torch::Tensor> counters,
+                          c10::optional<torch::Tensor> rope_cos, c10::optional<torch::Tensor> rope_sin) {
   TORCH_CHECK(q.is_cuda() && q.dim() == 4, "q must be [B, Tq, H, D]");
   // q may be a view into the fused QKV rows: unit dim stride, packed heads, uniform row stride
   // (a size-1 Tq dim may carry any stride: the row stride is then stride(0))
@@ -689,9 +767,6 @@ torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c
   int splits = std::max(1, std::min<int>((512 + items - 1) / items, (int)((S + split_keys - 1) / split_keys)));
   // the merging workgroup reads every split's partials: at most 16
   if (cnt) splits = std::min(splits, kMaxMergeSplits);
-  // the one-workgroup-per-item kernel below takes contexts up to 1024 keys (GQA batch 1: Gemma-3
-  // 1B 1.57 -> 1.26 ms/token at a 1024-slot cache, profiles/decode_r5.md)
-  const int small_keys = split_keys_env ? split_keys_env : 1024;
   const int64_t* sdev = nullptr;
   if (seq_len_dev.has_value() && seq_len_dev->defined()) {
     TORCH_CHECK(seq_len_dev->is_cuda() && seq_len_dev->scalar_type() == torch::kInt64 && seq_len_dev->numel() == 1,
@@ -714,25 +789,21 @@ torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c
   const float* ksp = quant ? k_scale->data_ptr<float>() : nullptr;
   const float* vsp = quant ? v_scale->data_ptr<float>() : nullptr;
   auto stream = at::hip::getCurrentHIPStream();
-  // small batches, bf16, one query row: the wave-parallel MFMA kernel (decode_small_kernel).
-  // PENROZ_DECODE_SMALL_ITEMS: the largest B·Hkv it takes (0 disables)
-  static const int small_items = [] {
-    const char* e = std::getenv("PENROZ_DECODE_SMALL_ITEMS");
-    return e ? std::atoi(e) : 64;
-  }();
-  static const bool small_any = [] {  // (A/B switch: also MHA head_dim 64 — GPT-2)
-    const char* e = std::getenv("PENROZ_DECODE_SMALL_ANY");
-    return e && e[0] == '1';
-  }();
-  const int G0 = H / Hkv;
-  // (GQA or wide heads only: at G = 1, D = 64 — GPT-2 batch 1 — the general kernel is ~1 µs faster
-  // per layer, profiles/decode_r5.md). It runs ONE workgroup per (batch, KV head) over the whole
-  // cache, so it only takes contexts up to small_keys (S = the capacity under graph capture);
-  // longer contexts keep the key-split grid
-  if (!quant && q.scalar_type() == torch::kBFloat16 && Tq == 1 && items <= small_items && S <= small_keys &&
-      (G0 >= 2 || D >= 128 || small_any) &&
-      (G0 == 1 || G0 == 2 || G0 == 4 || G0 == 8 || G0 == 16) && (D == 64 || D == 128 || D == 256 || D == 512) &&
-      G0 * D <= 4096 && (!fuse || kv_rs % 8 == 0)) {
+  // small batches, bf16, one query row: the wave-parallel MFMA kernel (decode_small_kernel)
+  const bool small = !quant && q.scalar_type() == torch::kBFloat16 && decode_small_applies(B, Tq, H, Hkv, D, S) &&
+                     (!fuse || kv_rs % 8 == 0);
+  const bool rope = rope_cos.has_value() && rope_cos->defined();
+  if (rope) {
+    TORCH_CHECK(small && fuse, "in-kernel RoPE: the small decode kernel with the fused append only "
+                "(check decode_small_applies first)");
+    for (const auto* t : {&*rope_cos, &*rope_sin})
+      TORCH_CHECK(t->is_cuda() && t->scalar_type() == torch::kFloat32 && t->is_contiguous() && t->numel() == D / 2,
+                  "rope cos / sin: contiguous fp32 [D/2] (one position)");
+  }
+  const float* rcp = rope ? rope_cos->data_ptr<float>() : nullptr;
+  const float* rsp = rope ? rope_sin->data_ptr<float>() : nullptr;
+  if (small) {
+    const int G0 = H / Hkv;
     const bf16* qp = reinterpret_cast<const bf16*>(q.data_ptr());
     bf16* kp = reinterpret_cast<bf16*>(kc.data_ptr());
     bf16* vp = reinterpret_cast<bf16*>(vc.data_ptr());
@@ -741,7 +812,7 @@ torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c
     const bf16* vnp = fuse ? reinterpret_cast<const bf16*>(v_new->data_ptr()) : nullptr;
 #define PENROZ_DSMALL(DD, GG)                                                                                       \
   hipLaunchKernelGGL((decode_small_kernel<DD, GG>), dim3(B * Hkv), dim3(256), 0, stream, qp, kp, vp, op, H, Hkv, cap, \
-                     (int)S, (float)scale, sdev, q_rs, knp, vnp, kv_rs)
+                     (int)S, (float)scale, sdev, q_rs, knp, vnp, kv_rs, rcp, rsp)
 #define PENROZ_DSMALL_G(DD)                      \
   switch (G0) {                                   \
     case 1: PENROZ_DSMALL(DD, 1); break;          \

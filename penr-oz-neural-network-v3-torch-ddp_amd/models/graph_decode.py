@@ -130,6 +130,24 @@ class StaticKVCache(_GraphMode, kvc.KVCache):
         return attn_ops.decode_attention(q, kc, vc, kc.shape[2], seq_len_dev=self.len_t)
 
 
+    def rope_attend_ok(self, B: int, H: int, Hkv: int, D: int) -> bool:
+        """``attend_rope`` applies: opted in (PENROZ_DECODE_ROPE_IN_ATTN=1), graph mode with the
+        fused append, the small decode kernel. Off by default: Gemma-3 1B batch 32 / 64 measured
+        2.115 / 2.109 and 2.433 / 2.444 ms/step with it vs 2.103 / 2.099 and 2.434 / 2.439 ms with
+        the separate RoPE pass (profiles/negative_r6_rope_in_decode_attn.log)."""
+        kc = self._k[0]
+        return (os.environ.get("PENROZ_DECODE_ROPE_IN_ATTN", "0") == "1" and self.graph_mode and FUSED_APPEND
+                and _ext.available()
+                and attn_ops.decode_rope_fusable(B, H, Hkv, D, kc.shape[2], kc.dtype))
+
+    def attend_rope(self, l: int, q: Tensor, k: Tensor, v: Tensor, cos: Tensor, sin: Tensor) -> Tensor:
+        """``attend`` with q / k unrotated: the decode kernel applies RoPE (cos / sin [1, D/2]) to
+        q and to the key it appends, in place of a separate RoPE pass over the QKV rows."""
+        kc, vc = self._k[l], self._v[l]
+        return attn_ops.decode_attention(q, kc, vc, kc.shape[2], seq_len_dev=self.len_t, k_new=k, v_new=v,
+                                         rope=(cos.view(-1), sin.view(-1)))
+
+
 class StaticTurboKVCache(_GraphMode, kvc.TurboQuantKVCache):
     def _attend_graph(self, l: int, q: Tensor, k: Tensor, v: Tensor) -> Tensor:
         # same per-token int8 quantiser as the eager append (kv_quantize)
@@ -467,13 +485,21 @@ class GemmaDecodeProgram:
                     qkv = qkv.view(rows, 1, -1)
                 elif DECODE_EPILOGUES and rows <= SKINNY_MAX_ROWS and gemm_ops.skinny_qkv_rope_ok(y, b["qkv"], D):
                     qkv = gemm_ops.skinny_qkv_rope(y, b["qkv"], cos, sin, D, H + Hkv).view(rows, 1, -1)
+                elif getattr(cache, "rope_attend_ok", None) is not None and cache.rope_attend_ok(rows, H, Hkv, D):
+                    # 17-64 rows: q and the new key rotated inside the decode attention kernel
+                    qkv = _linear(y, b["qkv"]).view(rows, 1, -1)
+                    q, k, v = qkv.split([H * D, Hkv * D, Hkv * D], dim=2)
+                    att = cache.attend_rope(l, q.reshape(rows, 1, H, D), k.view(rows, 1, Hkv, D),
+                                            v.view(rows, 1, Hkv, D), cos, sin)
+                    qkv = None
                 else:
                     qkv = rope_ops.apply_rope_qkv(_linear(y, b["qkv"]).view(rows, 1, -1), H, Hkv, D, inv, 0,
                                                   table=(cos, sin))
             else:
                 qkv = lin(y, b["qkv"]).view(rows, 1, -1)
-            q, k, v = qkv.split([H * D, Hkv * D, Hkv * D], dim=2)
-            att = cache.attend(l, q.reshape(rows, 1, H, D), k.view(rows, 1, Hkv, D), v.view(rows, 1, Hkv, D))
+            if qkv is not None:
+                q, k, v = qkv.split([H * D, Hkv * D, Hkv * D], dim=2)
+                att = cache.attend(l, q.reshape(rows, 1, H, D), k.view(rows, 1, Hkv, D), v.view(rows, 1, Hkv, D))
             o = lin(att.view(rows, H * D), b["o"])
             pa, pm, pre = b["post_attn"], b["post_mlp"], b["pre_mlp"]
             h, y = K.rms_residual(x, o, pa.weight if pa is not None else None, pre.weight, b["mode"],

@@ -217,10 +217,16 @@ def decode_counters(device: torch.device) -> Tensor | None:
     return cnt
 
 
+def decode_rope_fusable(B: int, H: int, Hkv: int, D: int, cap: int, cache_dtype: torch.dtype) -> bool:
+    """The decode kernel can rotate q and the appended key itself (``decode_attention(rope=)``):
+    the one-workgroup-per-(batch, KV head) kernel over a bf16 cache of ``cap`` slots."""
+    return cache_dtype == torch.bfloat16 and D % 16 == 0 and kernels().decode_small_applies(B, 1, H, Hkv, D, cap)
+
+
 def decode_attention(q: Tensor, k_cache: Tensor, v_cache: Tensor, seq_len: int,
                      k_scale: Tensor | None = None, v_scale: Tensor | None = None,
                      seq_len_dev: Tensor | None = None, k_new: Tensor | None = None,
-                     v_new: Tensor | None = None) -> Tensor:
+                     v_new: Tensor | None = None, rope: tuple[Tensor, Tensor] | None = None) -> Tensor:
     """Attention of ``q [B, Tq, H, D]`` against the first ``seq_len`` cache slots.
 
     Cache layout ``[B, Hkv, cap, D]`` (bf16/fp16/fp32, or int8 with per-token fp32 scales
@@ -230,8 +236,13 @@ def decode_attention(q: Tensor, k_cache: Tensor, v_cache: Tensor, seq_len: int,
     capacity bound) — the form a captured HIP graph replays at every position.
     ``k_new`` / ``v_new`` ([B, 1, Hkv, D], GPU kernel only): this step's K / V, appended at slot
     ``seq_len - 1`` by the attention kernel itself (int8 caches: quantised as ``kv_quantize_into``).
+    ``rope`` (fp32 cos / sin [D/2] of this step's single position; with ``k_new`` / ``v_new``): q and
+    the new key arrive unrotated and the kernel applies rotate-half RoPE itself — only where
+    ``decode_rope_fusable`` says so.
     """
     Tq = q.shape[1]
+    if rope is not None and (k_new is None or not use_kernels(q)):
+        raise ValueError("in-kernel RoPE needs the decode kernel's fused append")
     if use_kernels(q) and q.shape[-1] in DECODE_HEAD_DIMS:
         # a view into the fused QKV rows is read in place (packed heads, uniform row stride)
         if not (q.stride(3) == 1 and q.stride(2) == q.shape[3]
@@ -239,7 +250,7 @@ def decode_attention(q: Tensor, k_cache: Tensor, v_cache: Tensor, seq_len: int,
             q = q.contiguous()
         return kernels().decode_attn(q, k_cache, v_cache, k_scale, v_scale, int(seq_len),
                                      int(seq_len - Tq), 1.0 / math.sqrt(q.shape[-1]), seq_len_dev, k_new, v_new,
-                                     decode_counters(q.device))
+                                     decode_counters(q.device), *(rope if rope is not None else (None, None)))
     if k_new is not None:
         raise ValueError("fused KV append needs the decode kernel")
     if seq_len_dev is not None:

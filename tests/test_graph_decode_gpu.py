@@ -158,8 +158,11 @@ def test_rope_model_graph_decode_matches_eager(monkeypatch, head_dim):
 
 
 @pytest.mark.parametrize("model_type", ["gemma", "gemma2", "gemma3_text"])  # post-norm modes 2, 1, 0
-@pytest.mark.parametrize("rows", [1, 3, 8])  # 1, 3: decode GEMV path; 8: skinny MFMA kernels
-def test_gemma_program_step_matches_module_step(model_type, rows):
+# 1, 3: decode GEMV path; 8: skinny MFMA kernels; 24, 64: decode_gemm / hipBLASLt, with RoPE applied
+# inside the decode attention kernel (the opt-in PENROZ_DECODE_ROPE_IN_ATTN=1) or by the RoPE pass
+@pytest.mark.parametrize("rows,rope_in_attn", [(1, "0"), (3, "0"), (8, "0"), (24, "0"), (24, "1"), (64, "1")])
+def test_gemma_program_step_matches_module_step(monkeypatch, model_type, rows, rope_in_attn):
+    monkeypatch.setenv("PENROZ_DECODE_ROPE_IN_ATTN", rope_in_attn)
     m = _gemma_model(256, model_type)
     cap = 32
     dec = gd.GraphDecoder(m, rows, cap, 0.0, None)
@@ -176,6 +179,8 @@ def test_gemma_program_step_matches_module_step(model_type, rows):
             acts, _ = m(tok, skip_softmax=True)
             ref = acts[-1][:, -1, :].float()
             dec.cache.begin_step()
+            if rope_in_attn == "1":
+                assert dec.cache.rope_attend_ok(rows, 4, 1, 256), "in-kernel RoPE path not taken"
             got = dec.program.forward(tok, dec.cache).float()  # rewrites the same cache slot
         finally:
             dec.cache.graph_mode = False

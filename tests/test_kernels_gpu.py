@@ -895,6 +895,43 @@ def test_decode_attention_fused_append(dtype, int8, D, H, Hkv, S):
     _close(out, ref, 1e-6 if dtype != torch.float16 else 1e-3)
 
 
+@pytest.mark.parametrize("B,H,Hkv,D,S", [(64, 4, 1, 256, 1), (64, 4, 1, 256, 700), (17, 4, 1, 256, 1024),
+                                          (3, 8, 2, 128, 40), (2, 8, 1, 512, 300), (5, 8, 4, 64, 77)])
+def test_decode_attention_rope_in_kernel(B, H, Hkv, D, S):
+    """decode_attention(rope=) rotates q and the appended key itself == RoPE kernel (rope_vec,
+    the eager decode path) on the QKV rows, then the fused-append decode: same cache contents,
+    same output (both round the rotated values to bf16 once)."""
+    from penroz.ops import rope as R
+    torch.manual_seed(S + D + B)
+    cap = 1024
+    assert A.decode_rope_fusable(B, H, Hkv, D, cap, torch.bfloat16)
+    rows = torch.randn(B, 1, (H + 2 * Hkv) * D, device=DEV).bfloat16()
+    inv = 1.0 / (10000.0 ** (torch.arange(0, D, 2, device=DEV, dtype=torch.float32) / D))
+    pos = torch.tensor([S - 1], device=DEV)
+    cos, sin = R.rope_table(inv, 0, 1, DEV, offset_dev=pos)
+    rot = R.apply_rope_qkv(rows, H, Hkv, D, inv, 0, table=(cos, sin))
+    kc = torch.randn(B, Hkv, cap, D, device=DEV).bfloat16()
+    vc = torch.randn(B, Hkv, cap, D, device=DEV).bfloat16()
+    c1, c2 = (kc.clone(), vc.clone()), (kc.clone(), vc.clone())
+    sl = torch.tensor([S], device=DEV)
+
+    def split(r):
+        return (r[:, :, :H * D].view(B, 1, H, D), r[:, :, H * D:(H + Hkv) * D].view(B, 1, Hkv, D),
+                r[:, :, (H + Hkv) * D:].view(B, 1, Hkv, D))
+    q1, k1, v1 = split(rot)
+    ref = A.decode_attention(q1, c1[0], c1[1], cap, seq_len_dev=sl, k_new=k1, v_new=v1)
+    q2, k2, v2 = split(rows)
+    out = A.decode_attention(q2, c2[0], c2[1], cap, seq_len_dev=sl, k_new=k2, v_new=v2,
+                             rope=(cos.view(-1), sin.view(-1)))
+    torch.cuda.synchronize()
+    assert torch.equal(c1[1], c2[1])
+    kd = (c1[0].float() - c2[0].float()).abs()
+    # the appended key: at most one bf16 ulp apart (fma contraction may differ between the kernels)
+    assert kd.max().item() <= 2 ** -7 * c1[0].float().abs().max().item(), kd.max().item()
+    assert torch.equal(c1[0][:, :, :S - 1], c2[0][:, :, :S - 1]) and torch.equal(c1[0][:, :, S:], c2[0][:, :, S:])
+    _close(out, ref, 2e-2)
+
+
 @pytest.mark.parametrize("V,dt", [(50304, torch.bfloat16), (50257, torch.bfloat16), (4096, torch.float32)])
 def test_sample_step_and_advance(V, dt):
     """Graph-decode sampler: token -> idx_out[r] and out_buf[r, *step]; device-hashed uniforms
