@@ -418,7 +418,9 @@ __global__ void __launch_bounds__(256) decode_kernel(const TQ* __restrict__ q, c
 // unrotated and are rotated here (rotate-half pairs d, d + D/2, rope_vec_kernel's arithmetic), so the
 // decode step needs no separate RoPE pass. Column chunk s2 of a lane pairs with chunk s2 + KS/2 of
 // the same lane, so the rotation stays in registers.
-template <int D, int GMAX>  // GMAX: the exact query-group size H / Hkv
+// ROPE is a template flag so the default instantiations compile exactly as without it (as a run-time
+// branch it cost the D = 512 kernels 320 B/lane of scratch).
+template <int D, int GMAX, bool ROPE = false>  // GMAX: the exact query-group size H / Hkv
 __global__ void __launch_bounds__(256) decode_small_kernel(const bf16* __restrict__ q, bf16* __restrict__ kc,
                                                            bf16* __restrict__ vc, bf16* __restrict__ out, int H,
                                                            int Hkv, int cap, int S, float scale,
@@ -479,7 +481,7 @@ __global__ void __launch_bounds__(256) decode_small_kernel(const bf16* __restric
       f[s2 + KS / 2] = uint4{o2[0], o2[1], o2[2], o2[3]};
     }
   };
-  if (rc != nullptr) rotate(qf);
+  if constexpr (ROPE) rotate(qf);
   // keys of this wave
   const int per = ((S + 63) / 64) * 16;  // 16-key blocks, a quarter each
   const int k0 = w * per, k1 = min(S, k0 + per);
@@ -498,7 +500,9 @@ __global__ void __launch_bounds__(256) decode_small_kernel(const bf16* __restric
     const bf16* kr = fresh ? k_new + new_off : kc + (head_base + key) * D;
 #pragma unroll
     for (int s2 = 0; s2 < KS; ++s2) kf[s2] = *reinterpret_cast<const uint4*>(kr + 32 * s2 + 8 * qd);
-    if (rc != nullptr && fresh) rotate(kf);
+    if constexpr (ROPE) {
+      if (fresh) rotate(kf);
+    }
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const int kj = min(kb + j, S - 1);
@@ -523,7 +527,7 @@ __global__ void __launch_bounds__(256) decode_small_kernel(const bf16* __restric
     bf16* kd = kc + (head_base + S - 1) * D;
     bf16* vd = vc + (head_base + S - 1) * D;
     for (int d = 8 * lane; d < D; d += 512) {
-      if (rc != nullptr) {
+      if constexpr (ROPE) {
         constexpr int half = D / 2;
         const int j0 = d < half ? d : d - half;
         float x1[8], x2[8], y[8];
@@ -794,8 +798,8 @@ torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c
                      (!fuse || kv_rs % 8 == 0);
   const bool rope = rope_cos.has_value() && rope_cos->defined();
   if (rope) {
-    TORCH_CHECK(small && fuse, "in-kernel RoPE: the small decode kernel with the fused append only "
-                "(check decode_small_applies first)");
+    TORCH_CHECK(small && fuse && D <= 256, "in-kernel RoPE: the small decode kernel with the fused append, "
+                "head_dim <= 256 only (check decode_small_applies first)");
     for (const auto* t : {&*rope_cos, &*rope_sin})
       TORCH_CHECK(t->is_cuda() && t->scalar_type() == torch::kFloat32 && t->is_contiguous() && t->numel() == D / 2,
                   "rope cos / sin: contiguous fp32 [D/2] (one position)");
@@ -810,9 +814,15 @@ torch::Tensor decode_attn(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, c
     bf16* op = reinterpret_cast<bf16*>(out.data_ptr());
     const bf16* knp = fuse ? reinterpret_cast<const bf16*>(k_new->data_ptr()) : nullptr;
     const bf16* vnp = fuse ? reinterpret_cast<const bf16*>(v_new->data_ptr()) : nullptr;
-#define PENROZ_DSMALL(DD, GG)                                                                                       \
-  hipLaunchKernelGGL((decode_small_kernel<DD, GG>), dim3(B * Hkv), dim3(256), 0, stream, qp, kp, vp, op, H, Hkv, cap, \
-                     (int)S, (float)scale, sdev, q_rs, knp, vnp, kv_rs, rcp, rsp)
+#define PENROZ_DSMALL(DD, GG)                                                                                   \
+  do {                                                                                                            \
+  if (rope && DD <= 256)                                                                                          \
+    hipLaunchKernelGGL((decode_small_kernel<DD, GG, true>), dim3(B * Hkv), dim3(256), 0, stream, qp, kp, vp, op, H, \
+                       Hkv, cap, (int)S, (float)scale, sdev, q_rs, knp, vnp, kv_rs, rcp, rsp);                       \
+  else                                                                                                            \
+    hipLaunchKernelGGL((decode_small_kernel<DD, GG, false>), dim3(B * Hkv), dim3(256), 0, stream, qp, kp, vp, op, H, \
+                       Hkv, cap, (int)S, (float)scale, sdev, q_rs, knp, vnp, kv_rs, nullptr, nullptr);                \
+  } while (0)
 #define PENROZ_DSMALL_G(DD)                      \
   switch (G0) {                                   \
     case 1: PENROZ_DSMALL(DD, 1); break;          \

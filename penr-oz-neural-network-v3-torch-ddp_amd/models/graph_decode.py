@@ -133,7 +133,7 @@ class StaticKVCache(_GraphMode, kvc.KVCache):
     def rope_attend_ok(self, B: int, H: int, Hkv: int, D: int) -> bool:
         """``attend_rope`` applies: opted in (PENROZ_DECODE_ROPE_IN_ATTN=1), graph mode with the
         fused append, the small decode kernel. Off by default: Gemma-3 1B batch 32 / 64 measured
-        2.115 / 2.109 and 2.433 / 2.444 ms/step with it vs 2.103 / 2.099 and 2.434 / 2.439 ms with
+        2.108 / 2.100 and 2.442 / 2.445 ms/step with it vs 2.074 / 2.077 and 2.425 / 2.433 ms with
         the separate RoPE pass (profiles/negative_r6_rope_in_decode_attn.log)."""
         kc = self._k[0]
         return (os.environ.get("PENROZ_DECODE_ROPE_IN_ATTN", "0") == "1" and self.graph_mode and FUSED_APPEND

@@ -220,7 +220,8 @@ def decode_counters(device: torch.device) -> Tensor | None:
 def decode_rope_fusable(B: int, H: int, Hkv: int, D: int, cap: int, cache_dtype: torch.dtype) -> bool:
     """The decode kernel can rotate q and the appended key itself (``decode_attention(rope=)``):
     the one-workgroup-per-(batch, KV head) kernel over a bf16 cache of ``cap`` slots."""
-    return cache_dtype == torch.bfloat16 and D % 16 == 0 and kernels().decode_small_applies(B, 1, H, Hkv, D, cap)
+    return (cache_dtype == torch.bfloat16 and D % 16 == 0 and D <= 256
+            and kernels().decode_small_applies(B, 1, H, Hkv, D, cap))
 
 
 def decode_attention(q: Tensor, k_cache: Tensor, v_cache: Tensor, seq_len: int,

@@ -896,7 +896,7 @@ def test_decode_attention_fused_append(dtype, int8, D, H, Hkv, S):
 
 
 @pytest.mark.parametrize("B,H,Hkv,D,S", [(64, 4, 1, 256, 1), (64, 4, 1, 256, 700), (17, 4, 1, 256, 1024),
-                                          (3, 8, 2, 128, 40), (2, 8, 1, 512, 300), (5, 8, 4, 64, 77)])
+                                          (3, 8, 2, 128, 40), (2, 8, 2, 128, 300), (5, 8, 4, 64, 77)])
 def test_decode_attention_rope_in_kernel(B, H, Hkv, D, S):
     """decode_attention(rope=) rotates q and the appended key itself == RoPE kernel (rope_vec,
     the eager decode path) on the QKV rows, then the fused-append decode: same cache contents,
